@@ -1,0 +1,258 @@
+// qs_device.hpp — device-side data layout and the per-(pod, node) evaluation shared by every
+// gfx950 kernel of libqsched.  Semantics: spec/semantics.md (S4–S7); exactness arguments: S10.
+//
+// Layout in HBM: the node table is a structure of arrays of int32 columns in
+// compacted units (cpu millicores, memory 2^u bytes), plus per-node reciprocals precomputed at
+// load time (RN_f64(1/alloc) for BalancedAllocation, RN_f32(1/alloc) for LeastAllocated) and, for
+// profiles with TaintToleration / NodeAffinity / extended resources, mask and ext columns.
+// Everything here is compiled with -ffp-contract=off: the float64 path must round exactly like
+// Go's float64 (spec S5, kat K7).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+#include <stdint.h>
+
+namespace qs {
+
+constexpr int kWave = 64;
+
+// ---- device node table (SoA, n entries each) ------------------------------------------------
+struct DevTable {
+    int32_t *ac, *am;          // Allocatable cpu (m), memory (2^u B)
+    int32_t *rc, *rm;          // Requested
+    int32_t *zc, *zm;          // NonZeroRequested
+    int32_t *np, *mp;          // pod count, AllowedPodNumber
+    double *yc, *ym;           // RN_f64(1/alloc) (0 where alloc == 0)
+    int32_t *ae0, *re0, *ae1, *re1;  // extended resources (feature bit kFeatExt)
+    uint64_t *th, *ts;         // taint_hard, taint_soft
+    uint64_t *lb0, *lb1;       // label requirement bits
+    uint32_t n;
+};
+
+enum : uint32_t { kFeatTaint = 1u, kFeatAffinity = 2u, kFeatExt = 4u };
+
+// Profile constants resolved on the host.
+struct DevCfg {
+    int32_t wc, wm;              // LeastAllocated resource weights
+    double yd_both, yd_c, yd_m;  // RN_f64(1 / weight sums)
+    int32_t wtt, wna;            // TaintToleration / NodeAffinity plugin weights
+    uint32_t feat;               // kFeat* bits
+    uint32_t ba_skip_be;         // balanced_skip_besteffort
+};
+
+// Pod record (32 B).  w_fit / w_bal already resolved from the pod's QoS class (spec S9).
+struct alignas(16) DPod {
+    int32_t rc, rm, zc, zm;   // Requested / NonZeroRequested cpu, memory (compacted)
+    int32_t re0, re1;         // extended requests
+    uint16_t wfit, wbal;
+    uint32_t flags;           // bits 0-1 qos, 4-6 n_req_terms, 8-10 n_pref_terms
+};
+// Config-4 extension record (176 B), only read when kFeatTaint|kFeatAffinity.
+struct alignas(16) DPodX {
+    uint64_t tol_hard, tol_soft, sel0, sel1;
+    uint64_t req[4][2];
+    uint64_t pref[4][2];
+    int32_t pw[4];
+};
+
+// One node row in registers.
+struct Row {
+    int32_t ac, am, rc, rm, zc, zm, np, mp;
+    double yc, ym;
+};
+struct RowX {
+    int32_t ae0, re0, ae1, re1;
+    uint64_t th, ts, lb0, lb1;
+};
+
+__device__ __forceinline__ Row load_row(const DevTable &t, uint32_t i) {
+    Row r;
+    r.ac = t.ac[i]; r.am = t.am[i]; r.rc = t.rc[i]; r.rm = t.rm[i];
+    r.zc = t.zc[i]; r.zm = t.zm[i]; r.np = t.np[i]; r.mp = t.mp[i];
+    r.yc = t.yc[i]; r.ym = t.ym[i];
+    return r;
+}
+__device__ __forceinline__ Row empty_row() {
+    Row r;
+    r.ac = r.am = r.rc = r.rm = r.zc = r.zm = 0;
+    r.np = 0; r.mp = 0;  // pods + 1 > max_pods -> never feasible
+    r.yc = r.ym = 0.0;
+    return r;
+}
+template <uint32_t F>
+__device__ __forceinline__ RowX load_rowx(const DevTable &t, uint32_t i) {
+    RowX x;
+    x.ae0 = x.re0 = x.ae1 = x.re1 = 0;
+    x.th = x.ts = x.lb0 = x.lb1 = 0;
+    if (F & kFeatExt) { x.ae0 = t.ae0[i]; x.re0 = t.re0[i]; x.ae1 = t.ae1[i]; x.re1 = t.re1[i]; }
+    if (F & kFeatTaint) { x.th = t.th[i]; x.ts = t.ts[i]; }
+    if (F & kFeatAffinity) { x.lb0 = t.lb0[i]; x.lb1 = t.lb1[i]; }
+    return x;
+}
+__device__ __forceinline__ void store_dyn(const DevTable &t, uint32_t i, const Row &r) {
+    t.rc[i] = r.rc; t.rm[i] = r.rm; t.zc[i] = r.zc; t.zm[i] = r.zm; t.np[i] = r.np;
+}
+template <uint32_t F>
+__device__ __forceinline__ void store_dynx(const DevTable &t, uint32_t i, const RowX &x) {
+    if (F & kFeatExt) { t.re0[i] = x.re0; t.re1[i] = x.re1; }
+}
+// Reserve (spec S7; UP framework/types.go#NodeInfo.update(+1))
+__device__ __forceinline__ void reserve(Row &r, RowX &x, const DPod &p, int sign) {
+    r.rc += sign * p.rc; r.rm += sign * p.rm;
+    r.zc += sign * p.zc; r.zm += sign * p.zm;
+    r.np += sign;
+    x.re0 += sign * p.re0; x.re1 += sign * p.re1;
+}
+
+// ---- spec S4: NodeResourcesFit.Filter (UP noderesources/fit.go#fitsRequest) ------------------
+// Per-resource checks are skipped for zero requests, which also covers the all-zero early return.
+template <uint32_t F>
+__device__ __forceinline__ bool fits(const Row &r, const RowX &x, const DPod &p) {
+    bool ok = r.np < r.mp;
+    ok &= (p.rc <= 0) | (p.rc <= r.ac - r.rc);
+    ok &= (p.rm <= 0) | (p.rm <= r.am - r.rm);
+    if (F & kFeatExt) {
+        ok &= (p.re0 == 0) | (p.re0 <= x.ae0 - x.re0);
+        ok &= (p.re1 == 0) | (p.re1 <= x.ae1 - x.re1);
+    }
+    return ok;
+}
+__device__ __forceinline__ bool subset128(uint64_t m0, uint64_t m1, uint64_t b0, uint64_t b1) {
+    return ((m0 & ~b0) | (m1 & ~b1)) == 0;
+}
+template <uint32_t F>
+__device__ __forceinline__ bool feasible(const Row &r, const RowX &x, const DPod &p, const DPodX &px) {
+    bool ok = fits<F>(r, x, p);
+    if (F & kFeatTaint) ok &= (x.th & ~px.tol_hard) == 0;  // UP tainttoleration#Filter
+    if (F & kFeatAffinity) {                                 // UP nodeaffinity#Filter
+        ok &= subset128(px.sel0, px.sel1, x.lb0, x.lb1);
+        const uint32_t nt = (p.flags >> 4) & 7u;
+        bool any = nt == 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k)
+            any |= (k < nt) & subset128(px.req[k][0], px.req[k][1], x.lb0, x.lb1);
+        ok &= any;
+    }
+    return ok;
+}
+// raw TaintToleration score: intolerable PreferNoSchedule taints (UP tainttoleration#Score)
+__device__ __forceinline__ uint32_t taint_raw(const RowX &x, const DPodX &px) {
+    return (uint32_t)__popcll(x.ts & ~px.tol_soft);
+}
+// raw NodeAffinity score: weights of matching preferred terms (UP nodeaffinity#Score)
+__device__ __forceinline__ uint32_t affinity_raw(const RowX &x, const DPod &p, const DPodX &px) {
+    const uint32_t nt = (p.flags >> 8) & 7u;
+    uint32_t s = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k)
+        s += ((k < nt) & subset128(px.pref[k][0], px.pref[k][1], x.lb0, x.lb1)) ? (uint32_t)px.pw[k] : 0u;
+    return s;
+}
+
+// ---- exact small divisions (spec S10) -------------------------------------------------------
+// floor(n / d) for n < 2^32, 1 <= d < 2^29 and n / d <= ~1000, given y = RN_f64(1/d):
+// n*y is within 2^-52 relative of n/d, whose fractional part is 0 or in [1/d, 1 - 1/d]; a 2^-30
+// bias lifts exact integers clear of the truncation edge and can never carry a fraction over it.
+__device__ __forceinline__ uint32_t floor_div(uint32_t n, double y) {
+    return (uint32_t)__builtin_fma((double)n, y, 0x1p-30);
+}
+// UP least_allocated.go#leastRequestedScore: ((a - reqd) * 100) / a, 0 if reqd > a (a >= 0)
+__device__ __forceinline__ uint32_t least_requested(int32_t a, int32_t reqd, double ya) {
+    const int32_t rq = reqd < a ? reqd : a;                       // keep the discarded branch in range
+    const uint32_t n = __umul24((uint32_t)(a - rq), 100u);        // a < 2^24 (compaction limit)
+    const uint32_t q = floor_div(n, ya);
+    return reqd > a ? 0u : q;
+}
+// min(RN(r / a), 1) for a > 0, r >= 0 — Markstein quotient, exact here (spec S10)
+__device__ __forceinline__ double fraction(int32_t a, int32_t r, double y) {
+    const double R = (double)r, A = (double)a;
+    const double q0 = R * y;
+    const double rem = __builtin_fma(-q0, A, R);
+    const double q = __builtin_fma(rem, y, q0);
+    return r >= a ? 1.0 : q;
+}
+
+// ---- spec S5/S6: QoS-weighted total of one feasible node ------------------------------------
+template <uint32_t F>
+__device__ __forceinline__ uint32_t node_total(const Row &r, const RowX &x, const DPod &p,
+                                               const DPodX &px, const DevCfg &c, uint32_t mt,
+                                               double ymt, uint32_t ma, double yma, uint32_t *sc) {
+    // LeastAllocated (UP least_allocated.go#leastResourceScorer), NonZeroRequested + pod nz.
+    // Branch-free: a resource with alloc == 0 contributes weight 0 (its score is 0 as well).
+    const bool hc = r.ac != 0, hm = r.am != 0;
+    const uint32_t sc_c = least_requested(r.ac, r.zc + p.zc, r.yc);
+    const uint32_t sc_m = least_requested(r.am, r.zm + p.zm, r.ym);
+    const uint32_t wce = hc ? (uint32_t)c.wc : 0u, wme = hm ? (uint32_t)c.wm : 0u;
+    const uint32_t num = __umul24(sc_c, wce) + __umul24(sc_m, wme);
+    const uint32_t den = wce + wme;
+    const double yd = (hc & hm) ? c.yd_both : (hc ? c.yd_c : c.yd_m);
+    const uint32_t la = den ? floor_div(num, yd) : 0u;
+    // BalancedAllocation (UP balanced_allocation.go#balancedResourceScorer), Requested + pod req
+    const double f0 = fraction(r.ac, r.rc + p.rc, r.yc);
+    const double f1 = fraction(r.am, r.rm + p.rm, r.ym);
+    double sd = 0.0;
+    if (hc & hm) sd = __builtin_fabs((f0 - f1) / 2);
+    const double scaled = (1 - sd) * 100.0;
+    uint32_t ba = (uint32_t)(int32_t)scaled;  // int64() truncation toward zero
+    if (c.ba_skip_be && (p.flags & 3u) == 0) ba = 0;
+    uint32_t total = __umul24((uint32_t)p.wfit, la) + __umul24((uint32_t)p.wbal, ba);
+    uint32_t tt = 0, na = 0;
+    if (F & kFeatTaint) {  // reverse DefaultNormalizeScore (UP helper/normalize_score.go)
+        const uint32_t raw = taint_raw(x, px);
+        tt = mt == 0 ? 100u : 100u - floor_div(100u * raw, ymt);
+        total += __umul24((uint32_t)c.wtt, tt);
+    }
+    if (F & kFeatAffinity) {
+        const uint32_t raw = affinity_raw(x, p, px);
+        na = ma == 0 ? raw : floor_div(100u * raw, yma);
+        total += __umul24((uint32_t)c.wna, na);
+    }
+    if (sc) { sc[0] = la; sc[1] = ba; sc[2] = tt; sc[3] = na; }
+    return total;
+}
+
+// spec S7 packed key: ((total + 1) << 32) | (0xFFFFFFFF - idx); 0 = infeasible
+__device__ __forceinline__ uint64_t pack_key(uint32_t tv, uint32_t idx) {
+    return ((uint64_t)tv << 32) | (uint64_t)(0xFFFFFFFFu - idx);
+}
+__device__ __forceinline__ uint32_t key_node(uint64_t k) { return 0xFFFFFFFFu - (uint32_t)k; }
+
+// ---- 64-lane reductions with DPP (no LDS round trip) -----------------------------------------
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ uint32_t dpp32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, ROW_MASK, 0xF, false);
+}
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ uint64_t dpp_max64(uint64_t v) {
+    const uint32_t lo = dpp32<CTRL, ROW_MASK>((uint32_t)v);
+    const uint32_t hi = dpp32<CTRL, ROW_MASK>((uint32_t)(v >> 32));
+    const uint64_t o = ((uint64_t)hi << 32) | lo;
+    return o > v ? o : v;
+}
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ uint32_t dpp_max32(uint32_t v) {
+    const uint32_t o = dpp32<CTRL, ROW_MASK>(v);
+    return o > v ? o : v;
+}
+// Full-wave max; every lane must be active.  Result is wave-uniform.
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+    v = dpp_max32<0xB1>(v);        // quad_perm [1,0,3,2]
+    v = dpp_max32<0x4E>(v);        // quad_perm [2,3,0,1]
+    v = dpp_max32<0x141>(v);       // row_half_mirror
+    v = dpp_max32<0x140>(v);       // row_mirror: each row of 16 holds its max
+    v = dpp_max32<0x142, 0xA>(v);  // row_bcast:15 into rows 1, 3
+    v = dpp_max32<0x143, 0xC>(v);  // row_bcast:31 into rows 2, 3
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+// Max of packed keys as two 32-bit reductions: the score half first, then the index half among
+// the lanes holding that score (keys are unique, so this is the u64 max).
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+    const uint32_t hi = wave_max_u32((uint32_t)(v >> 32));
+    const uint32_t lo = wave_max_u32((uint32_t)(v >> 32) == hi ? (uint32_t)v : 0u);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// RN_f64(1/d) of a per-pod normalize maximum (IEEE division; once per pod, off the node loop).
+__device__ __forceinline__ double rcp_exact(uint32_t d) { return d ? 1.0 / (double)d : 0.0; }
+
+}  // namespace qs

@@ -1,0 +1,876 @@
+// qs_host.cpp — libqsched host runtime: the C ABI of include/qsched.h over the gfx950 kernels.
+//
+// Responsibilities:
+//  * authoritative int64 host mirror of the node table (UP framework/types.go#NodeInfo) with
+//    per-row generations (qs_node_upsert diff), rebuilt onto the device on demand;
+//  * compaction to the device layout (spec S10): memory in units of 2^u bytes, int32 columns,
+//    per-node reciprocals RN_f64(1/alloc), RN_f32(1/alloc);
+//  * pod precompute (spec S2/S3/S8/S9): QoSSort order, per-QoS weights, compact pod records;
+//  * engine dispatch (persistent / scan / lookahead) on one HIP stream per context;
+//  * error handling: every entry point catches everything and returns a qs_status.
+#include "../../include/qsched.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <exception>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "qs_device.hpp"
+#include "qs_launch.hpp"
+
+using namespace qs;
+
+namespace {
+
+constexpr int64_t kLimit = (1LL << 24) - 1;  // 24-bit multiplier range of the kernels (spec S10)
+
+struct QsError {
+    qs_status st;
+    std::string msg;
+};
+
+#define HIPCHK(x)                                                                          \
+    do {                                                                                   \
+        hipError_t e_ = (x);                                                               \
+        if (e_ != hipSuccess)                                                              \
+            throw QsError{QS_EDEVICE, std::string(#x) + ": " + hipGetErrorString(e_)};     \
+    } while (0)
+
+static void fail(qs_status st, const std::string &m) { throw QsError{st, m}; }
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+    void ensure(size_t b) {
+        if (b <= bytes) return;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        HIPCHK(hipMalloc(&p, b));
+        bytes = b;
+    }
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+    template <class T>
+    T *as() const { return (T *)p; }
+};
+
+// Host mirror of the canonical table.
+struct Mirror {
+    uint32_t n = 0;
+    std::vector<int64_t> ac, am, mp, rc, rm, zc, zm, np;
+    std::vector<int64_t> ae, re;  // [n][QS_MAX_EXT]
+    std::vector<uint64_t> th, ts, lb;  // lb [n][2]
+    std::vector<uint64_t> gen;
+    void resize(uint32_t nn) {
+        n = nn;
+        for (auto *v : {&ac, &am, &mp, &rc, &rm, &zc, &zm, &np}) v->assign(nn, 0);
+        ae.assign((size_t)nn * QS_MAX_EXT, 0);
+        re.assign((size_t)nn * QS_MAX_EXT, 0);
+        th.assign(nn, 0);
+        ts.assign(nn, 0);
+        lb.assign((size_t)nn * 2, 0);
+        gen.assign(nn, 0);
+    }
+};
+
+static int ctz64(int64_t v) { return v == 0 ? 64 : __builtin_ctzll((uint64_t)v); }
+
+}  // namespace
+
+struct qs_stream {
+    uint32_t p = 0;
+    uint32_t feat = 0;  // kFeat* bits of this stream (profile + extended resources in use)
+    std::vector<qs_pod> pods;      // canonical, arrival order
+    std::vector<uint32_t> order;   // stream position -> arrival index
+    DevBuf d_pods, d_podx, d_node, d_key, d_stamp;
+    bool ran = false;
+    int shift = 0;
+};
+
+struct qs_ctx {
+    std::mutex mu;
+    qs_config cfg{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    Mirror m;
+    int shift = 20;  // memory unit 2^shift bytes on the device
+    bool dev_valid = false;
+    DevTable dt{};
+    DevCfg dc{};
+    DevBuf tbl;  // all columns in one allocation
+    DevBuf tbl_saved;  // qs_table_save snapshot (whole allocation)
+    bool saved = false;
+    bool mirror_stale = false;  // device ran a stream since the last mirror sync
+    DevBuf diag;
+    DevBuf scratch, lists, one_pod, one_podx, out_feas, out_score, out_total;
+    uint32_t cap = 0;
+    // sharding (qs_open_shard)
+    int rank = 0, world = 1;
+};
+
+namespace {
+
+uint32_t feat_of(const qs_config &c) {
+    uint32_t f = 0;
+    if (c.enable_taint) f |= kFeatTaint;
+    if (c.enable_affinity) f |= kFeatAffinity;
+    return f;
+}
+
+void check_cfg(const qs_config &c) {
+    if (c.abi_version != QS_ABI_VERSION) fail(QS_EINVAL, "qs_config.abi_version mismatch");
+    if (c.fit_weight_cpu < 0 || c.fit_weight_mem < 0 || c.fit_weight_cpu > 65535 ||
+        c.fit_weight_mem > 65535)
+        fail(QS_EINVAL, "fit weights out of range");
+    int64_t wmax = 0;
+    for (int q = 0; q < 3; q++) {
+        if (c.w_fit[q] < 0 || c.w_bal[q] < 0 || c.w_fit[q] > 65535 || c.w_bal[q] > 65535)
+            fail(QS_EINVAL, "plugin weights must be in [0, 65535]");
+        wmax = std::max<int64_t>(wmax, (int64_t)c.w_fit[q] + c.w_bal[q]);
+    }
+    if (c.w_taint < 0 || c.w_affinity < 0 || c.w_taint > 65535 || c.w_affinity > 65535)
+        fail(QS_EINVAL, "plugin weights must be in [0, 65535]");
+    // total + 1 must fit the 32-bit score half of the packed key (spec S6/S7)
+    const int64_t tmax = 100 * (wmax + (c.enable_taint ? c.w_taint : 0) +
+                                (c.enable_affinity ? c.w_affinity : 0));
+    if (tmax >= 0x7FFFFFFF) fail(QS_EINVAL, "weighted total would overflow the packed key");
+}
+
+DevCfg make_devcfg(const qs_config &c) {
+    DevCfg d{};
+    d.wc = (int32_t)c.fit_weight_cpu;
+    d.wm = (int32_t)c.fit_weight_mem;
+    auto rcp = [](int64_t v) { return v > 0 ? 1.0 / (double)v : 0.0; };  // RN_f64(1/v)
+    d.yd_both = rcp(c.fit_weight_cpu + c.fit_weight_mem);
+    d.yd_c = rcp(c.fit_weight_cpu);
+    d.yd_m = rcp(c.fit_weight_mem);
+    d.wtt = c.w_taint;
+    d.wna = c.w_affinity;
+    d.feat = feat_of(c);
+    d.ba_skip_be = c.balanced_skip_besteffort ? 1u : 0u;
+    return d;
+}
+
+// memory unit shift for the table (<= 20, the MiB granularity of every k8s "Mi"/"Gi" quantity)
+int table_shift(const Mirror &m) {
+    int s = 20;
+    for (uint32_t i = 0; i < m.n; i++) {
+        s = std::min(s, ctz64(m.am[i]));
+        s = std::min(s, ctz64(m.rm[i]));
+        s = std::min(s, ctz64(m.zm[i]));
+    }
+    return s;
+}
+
+void check_range(int64_t v, const char *what, uint32_t i) {
+    if (v < 0 || v > kLimit)
+        fail(QS_EINVAL, std::string("node ") + std::to_string(i) + ": " + what +
+                            " outside the device range [0, 2^24) after compaction");
+}
+
+HostRow compact_row(const Mirror &m, uint32_t i, int shift) {
+    HostRow r{};
+    check_range(m.ac[i], "alloc_cpu", i);
+    check_range(m.rc[i], "req_cpu", i);
+    check_range(m.zc[i], "nz_cpu", i);
+    check_range(m.am[i] >> shift, "alloc_mem", i);
+    check_range(m.rm[i] >> shift, "req_mem", i);
+    check_range(m.zm[i] >> shift, "nz_mem", i);
+    check_range(m.np[i], "pods", i);
+    check_range(m.mp[i], "max_pods", i);
+    r.ac = (int32_t)m.ac[i];
+    r.am = (int32_t)(m.am[i] >> shift);
+    r.rc = (int32_t)m.rc[i];
+    r.rm = (int32_t)(m.rm[i] >> shift);
+    r.zc = (int32_t)m.zc[i];
+    r.zm = (int32_t)(m.zm[i] >> shift);
+    r.np = (int32_t)m.np[i];
+    r.mp = (int32_t)m.mp[i];
+    r.yc = r.ac ? 1.0 / (double)r.ac : 0.0;  // RN(1/alloc): IEEE division on the host
+    r.ym = r.am ? 1.0 / (double)r.am : 0.0;
+    for (int k = 0; k < QS_MAX_EXT; k++) {
+        check_range(m.ae[(size_t)i * QS_MAX_EXT + k], "alloc_ext", i);
+        check_range(m.re[(size_t)i * QS_MAX_EXT + k], "req_ext", i);
+    }
+    r.ae0 = (int32_t)m.ae[(size_t)i * QS_MAX_EXT + 0];
+    r.ae1 = (int32_t)m.ae[(size_t)i * QS_MAX_EXT + 1];
+    r.re0 = (int32_t)m.re[(size_t)i * QS_MAX_EXT + 0];
+    r.re1 = (int32_t)m.re[(size_t)i * QS_MAX_EXT + 1];
+    r.th = m.th[i];
+    r.ts = m.ts[i];
+    r.lb0 = m.lb[(size_t)i * 2];
+    r.lb1 = m.lb[(size_t)i * 2 + 1];
+    return r;
+}
+
+// Column layout inside ctx->tbl: 256-byte aligned columns of cap entries.  Returns the size;
+// assigns the column pointers when base != nullptr.
+size_t carve(DevTable &t, uint32_t cap, char *base) {
+    size_t off = 0;
+    auto col = [&](size_t elem) {
+        char *p = base ? base + off : nullptr;
+        off += ((size_t)cap * elem + 255) & ~(size_t)255;
+        return (void *)p;
+    };
+    t.ac = (int32_t *)col(4); t.am = (int32_t *)col(4); t.rc = (int32_t *)col(4);
+    t.rm = (int32_t *)col(4); t.zc = (int32_t *)col(4); t.zm = (int32_t *)col(4);
+    t.np = (int32_t *)col(4); t.mp = (int32_t *)col(4);
+    t.yc = (double *)col(8); t.ym = (double *)col(8);
+    t.ae0 = (int32_t *)col(4); t.re0 = (int32_t *)col(4); t.ae1 = (int32_t *)col(4);
+    t.re1 = (int32_t *)col(4);
+    t.th = (uint64_t *)col(8); t.ts = (uint64_t *)col(8);
+    t.lb0 = (uint64_t *)col(8); t.lb1 = (uint64_t *)col(8);
+    return off;
+}
+
+// Upload the whole mirror (compacted) to the device.
+void upload_table(qs_ctx *c) {
+    const uint32_t n = c->m.n;
+    const uint32_t cap = std::max<uint32_t>(64, (n + 63) & ~63u);
+    if (cap > c->cap || !c->tbl.p) {
+        c->tbl.ensure(carve(c->dt, cap, nullptr));
+        c->cap = cap;
+    }
+    carve(c->dt, c->cap, c->tbl.as<char>());
+    c->dt.n = n;
+    std::vector<double> yc(n), ym(n);
+    std::vector<int32_t> ac(n), am(n), rc(n), rm(n), zc(n), zm(n), np(n), mp(n), ae0(n), re0(n),
+        ae1(n), re1(n);
+    std::vector<uint64_t> th(n), ts(n), lb0(n), lb1(n);
+    for (uint32_t i = 0; i < n; i++) {
+        const HostRow r = compact_row(c->m, i, c->shift);
+        ac[i] = r.ac; am[i] = r.am; rc[i] = r.rc; rm[i] = r.rm; zc[i] = r.zc; zm[i] = r.zm;
+        np[i] = r.np; mp[i] = r.mp; yc[i] = r.yc; ym[i] = r.ym;
+        ae0[i] = r.ae0; re0[i] = r.re0; ae1[i] = r.ae1; re1[i] = r.re1;
+        th[i] = r.th; ts[i] = r.ts; lb0[i] = r.lb0; lb1[i] = r.lb1;
+    }
+    const DevTable &t = c->dt;
+    auto up = [&](void *dst, const void *src, size_t b) {
+        if (b) HIPCHK(hipMemcpyAsync(dst, src, b, hipMemcpyHostToDevice, c->stream));
+    };
+    up(t.ac, ac.data(), 4 * n); up(t.am, am.data(), 4 * n); up(t.rc, rc.data(), 4 * n);
+    up(t.rm, rm.data(), 4 * n); up(t.zc, zc.data(), 4 * n); up(t.zm, zm.data(), 4 * n);
+    up(t.np, np.data(), 4 * n); up(t.mp, mp.data(), 4 * n);
+    up(t.yc, yc.data(), 8 * n); up(t.ym, ym.data(), 8 * n);
+    up(t.ae0, ae0.data(), 4 * n); up(t.re0, re0.data(), 4 * n);
+    up(t.ae1, ae1.data(), 4 * n); up(t.re1, re1.data(), 4 * n);
+    up(t.th, th.data(), 8 * n); up(t.ts, ts.data(), 8 * n);
+    up(t.lb0, lb0.data(), 8 * n); up(t.lb1, lb1.data(), 8 * n);
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->dev_valid = true;
+}
+
+void push_row(qs_ctx *c, uint32_t i) {
+    if (!c->dev_valid) return;
+    const HostRow r = compact_row(c->m, i, c->shift);
+    hipLaunchKernelGGL(k_set_row, dim3(1), dim3(1), 0, c->stream, c->dt, i, r,
+                       kFeatExt | kFeatTaint | kFeatAffinity);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->stream));
+}
+
+// Refresh the dynamic mirror columns from the device after stream runs (values are multiples of
+// 2^shift by construction, so decompaction is exact).
+void sync_mirror(qs_ctx *c) {
+    if (!c->mirror_stale || !c->dev_valid) return;
+    const uint32_t n = c->m.n;
+    std::vector<int32_t> rc(n), rm(n), zc(n), zm(n), np(n), re0(n), re1(n);
+    const DevTable &t = c->dt;
+    auto dn = [&](void *dst, const void *src, size_t b) {
+        if (b) HIPCHK(hipMemcpyAsync(dst, src, b, hipMemcpyDeviceToHost, c->stream));
+    };
+    dn(rc.data(), t.rc, 4 * n); dn(rm.data(), t.rm, 4 * n); dn(zc.data(), t.zc, 4 * n);
+    dn(zm.data(), t.zm, 4 * n); dn(np.data(), t.np, 4 * n); dn(re0.data(), t.re0, 4 * n);
+    dn(re1.data(), t.re1, 4 * n);
+    HIPCHK(hipStreamSynchronize(c->stream));
+    Mirror &m = c->m;
+    for (uint32_t i = 0; i < n; i++) {
+        m.rc[i] = rc[i];
+        m.rm[i] = (int64_t)rm[i] << c->shift;
+        m.zc[i] = zc[i];
+        m.zm[i] = (int64_t)zm[i] << c->shift;
+        m.np[i] = np[i];
+        m.re[(size_t)i * QS_MAX_EXT] = re0[i];
+        m.re[(size_t)i * QS_MAX_EXT + 1] = re1[i];
+    }
+    c->mirror_stale = false;
+}
+
+int pod_min_shift(const qs_pod &p) { return std::min(ctz64(p.req_mem), ctz64(p.nz_mem)); }
+
+void check_pod(const qs_pod &p, uint32_t j) {
+    auto bad = [&](const char *w) {
+        fail(QS_EINVAL, std::string("pod ") + std::to_string(j) + ": " + w);
+    };
+    if (p.qos < 0 || p.qos > 2) bad("qos must be 0..2");
+    if (p.req_cpu < 0 || p.req_mem < 0 || p.nz_cpu < 0 || p.nz_mem < 0) bad("negative request");
+    for (int k = 0; k < QS_MAX_EXT; k++)
+        if (p.req_ext[k] < 0 || p.req_ext[k] > kLimit) bad("req_ext out of range");
+    if (p.req_cpu > kLimit || p.nz_cpu > kLimit) bad("cpu request out of range");
+    if (p.n_req_terms < 0 || p.n_req_terms > QS_MAX_TERMS || p.n_pref_terms < 0 ||
+        p.n_pref_terms > QS_MAX_TERMS)
+        bad("term count out of range");
+    for (int t = 0; t < p.n_pref_terms; t++)
+        if (p.pref_weight[t] < 0 || p.pref_weight[t] > 100) bad("preferred term weight must be 0..100");
+}
+
+DPod compact_pod(const qs_ctx *c, const qs_pod &p, uint32_t j, int shift) {
+    check_pod(p, j);
+    if ((p.req_mem >> shift) > kLimit || (p.nz_mem >> shift) > kLimit)
+        fail(QS_EINVAL, "pod " + std::to_string(j) + ": memory request out of the device range");
+    DPod d{};
+    d.rc = (int32_t)p.req_cpu;
+    d.rm = (int32_t)(p.req_mem >> shift);
+    d.zc = (int32_t)p.nz_cpu;
+    d.zm = (int32_t)(p.nz_mem >> shift);
+    d.re0 = (int32_t)p.req_ext[0];
+    d.re1 = (int32_t)p.req_ext[1];
+    d.wfit = (uint16_t)c->cfg.w_fit[p.qos];
+    d.wbal = (uint16_t)c->cfg.w_bal[p.qos];
+    d.flags = (uint32_t)p.qos | ((uint32_t)p.n_req_terms << 4) | ((uint32_t)p.n_pref_terms << 8);
+    return d;
+}
+
+DPodX compact_podx(const qs_pod &p) {
+    DPodX x{};
+    x.tol_hard = p.tol_hard;
+    x.tol_soft = p.tol_soft;
+    x.sel0 = p.sel[0];
+    x.sel1 = p.sel[1];
+    for (int t = 0; t < QS_MAX_TERMS; t++) {
+        x.req[t][0] = p.req_terms[t][0];
+        x.req[t][1] = p.req_terms[t][1];
+        x.pref[t][0] = p.pref_terms[t][0];
+        x.pref[t][1] = p.pref_terms[t][1];
+        x.pw[t] = p.pref_weight[t];
+    }
+    return x;
+}
+
+// spec S8 QoSSort: stable by (qos desc, priority desc, arrival asc)
+std::vector<uint32_t> qos_order(const qs_pod *pods, uint32_t p, bool sort) {
+    std::vector<uint32_t> o(p);
+    for (uint32_t j = 0; j < p; j++) o[j] = j;
+    if (sort)
+        std::stable_sort(o.begin(), o.end(), [&](uint32_t a, uint32_t b) {
+            if (pods[a].qos != pods[b].qos) return pods[a].qos > pods[b].qos;
+            return pods[a].priority > pods[b].priority;
+        });
+    return o;
+}
+
+void mirror_reserve(Mirror &m, uint32_t i, const qs_pod &p, int sign) {
+    m.rc[i] += sign * p.req_cpu;
+    m.rm[i] += sign * p.req_mem;
+    for (int k = 0; k < QS_MAX_EXT; k++) m.re[(size_t)i * QS_MAX_EXT + k] += sign * p.req_ext[k];
+    m.zc[i] += sign * p.nz_cpu;
+    m.zm[i] += sign * p.nz_mem;
+    m.np[i] += sign;
+}
+
+void ensure_shift(qs_ctx *c, int want) {
+    if (want < c->shift) {
+        sync_mirror(c);  // a finer memory unit is needed: recompact from the mirror
+        c->shift = want;
+        c->dev_valid = false;
+    }
+    if (!c->dev_valid) upload_table(c);
+}
+
+template <class F>
+qs_status guarded(qs_ctx *c, F &&f) {
+    if (!c) return QS_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    try {
+        f();
+        c->err.clear();
+        return QS_OK;
+    } catch (const QsError &e) {
+        c->err = e.msg;
+        return e.st;
+    } catch (const std::bad_alloc &) {
+        c->err = "out of host memory";
+        return QS_ENOMEM;
+    } catch (const std::exception &e) {
+        c->err = e.what();
+        return QS_EINVAL;
+    } catch (...) {
+        c->err = "unknown error";
+        return QS_EINVAL;
+    }
+}
+
+int pick_engine(const qs_ctx *c, uint32_t n) {
+    int e = c->cfg.engine;
+    const uint32_t feat = c->dc.feat;
+    if (e == QS_ENGINE_AUTO) {
+        if (!(feat & (kFeatTaint | kFeatAffinity)) && n > 0) e = QS_ENGINE_LOOKAHEAD;
+        else if (n <= persistent_max_nodes(feat)) e = QS_ENGINE_PERSISTENT;
+        else e = QS_ENGINE_SCAN;
+    }
+    if (e == QS_ENGINE_PERSISTENT && n > persistent_max_nodes(feat))
+        fail(QS_EINVAL, "PERSISTENT engine supports at most " +
+                            std::to_string(persistent_max_nodes(feat)) + " nodes for this profile");
+    if (e == QS_ENGINE_LOOKAHEAD && (feat & (kFeatTaint | kFeatAffinity)))
+        fail(QS_EINVAL, "LOOKAHEAD engine does not support TaintToleration/NodeAffinity yet");
+    return e;
+}
+
+uint32_t la_window(const qs_ctx *c) {
+    int K = c->cfg.lookahead > 0 ? c->cfg.lookahead : 64;
+    return (uint32_t)std::min(64, std::max(1, K));
+}
+
+void percentile_stats(const std::vector<uint64_t> &st, qs_stats *s) {
+    if (st.size() < 2) return;
+    std::vector<double> d(st.size() - 1);
+    for (size_t i = 1; i < st.size(); i++) d[i - 1] = (double)(st[i] - st[i - 1]) * 0.01;  // 100 MHz
+    std::sort(d.begin(), d.end());
+    auto pct = [&](double q) { return d[std::min(d.size() - 1, (size_t)(q * (double)(d.size() - 1) + 0.5))]; };
+    s->p50_cycle_us = pct(0.50);
+    s->p99_cycle_us = pct(0.99);
+    s->max_cycle_us = d.back();
+}
+
+}  // namespace
+
+// =============================================================================================
+// C ABI
+// =============================================================================================
+extern "C" {
+
+const char *qs_version(void) { return "qsched 0.1 (gfx950)"; }
+
+void qs_config_default(qs_config *cfg) {
+    if (!cfg) return;
+    std::memset(cfg, 0, sizeof(*cfg));
+    cfg->abi_version = QS_ABI_VERSION;
+    cfg->engine = QS_ENGINE_AUTO;
+    cfg->fit_weight_cpu = 1;
+    cfg->fit_weight_mem = 1;
+    const int32_t wf[3] = {1, 2, 3}, wb[3] = {1, 1, 1};  // spec S9
+    for (int q = 0; q < 3; q++) { cfg->w_fit[q] = wf[q]; cfg->w_bal[q] = wb[q]; }
+    cfg->w_taint = 3;     // UP apis/config/v1/default_plugins.go TaintToleration weight
+    cfg->w_affinity = 2;  // NodeAffinity weight
+    cfg->qos_sort = 1;
+}
+
+qs_status qs_open(const qs_config *cfg, int device, qs_ctx **out) {
+    if (!cfg || !out) return QS_EINVAL;
+    *out = nullptr;
+    qs_ctx *c = new (std::nothrow) qs_ctx();
+    if (!c) return QS_ENOMEM;
+    try {
+        check_cfg(*cfg);
+        c->cfg = *cfg;
+        c->device = device;
+        int ndev = 0;
+        HIPCHK(hipGetDeviceCount(&ndev));
+        if (device < 0 || device >= ndev) fail(QS_EINVAL, "no such device");
+        HIPCHK(hipSetDevice(device));
+        HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        c->dc = make_devcfg(c->cfg);
+        c->scratch.ensure(scan_scratch_bytes());
+        HIPCHK(hipMemset(c->scratch.p, 0, scan_scratch_bytes()));
+    } catch (const QsError &e) {
+        delete c;
+        return e.st;
+    } catch (...) {
+        delete c;
+        return QS_EDEVICE;
+    }
+    *out = c;
+    return QS_OK;
+}
+
+qs_status qs_close(qs_ctx *c) {
+    if (!c) return QS_EINVAL;
+    {
+        std::lock_guard<std::mutex> lk(c->mu);
+        (void)hipSetDevice(c->device);
+        if (c->stream) (void)hipStreamSynchronize(c->stream);
+    }
+    hipStream_t s = c->stream;
+    delete c;  // DevBuf destructors free device memory
+    if (s) (void)hipStreamDestroy(s);
+    return QS_OK;
+}
+
+const char *qs_last_error(const qs_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+qs_status qs_nodes_load(qs_ctx *c, const qs_node_soa *nd, uint32_t n) {
+    return guarded(c, [&] {
+        if (!nd || !nd->alloc_cpu || !nd->alloc_mem) fail(QS_EINVAL, "alloc_cpu/alloc_mem required");
+        HIPCHK(hipSetDevice(c->device));
+        Mirror &m = c->m;
+        m.resize(n);
+        auto get = [](const int64_t *a, size_t i, int64_t d) { return a ? a[i] : d; };
+        for (uint32_t i = 0; i < n; i++) {
+            m.ac[i] = nd->alloc_cpu[i];
+            m.am[i] = nd->alloc_mem[i];
+            m.mp[i] = get(nd->max_pods, i, 110);
+            m.rc[i] = get(nd->req_cpu, i, 0);
+            m.rm[i] = get(nd->req_mem, i, 0);
+            m.zc[i] = get(nd->nz_cpu, i, 0);
+            m.zm[i] = get(nd->nz_mem, i, 0);
+            m.np[i] = get(nd->pods, i, 0);
+            for (int k = 0; k < QS_MAX_EXT; k++) {
+                m.ae[(size_t)i * QS_MAX_EXT + k] = get(nd->alloc_ext, (size_t)i * QS_MAX_EXT + k, 0);
+                m.re[(size_t)i * QS_MAX_EXT + k] = get(nd->req_ext, (size_t)i * QS_MAX_EXT + k, 0);
+            }
+            m.th[i] = nd->taint_hard ? nd->taint_hard[i] : 0;
+            m.ts[i] = nd->taint_soft ? nd->taint_soft[i] : 0;
+            m.lb[2 * (size_t)i] = nd->label_bits ? nd->label_bits[2 * (size_t)i] : 0;
+            m.lb[2 * (size_t)i + 1] = nd->label_bits ? nd->label_bits[2 * (size_t)i + 1] : 0;
+        }
+        c->shift = table_shift(m);
+        c->dev_valid = false;
+        c->saved = false;
+        c->mirror_stale = false;
+        upload_table(c);
+    });
+}
+
+qs_status qs_nodes_read(qs_ctx *c, const qs_node_soa_out *o, uint32_t n) {
+    return guarded(c, [&] {
+        if (!o) fail(QS_EINVAL, "null output");
+        if (n != c->m.n) fail(QS_EINVAL, "n does not match the loaded table");
+        sync_mirror(c);
+        const Mirror &m = c->m;
+        auto put = [](int64_t *d, const std::vector<int64_t> &s) {
+            if (d) std::memcpy(d, s.data(), s.size() * 8);
+        };
+        put(o->alloc_cpu, m.ac); put(o->alloc_mem, m.am); put(o->max_pods, m.mp);
+        put(o->req_cpu, m.rc); put(o->req_mem, m.rm); put(o->nz_cpu, m.zc); put(o->nz_mem, m.zm);
+        put(o->pods, m.np); put(o->alloc_ext, m.ae); put(o->req_ext, m.re);
+        if (o->taint_hard) std::memcpy(o->taint_hard, m.th.data(), 8 * (size_t)n);
+        if (o->taint_soft) std::memcpy(o->taint_soft, m.ts.data(), 8 * (size_t)n);
+        if (o->label_bits) std::memcpy(o->label_bits, m.lb.data(), 16 * (size_t)n);
+    });
+}
+
+qs_status qs_node_upsert(qs_ctx *c, uint32_t idx, const qs_node_row *r, uint64_t generation) {
+    return guarded(c, [&] {
+        if (!r) fail(QS_EINVAL, "null row");
+        HIPCHK(hipSetDevice(c->device));
+        sync_mirror(c);
+        Mirror &m = c->m;
+        if (idx > m.n) fail(QS_EINVAL, "idx beyond table end (append only at idx == n)");
+        if (idx == m.n) {  // append one node
+            Mirror old = m;
+            m.resize(old.n + 1);
+            auto cp = [&](std::vector<int64_t> &d, const std::vector<int64_t> &s) { std::copy(s.begin(), s.end(), d.begin()); };
+            cp(m.ac, old.ac); cp(m.am, old.am); cp(m.mp, old.mp); cp(m.rc, old.rc); cp(m.rm, old.rm);
+            cp(m.zc, old.zc); cp(m.zm, old.zm); cp(m.np, old.np); cp(m.ae, old.ae); cp(m.re, old.re);
+            std::copy(old.th.begin(), old.th.end(), m.th.begin());
+            std::copy(old.ts.begin(), old.ts.end(), m.ts.begin());
+            std::copy(old.lb.begin(), old.lb.end(), m.lb.begin());
+            std::copy(old.gen.begin(), old.gen.end(), m.gen.begin());
+            c->dev_valid = false;
+        } else if (generation != 0 && generation <= m.gen[idx]) {
+            return;  // already applied (UP NodeInfo.Generation diff)
+        }
+        m.ac[idx] = r->alloc_cpu; m.am[idx] = r->alloc_mem; m.mp[idx] = r->max_pods;
+        m.rc[idx] = r->req_cpu; m.rm[idx] = r->req_mem; m.zc[idx] = r->nz_cpu; m.zm[idx] = r->nz_mem;
+        m.np[idx] = r->pods;
+        for (int k = 0; k < QS_MAX_EXT; k++) {
+            m.ae[(size_t)idx * QS_MAX_EXT + k] = r->alloc_ext[k];
+            m.re[(size_t)idx * QS_MAX_EXT + k] = r->req_ext[k];
+        }
+        m.th[idx] = r->taint_hard; m.ts[idx] = r->taint_soft;
+        m.lb[2 * (size_t)idx] = r->label_bits[0]; m.lb[2 * (size_t)idx + 1] = r->label_bits[1];
+        m.gen[idx] = generation;
+        const int want = std::min({ctz64(r->alloc_mem), ctz64(r->req_mem), ctz64(r->nz_mem)});
+        if (want < c->shift) { c->shift = want; c->dev_valid = false; }
+        if (!c->dev_valid) upload_table(c);
+        else push_row(c, idx);
+    });
+}
+
+static qs_status reserve_impl(qs_ctx *c, uint32_t node, const qs_pod *p, int sign) {
+    return guarded(c, [&] {
+        if (!p) fail(QS_EINVAL, "null pod");
+        if (node >= c->m.n) fail(QS_EINVAL, "node index out of range");
+        check_pod(*p, 0);
+        HIPCHK(hipSetDevice(c->device));
+        sync_mirror(c);
+        mirror_reserve(c->m, node, *p, sign);
+        ensure_shift(c, pod_min_shift(*p));
+        push_row(c, node);
+    });
+}
+qs_status qs_reserve(qs_ctx *c, uint32_t node, const qs_pod *p) { return reserve_impl(c, node, p, +1); }
+qs_status qs_unreserve(qs_ctx *c, uint32_t node, const qs_pod *p) { return reserve_impl(c, node, p, -1); }
+
+qs_status qs_score_pod(qs_ctx *c, const qs_pod *pod, uint8_t *feas, int32_t *score, int32_t *total,
+                       int32_t *best) {
+    return guarded(c, [&] {
+        if (!pod) fail(QS_EINVAL, "null pod");
+        HIPCHK(hipSetDevice(c->device));
+        const uint32_t n = c->m.n;
+        ensure_shift(c, pod_min_shift(*pod));
+        const DPod dp = compact_pod(c, *pod, 0, c->shift);
+        const DPodX dx = compact_podx(*pod);
+        c->dc.feat = feat_of(c->cfg) | ((pod->req_ext[0] || pod->req_ext[1]) ? kFeatExt : 0u);
+        c->one_pod.ensure(sizeof(DPod));
+        c->one_podx.ensure(sizeof(DPodX));
+        c->out_feas.ensure(std::max<size_t>(n, 1));
+        c->out_score.ensure(std::max<size_t>(16 * (size_t)n, 16));
+        c->out_total.ensure(std::max<size_t>(4 * (size_t)n, 4));
+        HIPCHK(hipMemcpyAsync(c->one_pod.p, &dp, sizeof dp, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(c->one_podx.p, &dx, sizeof dx, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemsetAsync(c->scratch.p, 0, scan_scratch_bytes(), c->stream));
+        if (n) {
+            HIPCHK(launch_scan_pod(c->dt, c->one_pod.as<DPod>(), c->one_podx.as<DPodX>(), 0, c->dc,
+                                   c->scratch.p, nullptr, nullptr, nullptr, c->out_feas.as<uint8_t>(),
+                                   c->out_score.as<int32_t>(), c->out_total.as<int32_t>(), false,
+                                   c->stream));
+        }
+        unsigned long long kbest = 0;
+        HIPCHK(hipMemcpyAsync(&kbest, c->scratch.p, 8, hipMemcpyDeviceToHost, c->stream));
+        if (feas && n) HIPCHK(hipMemcpyAsync(feas, c->out_feas.p, n, hipMemcpyDeviceToHost, c->stream));
+        if (score && n) HIPCHK(hipMemcpyAsync(score, c->out_score.p, 16 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+        if (total && n) HIPCHK(hipMemcpyAsync(total, c->out_total.p, 4 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (best) *best = kbest ? (int32_t)(0xFFFFFFFFu - (uint32_t)kbest) : -1;
+    });
+}
+
+qs_status qs_stream_prepare(qs_ctx *c, const qs_pod *pods, uint32_t p, qs_stream **out) {
+    if (!out) return QS_EINVAL;
+    *out = nullptr;
+    qs_stream *s = nullptr;
+    qs_status st = guarded(c, [&] {
+        if (p && !pods) fail(QS_EINVAL, "null pods");
+        HIPCHK(hipSetDevice(c->device));
+        s = new qs_stream();
+        s->p = p;
+        s->pods.assign(pods, pods + p);
+        int want = c->shift;
+        for (uint32_t j = 0; j < p; j++) {
+            check_pod(pods[j], j);
+            want = std::min(want, pod_min_shift(pods[j]));
+        }
+        ensure_shift(c, want);
+        s->shift = c->shift;
+        s->feat = feat_of(c->cfg);
+        for (uint32_t j = 0; j < p; j++)
+            if (pods[j].req_ext[0] || pods[j].req_ext[1]) { s->feat |= kFeatExt; break; }
+        s->order = qos_order(pods, p, c->cfg.qos_sort != 0);
+        std::vector<DPod> dp(std::max<uint32_t>(p, 1));
+        const bool needx = feat_of(c->cfg) & (kFeatTaint | kFeatAffinity);
+        std::vector<DPodX> dx(needx ? std::max<uint32_t>(p, 1) : 1);
+        for (uint32_t k = 0; k < p; k++) {
+            const uint32_t j = s->order[k];
+            dp[k] = compact_pod(c, pods[j], j, c->shift);
+            if (needx) dx[k] = compact_podx(pods[j]);
+        }
+        const size_t P1 = std::max<uint32_t>(p, 1);
+        s->d_pods.ensure(sizeof(DPod) * P1);
+        s->d_podx.ensure(sizeof(DPodX) * dx.size());
+        s->d_node.ensure(4 * P1);
+        s->d_key.ensure(8 * P1);
+        if (c->cfg.record_timestamps) s->d_stamp.ensure(8 * P1);
+        HIPCHK(hipMemcpyAsync(s->d_pods.p, dp.data(), sizeof(DPod) * p, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(s->d_podx.p, dx.data(), sizeof(DPodX) * dx.size(), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+    });
+    if (st != QS_OK) {
+        delete s;
+        return st;
+    }
+    *out = s;
+    return QS_OK;
+}
+
+qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) {
+    return guarded(c, [&] {
+        if (!s) fail(QS_EINVAL, "null stream");
+        if (mode != QS_MODE_EXACT) fail(QS_EINVAL, "only QS_MODE_EXACT is implemented");
+        if (s->shift != c->shift || !c->dev_valid) fail(QS_ESTATE, "node table recompacted after prepare");
+        HIPCHK(hipSetDevice(c->device));
+        const uint32_t n = c->m.n, P = s->p;
+        c->dc.feat = s->feat;
+        const int eng = pick_engine(c, n);
+        int32_t *on = s->d_node.as<int32_t>();
+        uint64_t *ok = s->d_key.as<uint64_t>();
+        uint64_t *st = c->cfg.record_timestamps ? s->d_stamp.as<uint64_t>() : nullptr;
+        uint64_t batches = 0;
+        hipEvent_t e0, e1;
+        HIPCHK(hipEventCreate(&e0));
+        HIPCHK(hipEventCreate(&e1));
+        HIPCHK(hipEventRecord(e0, c->stream));
+        if (P > 0 && n == 0) {
+            HIPCHK(hipMemsetAsync(on, 0xFF, 4 * (size_t)P, c->stream));
+            HIPCHK(hipMemsetAsync(ok, 0, 8 * (size_t)P, c->stream));
+        } else if (P > 0) {
+            const DPod *dp = s->d_pods.as<DPod>();
+            const DPodX *dx = s->d_podx.as<DPodX>();
+            if (eng == QS_ENGINE_PERSISTENT) {
+                HIPCHK(launch_persistent(c->dt, dp, dx, P, c->dc, on, ok, st, c->stream));
+                batches = 1;
+            } else if (eng == QS_ENGINE_SCAN) {
+                HIPCHK(hipMemsetAsync(c->scratch.p, 0, scan_scratch_bytes(), c->stream));
+                for (uint32_t k = 0; k < P; k++)
+                    HIPCHK(launch_scan_pod(c->dt, dp, dx, k, c->dc, c->scratch.p, on, ok, st,
+                                           nullptr, nullptr, nullptr, true, c->stream));
+                batches = P;
+            } else {
+                const LaGeom geo = la_geometry(n, la_window(c));
+                if (geo.G == 0) fail(QS_EINVAL, "no lookahead geometry for this table size");
+                const size_t lbytes = 8ull * geo.K * 64 * geo.epl;
+                c->lists.ensure(lbytes);
+                HIPCHK(hipMemsetAsync(c->lists.p, 0, lbytes, c->stream));  // padding entries stay 0
+                // QS_DIAG=1: diagnostic resolver with per-segment shader-clock stamps (stderr)
+                static const bool diag_on = getenv("QS_DIAG") && getenv("QS_DIAG")[0] == '1';
+                uint64_t *diag = nullptr;
+                if (diag_on) {
+                    c->diag.ensure(64);
+                    HIPCHK(hipMemsetAsync(c->diag.p, 0, 64, c->stream));
+                    diag = c->diag.as<uint64_t>();
+                }
+                for (uint32_t s0 = 0; s0 < P; s0 += geo.K) {
+                    HIPCHK(launch_la_window(c->dt, dp, s0, P, c->dc, geo, c->lists.as<uint64_t>(), on,
+                                            ok, st, diag, c->stream));
+                    ++batches;
+                }
+                if (diag_on) {
+                    uint64_t h[8] = {0};
+                    HIPCHK(hipMemcpyAsync(h, diag, 48, hipMemcpyDeviceToHost, c->stream));
+                    HIPCHK(hipStreamSynchronize(c->stream));
+                    const double np = h[5] ? (double)h[5] : 1.0;
+                    fprintf(stderr, "QS_DIAG resolve cycles/pod: cand %.0f issue %.0f fresh %.0f wmax %.0f commit %.0f (pods %llu, G=%u E=%u epl=%u)\n",
+                            h[0] / np, h[1] / np, h[2] / np, h[3] / np, h[4] / np,
+                            (unsigned long long)h[5], geo.G, geo.E, geo.epl);
+                }
+            }
+        }
+        HIPCHK(hipEventRecord(e1, c->stream));
+        HIPCHK(hipEventSynchronize(e1));
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        s->ran = true;
+        c->mirror_stale = true;
+        if (stats) {
+            std::memset(stats, 0, sizeof(*stats));
+            stats->pods = P;
+            stats->evals = (uint64_t)P * n;
+            stats->wall_s = ms * 1e-3;
+            stats->batches = batches;
+            stats->engine_used = eng;
+        }
+    });
+}
+
+qs_status qs_stream_results(qs_ctx *c, qs_stream *s, int32_t *placement, uint64_t *best_key) {
+    return guarded(c, [&] {
+        if (!s || !s->ran) fail(QS_ESTATE, "stream has not run");
+        HIPCHK(hipSetDevice(c->device));
+        const uint32_t P = s->p;
+        std::vector<int32_t> node(P);
+        std::vector<uint64_t> key(P);
+        if (P) {
+            HIPCHK(hipMemcpyAsync(node.data(), s->d_node.p, 4 * (size_t)P, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipMemcpyAsync(key.data(), s->d_key.p, 8 * (size_t)P, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+        }
+        for (uint32_t k = 0; k < P; k++) {
+            const uint32_t j = s->order[k];
+            if (placement) placement[j] = node[k];
+            if (best_key) best_key[j] = key[k];
+        }
+    });
+}
+
+qs_status qs_stream_free(qs_ctx *c, qs_stream *s) {
+    (void)c;
+    delete s;
+    return QS_OK;
+}
+
+qs_status qs_table_save(qs_ctx *c) {
+    return guarded(c, [&] {
+        if (!c->dev_valid) fail(QS_ESTATE, "no node table loaded");
+        HIPCHK(hipSetDevice(c->device));
+        c->tbl_saved.ensure(c->tbl.bytes);
+        HIPCHK(hipMemcpyAsync(c->tbl_saved.p, c->tbl.p, c->tbl.bytes, hipMemcpyDeviceToDevice, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        c->saved = true;
+    });
+}
+
+qs_status qs_table_restore(qs_ctx *c) {
+    return guarded(c, [&] {
+        if (!c->saved || !c->dev_valid || c->tbl_saved.bytes != c->tbl.bytes)
+            fail(QS_ESTATE, "no matching qs_table_save snapshot");
+        HIPCHK(hipSetDevice(c->device));
+        HIPCHK(hipMemcpyAsync(c->tbl.p, c->tbl_saved.p, c->tbl.bytes, hipMemcpyDeviceToDevice, c->stream));
+        c->mirror_stale = true;  // mirror re-reads the restored rows on demand
+    });
+}
+
+qs_status qs_schedule_stream(qs_ctx *c, const qs_pod *pods, uint32_t p, qs_mode mode,
+                             int32_t *placement, qs_stats *stats) {
+    using clk = std::chrono::steady_clock;
+    auto t0 = clk::now();
+    qs_stream *s = nullptr;
+    qs_status st = qs_stream_prepare(c, pods, p, &s);
+    if (st != QS_OK) return st;
+    auto t1 = clk::now();
+    qs_stats local{};
+    st = qs_stream_run(c, s, mode, &local);
+    if (st != QS_OK) { qs_stream_free(nullptr, s); return st; }
+    auto t2 = clk::now();
+    st = qs_stream_results(c, s, placement, nullptr);
+    if (st == QS_OK && c->cfg.record_timestamps && p > 1) {
+        std::vector<uint64_t> stamps(p);
+        if (hipMemcpy(stamps.data(), s->d_stamp.p, 8 * (size_t)p, hipMemcpyDeviceToHost) == hipSuccess)
+            percentile_stats(stamps, &local);
+    }
+    auto t3 = clk::now();
+    for (uint32_t j = 0; j < p && st == QS_OK; j++) {
+        if (placement[j] >= 0) local.placed++;
+        else local.unschedulable++;
+    }
+    qs_status st2 = qs_stream_free(c, s);
+    if (st == QS_OK) st = st2;
+    local.h2d_s = std::chrono::duration<double>(t1 - t0).count();
+    local.d2h_s = std::chrono::duration<double>(t3 - t2).count();
+    if (stats) *stats = local;
+    return st;
+}
+
+size_t qs_struct_size(int which) {
+    switch (which) {
+        case 0: return sizeof(qs_config);
+        case 1: return sizeof(qs_node_soa);
+        case 2: return sizeof(qs_node_row);
+        case 3: return sizeof(qs_pod);
+        case 4: return sizeof(qs_container);
+        case 5: return sizeof(qs_stats);
+        default: return 0;
+    }
+}
+
+qs_status qs_stream_stamps(qs_ctx *c, qs_stream *s, uint64_t *stamps) {
+    return guarded(c, [&] {
+        if (!s || !s->ran || !s->d_stamp.p) fail(QS_ESTATE, "no timestamps recorded");
+        HIPCHK(hipMemcpy(stamps, s->d_stamp.p, 8 * (size_t)s->p, hipMemcpyDeviceToHost));
+    });
+}
+
+}  // extern "C"

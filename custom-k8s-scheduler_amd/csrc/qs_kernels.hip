@@ -1,0 +1,616 @@
+// qs_kernels.hip — gfx950 kernels of the exact per-pod scheduling cycle (spec/semantics.md S4–S7).
+//
+// Engines (all bit-exact with the oracle):
+//   PERSISTENT  k_persistent: ONE resident workgroup runs the whole pod stream; node rows live in
+//               VGPRs (NPT rows per lane), Filter+Score in registers, DPP wave argmax, one LDS
+//               exchange + one barrier per pod, Reserve applied by the owning lane.  N <= 8192.
+//   SCAN        k_scan_norm / k_scan_key / k_scan_commit: per-pod grid scan over the HBM table with
+//               u64 atomicMax of packed keys, then a 1-thread commit that applies Reserve.  Any N.
+//   LOOKAHEAD   k_la_select + k_la_resolve: exact top-K lookahead.  For a window of K pods the
+//               whole chip scores all K×N (pod, node) pairs against the window-start table and
+//               keeps, per pod and node-chunk, the top-L keys (L = K).  One wave then resolves the
+//               window sequentially: pod i's winner is the max of (fresh keys of the <= i nodes
+//               modified earlier in the window) and (the best stale key of an unmodified node,
+//               which is always inside the top-L lists).  Bit-exact; SURVEY.md §7 H4 option 3.
+#include <algorithm>
+
+#include "qs_device.hpp"
+#include "qs_launch.hpp"
+
+namespace qs {
+
+constexpr uint32_t kFeatNorm = kFeatTaint | kFeatAffinity;
+
+// =============================================================================================
+// PERSISTENT engine
+// =============================================================================================
+template <int NPT, int BS, uint32_t F>
+__global__ __launch_bounds__(BS) void k_persistent(DevTable t, const DPod *__restrict__ pods,
+                                                   const DPodX *__restrict__ podx, uint32_t P,
+                                                   DevCfg c, int32_t *__restrict__ out_node,
+                                                   uint64_t *__restrict__ out_key,
+                                                   uint64_t *__restrict__ stamps) {
+    constexpr int NW = BS / kWave;
+    __shared__ uint64_t red[2][NW];
+    __shared__ uint32_t redn[2][2][NW];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint32_t n = t.n;
+    Row r[NPT];
+    RowX x[NPT];
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+        const uint32_t idx = tid + k * BS;
+        if (idx < n) { r[k] = load_row(t, idx); x[k] = load_rowx<F>(t, idx); }
+        else { r[k] = empty_row(); x[k] = RowX{0, 0, 0, 0, 0, 0, 0, 0}; }
+    }
+    DPod pn = pods[0];
+    for (uint32_t s = 0; s < P; ++s) {
+        const DPod p = pn;
+        pn = pods[s + 1 < P ? s + 1 : s];  // prefetch the next pod record (scalar loads)
+        DPodX px;
+        if (F & kFeatNorm) px = podx[s];
+        uint32_t mt = 0, ma = 0;
+        double ymt = 0.0, yma = 0.0;
+        if (F & kFeatNorm) {  // NormalizeScore maxima over feasible nodes (spec S5)
+            uint32_t lt = 0, la = 0;
+#pragma unroll
+            for (int k = 0; k < NPT; ++k) {
+                const bool f = feasible<F>(r[k], x[k], p, px);
+                const uint32_t a = f ? taint_raw(x[k], px) : 0u;
+                const uint32_t b = f ? affinity_raw(x[k], p, px) : 0u;
+                lt = a > lt ? a : lt;
+                la = b > la ? b : la;
+            }
+            lt = wave_max_u32(lt);
+            la = wave_max_u32(la);
+            if (lane == 0) { redn[s & 1][0][w] = lt; redn[s & 1][1][w] = la; }
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < NW; ++i) {
+                const uint32_t a = redn[s & 1][0][i], b = redn[s & 1][1][i];
+                mt = a > mt ? a : mt;
+                ma = b > ma ? b : ma;
+            }
+            ymt = rcp_exact(mt);
+            yma = rcp_exact(ma);
+        }
+        uint64_t best = 0;
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+            const bool f = feasible<F>(r[k], x[k], p, px);
+            const uint32_t tot = node_total<F>(r[k], x[k], p, px, c, mt, ymt, ma, yma, nullptr);
+            const uint64_t key = f ? pack_key(tot + 1, tid + k * BS) : 0ull;
+            best = key > best ? key : best;
+        }
+        best = wave_max_u64(best);
+        if (lane == 0) red[s & 1][w] = best;
+        __syncthreads();
+        uint64_t ks = 0;
+#pragma unroll
+        for (int i = 0; i < NW; ++i) {
+            const uint64_t v = red[s & 1][i];
+            ks = v > ks ? v : ks;
+        }
+        const uint32_t win = key_node(ks);
+        if (ks != 0) {
+#pragma unroll
+            for (int k = 0; k < NPT; ++k)
+                if (tid + k * BS == win) reserve(r[k], x[k], p, +1);
+        }
+        if (tid == 0) {
+            out_node[s] = ks ? (int32_t)win : -1;
+            if (out_key) out_key[s] = ks;
+            if (stamps) stamps[s] = __builtin_amdgcn_s_memrealtime();
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+        const uint32_t idx = tid + k * BS;
+        if (idx < n) { store_dyn(t, idx, r[k]); store_dynx<F>(t, idx, x[k]); }
+    }
+}
+
+// =============================================================================================
+// SCAN engine (and qs_score_pod)
+// =============================================================================================
+struct ScanScratch {
+    unsigned long long best;
+    uint32_t mt, ma;
+};
+
+template <uint32_t F>
+__global__ __launch_bounds__(256) void k_scan_norm(DevTable t, const DPod *__restrict__ pods,
+                                                   const DPodX *__restrict__ podx, uint32_t s,
+                                                   ScanScratch *sc) {
+    const DPod p = pods[s];
+    const DPodX px = podx[s];
+    uint32_t lt = 0, la = 0;
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < t.n; i += gridDim.x * 256) {
+        const Row r = load_row(t, i);
+        const RowX x = load_rowx<F>(t, i);
+        if (feasible<F>(r, x, p, px)) {
+            const uint32_t a = taint_raw(x, px), b = affinity_raw(x, p, px);
+            lt = a > lt ? a : lt;
+            la = b > la ? b : la;
+        }
+    }
+    lt = wave_max_u32(lt);
+    la = wave_max_u32(la);
+    if ((threadIdx.x & 63) == 0) {
+        if (lt) atomicMax(&sc->mt, lt);
+        if (la) atomicMax(&sc->ma, la);
+    }
+}
+
+// Keys for every node; optionally per-node outputs for qs_score_pod.
+template <uint32_t F>
+__global__ __launch_bounds__(256) void k_scan_key(DevTable t, const DPod *__restrict__ pods,
+                                                  const DPodX *__restrict__ podx, uint32_t s,
+                                                  DevCfg c, ScanScratch *sc, uint8_t *feas_out,
+                                                  int32_t *score_out, int32_t *total_out) {
+    const DPod p = pods[s];
+    DPodX px;
+    uint32_t mt = 0, ma = 0;
+    if (F & kFeatNorm) { px = podx[s]; mt = sc->mt; ma = sc->ma; }
+    const double ymt = rcp_exact(mt), yma = rcp_exact(ma);
+    uint64_t best = 0;
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < t.n; i += gridDim.x * 256) {
+        const Row r = load_row(t, i);
+        const RowX x = load_rowx<F>(t, i);
+        const bool f = feasible<F>(r, x, p, px);
+        uint32_t sco[4];
+        const uint32_t tot = node_total<F>(r, x, p, px, c, mt, ymt, ma, yma, score_out ? sco : nullptr);
+        const uint64_t key = f ? pack_key(tot + 1, i) : 0ull;
+        best = key > best ? key : best;
+        if (feas_out) feas_out[i] = f;
+        if (total_out) total_out[i] = f ? (int32_t)tot : -1;
+        if (score_out) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) score_out[4 * (size_t)i + q] = f ? (int32_t)sco[q] : 0;
+        }
+    }
+    best = wave_max_u64(best);
+    if ((threadIdx.x & 63) == 0 && best) atomicMax(&sc->best, (unsigned long long)best);
+}
+
+// Decode the winner, apply Reserve to the HBM row, emit outputs, reset the scratch.
+template <uint32_t F>
+__global__ void k_scan_commit(DevTable t, const DPod *__restrict__ pods, uint32_t s, ScanScratch *sc,
+                              int32_t *out_node, uint64_t *out_key, uint64_t *stamps) {
+    const uint64_t ks = sc->best;
+    const DPod p = pods[s];
+    if (ks) {
+        const uint32_t w = key_node(ks);
+        Row r = load_row(t, w);
+        RowX x = load_rowx<F>(t, w);
+        reserve(r, x, p, +1);
+        store_dyn(t, w, r);
+        store_dynx<F>(t, w, x);
+    }
+    out_node[s] = ks ? (int32_t)key_node(ks) : -1;
+    if (out_key) out_key[s] = ks;
+    if (stamps) stamps[s] = __builtin_amdgcn_s_memrealtime();
+    sc->best = 0;
+    sc->mt = 0;
+    sc->ma = 0;
+}
+
+// =============================================================================================
+// LOOKAHEAD engine
+// =============================================================================================
+// Block-wide sum of a wave-uniform per-wave value (one barrier; parity-buffered LDS).
+template <int NW>
+__device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t (*buf)[NW], int &par, int lane,
+                                              int w) {
+    if (lane == 0) buf[par][w] = v;
+    __syncthreads();
+    uint32_t s = 0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) s += buf[par][i];
+    par ^= 1;
+    return s;
+}
+
+// Grid: K pods × G node-chunks.  Block (k, g) scores pod s0+k on chunk g and writes the top-L
+// keys of that chunk (lowest node index first among equal totals) to lists[(k*G+g)*L ...].
+// Wave w owns the contiguous sub-range [start + w*E*64, start + (w+1)*E*64), so node-index order
+// is (wave, j, lane) order and tie ranks come from ballots + one cross-wave prefix.
+template <int BS, int E, uint32_t F>
+__global__ __launch_bounds__(BS) void k_la_select(DevTable t, const DPod *__restrict__ pods,
+                                                  DevCfg c, uint32_t s0, uint32_t P, uint32_t G,
+                                                  uint32_t L, uint32_t chunk, uint32_t GLp,
+                                                  uint64_t *__restrict__ lists) {
+    constexpr int NW = BS / kWave;
+    __shared__ uint32_t cnt[2][NW];
+    __shared__ uint32_t slot_ctr;
+    const uint32_t k = blockIdx.x / G, g = blockIdx.x % G;
+    const uint32_t s = s0 + k;
+    if (s >= P) return;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const DPod p = pods[s];
+    const DPodX px{};
+    const uint32_t start = g * chunk;
+    const uint32_t end = min(t.n, start + chunk);
+    const uint32_t base = start + (uint32_t)w * E * kWave + lane;
+    uint32_t tv[E];
+    uint32_t lmax = 0;
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+        const uint32_t idx = base + j * kWave;
+        tv[j] = 0;
+        if (idx < end) {
+            const Row r = load_row(t, idx);
+            const RowX x = load_rowx<F>(t, idx);
+            const bool f = feasible<F>(r, x, p, px);
+            const uint32_t tot = node_total<F>(r, x, p, px, c, 0, 0.0, 0, 0.0, nullptr);
+            tv[j] = f ? tot + 1 : 0;
+        }
+        lmax = tv[j] > lmax ? tv[j] : lmax;
+    }
+    int par = 0;
+    if (tid == 0) slot_ctr = 0;
+    // block max of tv (reuse the sum buffer: a max of wave maxima)
+    const uint32_t wmax = wave_max_u32(lmax);
+    if (lane == 0) cnt[par][w] = wmax;
+    __syncthreads();
+    uint32_t maxtv = 0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) maxtv = cnt[par][i] > maxtv ? cnt[par][i] : maxtv;
+    par ^= 1;
+    auto count_ge = [&](uint32_t thr) -> uint32_t {
+        uint32_t cw = 0;
+#pragma unroll
+        for (int j = 0; j < E; ++j) cw += (uint32_t)__popcll(__ballot(tv[j] >= thr));
+        return block_sum<NW>(cw, cnt, par, lane, w);
+    };
+    // T = largest threshold with count(tv >= T) >= L, or 1 if fewer than L feasible nodes.
+    uint32_t T = 1;
+    if (maxtv > 0) {
+        const uint32_t call = count_ge(1);
+        if (call > L) {
+            if (count_ge(maxtv) >= L) {
+                T = maxtv;
+            } else {
+                uint32_t lo = 1, hi = maxtv;  // count(>=lo) >= L > count(>=hi)
+                while (hi - lo > 1) {
+                    const uint32_t mid = lo + (hi - lo) / 2;
+                    if (count_ge(mid) >= L) lo = mid; else hi = mid;
+                }
+                T = lo;
+            }
+        }
+    }
+    const uint32_t c_gt = count_ge(T + 1);  // < L (or all feasible when fewer than L)
+    const uint32_t need = L > c_gt ? L - c_gt : 0;
+    // ties at T, lowest index first: rank = (ties in earlier waves) + (earlier j) + mbcnt
+    uint64_t tb[E];
+    uint32_t tie_w = 0;
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+        tb[j] = __ballot(tv[j] == T && maxtv > 0);
+        tie_w += (uint32_t)__popcll(tb[j]);
+    }
+    if (lane == 0) cnt[par][w] = tie_w;
+    __syncthreads();
+    uint32_t rank = 0, ties_total = 0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+        const uint32_t v = cnt[par][i];
+        rank += i < w ? v : 0u;
+        ties_total += v;
+    }
+    uint64_t *out = lists + (size_t)k * GLp + (size_t)g * L;
+    const uint64_t lane_mask_lt = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+        const uint32_t idx = base + j * kWave;
+        if (tv[j] > T) {
+            const uint32_t sl = atomicAdd(&slot_ctr, 1u);
+            out[sl] = pack_key(tv[j], idx);
+        } else if ((tb[j] >> lane) & 1ull) {
+            const uint32_t rk = rank + (uint32_t)__popcll(tb[j] & lane_mask_lt);
+            if (rk < need) out[c_gt + rk] = pack_key(tv[j], idx);
+        }
+        rank += (uint32_t)__popcll(tb[j]);
+    }
+    const uint32_t written = c_gt + (ties_total < need ? ties_total : need);
+    for (uint32_t i = written + tid; i < L; i += BS) out[i] = 0;
+}
+
+// One wave resolves the window sequentially (spec S7 order).  Dirty (modified-in-window) node
+// rows live in the lanes' registers (slot = lane); a dynamic-LDS bitmap marks dirty nodes.
+// Per pod, off the critical path: the window's pod records sit one per lane (read by readlane),
+// the next pod's list entries are prefetched, and every lane prefetches the row of its best clean
+// candidate so that a newly dirtied winner's row is already in a register when the argmax lands.
+// Results are kept one per lane (lane i = pod i) and stored once per window.
+// Diagnostic build only (DIAG = true, QS_DIAG=1 at run time): shader-clock stamps per segment.
+__device__ __forceinline__ uint64_t diag_stamp() {
+    uint64_t t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define QS_STAMP(k)                                  \
+    if (DIAG) {                                      \
+        const uint64_t t_ = diag_stamp();            \
+        dsum[k] += t_ - tprev;                       \
+        tprev = t_;                                  \
+    }
+
+template <uint32_t F, int EPL, bool DIAG>
+__global__ __launch_bounds__(64) void k_la_resolve(DevTable t, const DPod *__restrict__ pods,
+                                                   DevCfg c, uint32_t s0, uint32_t P, uint32_t K,
+                                                   uint32_t GLp, const uint64_t *__restrict__ lists,
+                                                   int32_t *__restrict__ out_node,
+                                                   uint64_t *__restrict__ out_key,
+                                                   uint64_t *__restrict__ stamps,
+                                                   uint64_t *__restrict__ diag) {
+    uint64_t dsum[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t tprev = 0;
+    extern __shared__ __attribute__((aligned(16))) uint32_t dirty[];
+    const int lane = threadIdx.x;
+    const uint32_t nwords = (t.n + 31) / 32;
+    for (uint32_t i = lane; i < nwords; i += 64) dirty[i] = 0;
+    const uint32_t kend = min(K, P - s0);
+    // staging area for a newly dirtied row (after the bitmap; 16-byte aligned)
+    Row *stage = (Row *)(dirty + ((nwords + 3) & ~3u));
+    RowX *stagex = (RowX *)(stage + 1);
+    DPod pn = pods[s0];  // uniform: scalar loads, prefetched one pod ahead
+    const DPodX px{};
+    Row dr = empty_row();
+    RowX dx{};
+    uint32_t didx = 0xFFFFFFFFu;
+    uint32_t nd = 0;
+    uint64_t res_key = 0, res_stamp = 0;
+    uint64_t ent[EPL];
+#pragma unroll
+    for (int m = 0; m < EPL; ++m) ent[m] = lists[lane + 64 * m];
+    __syncthreads();
+    if (DIAG) tprev = diag_stamp();
+    for (uint32_t i = 0; i < kend; ++i) {
+        const DPod p = pn;
+        if (i + 1 < kend) pn = pods[s0 + i + 1];
+        // best clean stale candidate of this lane: all bitmap reads issued together
+        uint32_t word[EPL];
+#pragma unroll
+        for (int m = 0; m < EPL; ++m) {
+            const uint32_t nidx = ent[m] ? key_node(ent[m]) : 0u;
+            word[m] = dirty[nidx >> 5] >> (nidx & 31);
+        }
+        uint64_t cand = 0;
+#pragma unroll
+        for (int m = 0; m < EPL; ++m) {
+            const uint64_t e = (word[m] & 1u) ? 0ull : ent[m];
+            cand = e > cand ? e : cand;
+        }
+        QS_STAMP(0)
+        // prefetch the candidate's row (used only if it wins) and the next pod's entries
+        const uint32_t cidx = cand ? key_node(cand) : 0u;
+        const Row crow = load_row(t, cidx);
+        const RowX cx = load_rowx<F>(t, cidx);
+        if (i + 1 < kend) {
+            const uint64_t *nl = lists + (size_t)(i + 1) * GLp;
+#pragma unroll
+            for (int m = 0; m < EPL; ++m) ent[m] = nl[lane + 64 * m];
+        }
+        QS_STAMP(1)
+        // fresh keys of the dirty slots
+        const bool f = feasible<F>(dr, dx, p, px);
+        const uint32_t tot = node_total<F>(dr, dx, p, px, c, 0, 0.0, 0, 0.0, nullptr);
+        const uint64_t fk = ((uint32_t)lane < nd && f) ? pack_key(tot + 1, didx) : 0ull;
+        const uint64_t best = fk > cand ? fk : cand;
+        QS_STAMP(2)
+        const uint64_t ks = wave_max_u64(best);
+        QS_STAMP(3)
+        if (ks) {
+            const uint32_t win = key_node(ks);
+            const bool own = (uint32_t)lane < nd && didx == win;
+            if (__ballot(own)) {
+                if (own) reserve(dr, dx, p, +1);
+            } else {
+                // the winner is a clean node: its row was prefetched by the lane whose cand == ks;
+                // hand it to slot lane nd through LDS (same wave: LDS operations stay in order)
+                const int src = (int)__builtin_ctzll(__ballot(cand == ks));
+                if (lane == src) { *stage = crow; if (F & kFeatExt) *stagex = cx; }
+                const Row nr = *stage;
+                RowX nx{};
+                if (F & kFeatExt) nx = *stagex;
+                if ((uint32_t)lane == nd) {
+                    dr = nr;
+                    dx = nx;
+                    reserve(dr, dx, p, +1);
+                    didx = win;
+                    dirty[win >> 5] |= 1u << (win & 31);
+                }
+                ++nd;
+            }
+        }
+        QS_STAMP(4)
+        if ((uint32_t)lane == i) {
+            res_key = ks;
+            if (stamps) res_stamp = __builtin_amdgcn_s_memrealtime();
+        }
+    }
+    if (DIAG && lane == 0) {
+        for (int k = 0; k < 5; ++k) atomicAdd((unsigned long long *)&diag[k], (unsigned long long)dsum[k]);
+        atomicAdd((unsigned long long *)&diag[5], (unsigned long long)kend);
+    }
+    if ((uint32_t)lane < kend) {
+        const uint32_t s = s0 + lane;
+        out_node[s] = res_key ? (int32_t)key_node(res_key) : -1;
+        if (out_key) out_key[s] = res_key;
+        if (stamps) stamps[s] = res_stamp;
+    }
+    if ((uint32_t)lane < nd) { store_dyn(t, didx, dr); store_dynx<F>(t, didx, dx); }
+}
+
+// =============================================================================================
+// small row kernels (qs_node_upsert / qs_reserve / qs_unreserve)
+// =============================================================================================
+__global__ void k_set_row(DevTable t, uint32_t i, HostRow v, uint32_t feat) {
+    t.ac[i] = v.ac; t.am[i] = v.am; t.rc[i] = v.rc; t.rm[i] = v.rm;
+    t.zc[i] = v.zc; t.zm[i] = v.zm; t.np[i] = v.np; t.mp[i] = v.mp;
+    t.yc[i] = v.yc; t.ym[i] = v.ym;
+    if (feat & kFeatExt) { t.ae0[i] = v.ae0; t.re0[i] = v.re0; t.ae1[i] = v.ae1; t.re1[i] = v.re1; }
+    if (feat & kFeatTaint) { t.th[i] = v.th; t.ts[i] = v.ts; }
+    if (feat & kFeatAffinity) { t.lb0[i] = v.lb0; t.lb1[i] = v.lb1; }
+}
+
+// =============================================================================================
+// launchers
+// =============================================================================================
+#define QS_RET(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return e_; } while (0)
+
+template <int NPT, int BS, uint32_t F>
+static hipError_t persistent_t(const DevTable &t, const DPod *pods, const DPodX *podx, uint32_t P,
+                               const DevCfg &c, int32_t *on, uint64_t *ok, uint64_t *st,
+                               hipStream_t stream) {
+    hipLaunchKernelGGL((k_persistent<NPT, BS, F>), dim3(1), dim3(BS), 0, stream, t, pods, podx, P,
+                       c, on, ok, st);
+    return hipGetLastError();
+}
+
+// Largest node count per feature set that keeps every row in VGPRs without scratch spills
+// (checked with -Rpass-analysis=kernel-resource-usage at 1024 threads, 4 waves/SIMD).
+template <uint32_t F>
+static constexpr uint32_t persistent_cap() {
+    return F == 0 ? 6144u : (F == kFeatExt ? 5120u : 2048u);
+}
+
+template <uint32_t F>
+static hipError_t persistent_f(const DevTable &t, const DPod *pods, const DPodX *podx, uint32_t P,
+                               const DevCfg &c, int32_t *on, uint64_t *ok, uint64_t *st,
+                               hipStream_t stream) {
+    const uint32_t n = t.n;
+    if (n > persistent_cap<F>()) return hipErrorInvalidValue;
+    if (n <= 64) return persistent_t<1, 64, F>(t, pods, podx, P, c, on, ok, st, stream);
+    if (n <= 128) return persistent_t<1, 128, F>(t, pods, podx, P, c, on, ok, st, stream);
+    if (n <= 256) return persistent_t<1, 256, F>(t, pods, podx, P, c, on, ok, st, stream);
+    if (n <= 512) return persistent_t<1, 512, F>(t, pods, podx, P, c, on, ok, st, stream);
+    if (n <= 1024) return persistent_t<1, 1024, F>(t, pods, podx, P, c, on, ok, st, stream);
+    if (n <= 2048) return persistent_t<2, 1024, F>(t, pods, podx, P, c, on, ok, st, stream);
+    if constexpr (persistent_cap<F>() > 2048) {
+        if (n <= 3072) return persistent_t<3, 1024, F>(t, pods, podx, P, c, on, ok, st, stream);
+        if (n <= 4096) return persistent_t<4, 1024, F>(t, pods, podx, P, c, on, ok, st, stream);
+        if (n <= 5120) return persistent_t<5, 1024, F>(t, pods, podx, P, c, on, ok, st, stream);
+    }
+    if constexpr (persistent_cap<F>() > 5120) {
+        if (n <= 6144) return persistent_t<6, 1024, F>(t, pods, podx, P, c, on, ok, st, stream);
+    }
+    return hipErrorInvalidValue;
+}
+
+static uint32_t feat_class(uint32_t feat) {
+    return feat == 0 ? 0u : (feat == kFeatExt ? kFeatExt : (kFeatExt | kFeatTaint | kFeatAffinity));
+}
+
+hipError_t launch_persistent(const DevTable &t, const DPod *pods, const DPodX *podx, uint32_t P,
+                             const DevCfg &c, int32_t *on, uint64_t *ok, uint64_t *st,
+                             hipStream_t stream) {
+    switch (feat_class(c.feat)) {
+        case 0: return persistent_f<0>(t, pods, podx, P, c, on, ok, st, stream);
+        case kFeatExt: return persistent_f<kFeatExt>(t, pods, podx, P, c, on, ok, st, stream);
+        default:
+            return persistent_f<kFeatExt | kFeatTaint | kFeatAffinity>(t, pods, podx, P, c, on, ok,
+                                                                         st, stream);
+    }
+}
+
+uint32_t persistent_max_nodes(uint32_t feat) {
+    switch (feat_class(feat)) {
+        case 0: return persistent_cap<0>();
+        case kFeatExt: return persistent_cap<kFeatExt>();
+        default: return persistent_cap<kFeatExt | kFeatTaint | kFeatAffinity>();
+    }
+}
+
+template <uint32_t F>
+static hipError_t scan_pod_f(const DevTable &t, const DPod *pods, const DPodX *podx, uint32_t s,
+                             const DevCfg &c, void *scratch, int32_t *on, uint64_t *ok,
+                             uint64_t *st, uint8_t *feas, int32_t *score, int32_t *total,
+                             bool commit, hipStream_t stream) {
+    ScanScratch *sc = (ScanScratch *)scratch;
+    const uint32_t blocks = min(2048u, max(1u, (t.n + 255) / 256));
+    if (F & kFeatNorm)
+        hipLaunchKernelGGL((k_scan_norm<F>), dim3(blocks), dim3(256), 0, stream, t, pods, podx, s, sc);
+    hipLaunchKernelGGL((k_scan_key<F>), dim3(blocks), dim3(256), 0, stream, t, pods, podx, s, c, sc,
+                       feas, score, total);
+    if (commit)
+        hipLaunchKernelGGL((k_scan_commit<F>), dim3(1), dim3(1), 0, stream, t, pods, s, sc, on, ok, st);
+    return hipGetLastError();
+}
+
+hipError_t launch_scan_pod(const DevTable &t, const DPod *pods, const DPodX *podx, uint32_t s,
+                           const DevCfg &c, void *scratch, int32_t *on, uint64_t *ok, uint64_t *st,
+                           uint8_t *feas, int32_t *score, int32_t *total, bool commit,
+                           hipStream_t stream) {
+    switch (feat_class(c.feat)) {
+        case 0: return scan_pod_f<0>(t, pods, podx, s, c, scratch, on, ok, st, feas, score, total, commit, stream);
+        case kFeatExt: return scan_pod_f<kFeatExt>(t, pods, podx, s, c, scratch, on, ok, st, feas, score, total, commit, stream);
+        default:
+            return scan_pod_f<kFeatExt | kFeatTaint | kFeatAffinity>(t, pods, podx, s, c, scratch, on, ok, st, feas, score, total, commit, stream);
+    }
+}
+
+size_t scan_scratch_bytes() { return sizeof(ScanScratch); }
+
+template <uint32_t F>
+static hipError_t la_window_f(const DevTable &t, const DPod *pods, uint32_t s0, uint32_t P,
+                              const DevCfg &c, const LaGeom &geo, uint64_t *lists, int32_t *on,
+                              uint64_t *ok, uint64_t *st, uint64_t *diag, hipStream_t stream) {
+    const uint32_t K = geo.K, G = geo.G, L = geo.L, GLp = geo.epl * 64;
+    const uint32_t kw = min(K, P - s0);
+    const dim3 grid(kw * G);
+    switch (geo.E) {
+#define QS_SEL(EE) case EE: hipLaunchKernelGGL((k_la_select<256, EE, F>), grid, dim3(256), 0, stream, t, pods, c, s0, P, G, L, geo.chunk, GLp, lists); break;
+        QS_SEL(1) QS_SEL(2) QS_SEL(3) QS_SEL(4) QS_SEL(5) QS_SEL(6) QS_SEL(8) QS_SEL(10) QS_SEL(12) QS_SEL(16)
+#undef QS_SEL
+        default: return hipErrorInvalidValue;
+    }
+    QS_RET(hipGetLastError());
+    const size_t lds = (((t.n + 31) / 32 + 3) & ~3u) * 4 + sizeof(Row) + sizeof(RowX);
+    switch (geo.epl) {
+#define QS_RES(EP) case EP: if (diag) hipLaunchKernelGGL((k_la_resolve<F, EP, true>), dim3(1), dim3(64), lds, stream, t, pods, c, s0, P, K, GLp, lists, on, ok, st, diag); \
+                            else hipLaunchKernelGGL((k_la_resolve<F, EP, false>), dim3(1), dim3(64), lds, stream, t, pods, c, s0, P, K, GLp, lists, on, ok, st, diag); break;
+        QS_RES(1) QS_RES(2) QS_RES(4) QS_RES(8) QS_RES(16)
+#undef QS_RES
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_la_window(const DevTable &t, const DPod *pods, uint32_t s0, uint32_t P,
+                            const DevCfg &c, const LaGeom &geo, uint64_t *lists, int32_t *on,
+                            uint64_t *ok, uint64_t *st, uint64_t *diag, hipStream_t stream) {
+    if (c.feat & kFeatNorm) return hipErrorInvalidValue;
+    if (c.feat & kFeatExt) return la_window_f<kFeatExt>(t, pods, s0, P, c, geo, lists, on, ok, st, diag, stream);
+    return la_window_f<0>(t, pods, s0, P, c, geo, lists, on, ok, st, diag, stream);
+}
+
+LaGeom la_geometry(uint32_t n, uint32_t K) {
+    // G node chunks per pod: about 1,280 nodes (E = 5 per lane of a 256-thread block) per chunk,
+    // capped so the resolver sees at most 1,024 list entries per pod (16 per lane).
+    static const uint32_t Es[] = {1, 2, 3, 4, 5, 6, 8, 10, 12, 16};
+    LaGeom g{};
+    g.K = K;
+    g.L = K;
+    const uint32_t gmax = std::max(1u, 1024u / g.L);
+    uint32_t G = std::max(1u, std::min(gmax, (n + 1279) / 1280));
+    const uint32_t per = (n + G - 1) / G;
+    const uint32_t e_need = std::max(1u, (per + 255) / 256);
+    uint32_t E = 0;
+    for (uint32_t e : Es)
+        if (e >= e_need) { E = e; break; }
+    if (E == 0) { g.G = 0; return g; }  // table too large for one-level lists
+    g.E = E;
+    g.chunk = E * 256;
+    g.G = std::max(1u, (n + g.chunk - 1) / g.chunk);
+    const uint32_t need = (g.G * g.L + 63) / 64;  // list entries per resolver lane
+    g.epl = 1;
+    while (g.epl < need) g.epl *= 2;
+    if (g.epl > 16) g.G = 0;
+    return g;
+}
+
+}  // namespace qs

@@ -1,0 +1,48 @@
+// qs_launch.hpp — host-callable launchers of the gfx950 kernels (defined in qs_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace qs {
+
+struct DevTable;
+struct DevCfg;
+struct DPod;
+struct DPodX;
+
+// One compacted node row, passed by value to k_set_row.
+struct HostRow {
+    int32_t ac, am, rc, rm, zc, zm, np, mp;
+    double yc, ym;
+    int32_t ae0, re0, ae1, re1;
+    uint64_t th, ts, lb0, lb1;
+};
+
+// Lookahead geometry: window K pods, list length L (= K), G node chunks of `chunk` nodes per pod,
+// E nodes per lane in the select kernel (256-thread blocks).
+// epl = list entries per resolver lane (power of two); a pod's lists occupy 64*epl entries.
+struct LaGeom {
+    uint32_t K, L, G, E, chunk, epl;
+};
+
+hipError_t launch_persistent(const DevTable &t, const DPod *pods, const DPodX *podx, uint32_t P,
+                             const DevCfg &c, int32_t *out_node, uint64_t *out_key,
+                             uint64_t *stamps, hipStream_t stream);
+uint32_t persistent_max_nodes(uint32_t feat);
+
+hipError_t launch_scan_pod(const DevTable &t, const DPod *pods, const DPodX *podx, uint32_t s,
+                           const DevCfg &c, void *scratch, int32_t *out_node, uint64_t *out_key,
+                           uint64_t *stamps, uint8_t *feas, int32_t *score, int32_t *total,
+                           bool commit, hipStream_t stream);
+size_t scan_scratch_bytes();
+
+LaGeom la_geometry(uint32_t n, uint32_t K);
+hipError_t launch_la_window(const DevTable &t, const DPod *pods, uint32_t s0, uint32_t P,
+                            const DevCfg &c, const LaGeom &geo, uint64_t *lists, int32_t *out_node,
+                            uint64_t *out_key, uint64_t *stamps, uint64_t *diag,
+                            hipStream_t stream);
+
+__global__ void k_set_row(DevTable t, uint32_t i, HostRow v, uint32_t feat);
+
+}  // namespace qs

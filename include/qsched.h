@@ -1,0 +1,193 @@
+/*
+ * qsched.h — C ABI of libqsched.so, the MI355X (gfx950) scheduling core.
+ *
+ * This is the drop-in boundary: the surface a kube-scheduler framework plugin
+ * binds through cgo (or any FFI).  Plain C types only — no HIP, no torch, no C++.
+ *
+ * What each entry point replaces (upstream kube-scheduler v1.32, `UP <path>#<symbol>`; the mounted
+ * reference /root/reference/README.md:1 is a title line, so there is no reference-side FFI to cite
+ * beyond the north_star's "thin cgo C-ABI" in BASELINE.json:5):
+ *   qs_open / qs_close        framework.Handle-scoped plugin state (UP cmd/kube-scheduler/app#WithPlugin
+ *                             factory `func(ctx, runtime.Object, framework.Handle) (framework.Plugin, error)`)
+ *   qs_nodes_load             Cache.UpdateSnapshot → Snapshot NodeInfo list (UP backend/cache#Snapshot)
+ *   qs_node_upsert            per-NodeInfo Generation diff (UP framework/types.go#NodeInfo.Generation)
+ *   qs_score_pod              PreFilter+Filter+PreScore+Score+NormalizeScore for ALL nodes of one pod
+ *                             (UP framework/interface.go#{PreFilterPlugin,FilterPlugin,ScorePlugin,
+ *                             ScoreExtensions}; UP schedule_one.go#{findNodesThatPassFilters,prioritizeNodes})
+ *   qs_reserve / qs_unreserve ReservePlugin.Reserve / Unreserve → NodeInfo.AddPod / RemovePod
+ *                             (UP framework/interface.go#ReservePlugin, framework/types.go#NodeInfo.update)
+ *   qs_schedule_stream        ScheduleOne loop with deterministic selectHost (UP schedule_one.go#
+ *                             {ScheduleOne,schedulingCycle,selectHost,assume}; spec/semantics.md S7/S8)
+ *
+ * Semantics: spec/semantics.md.  Ownership: every pointer argument is borrowed for the duration of
+ * the call only (cgo rule: C never retains Go pointers); outputs go to caller-allocated arrays of
+ * the stated length.  Quantities are canonical int64 (millicores, bytes, counts).  Errors are
+ * return codes, never exceptions or aborts; `qs_last_error` holds the message.  Unschedulable is
+ * not an error: placement −1.  Threading: one mutex per context serialises every call.
+ */
+#ifndef QSCHED_H
+#define QSCHED_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QS_ABI_VERSION 1
+#define QS_MAX_EXT 2   /* extended resources per node/pod (e.g. amd.com/gpu) */
+#define QS_MAX_TERMS 4 /* node-affinity terms per pod (required OR-terms, preferred terms) */
+
+typedef enum qs_status {
+    QS_OK = 0,
+    QS_EINVAL = 1,   /* bad argument / input outside the device layout's range */
+    QS_EDEVICE = 2,  /* HIP or RCCL failure (message in qs_last_error) */
+    QS_ETIMEOUT = 3, /* persistent-kernel spin bound hit */
+    QS_ENOMEM = 4,
+    QS_ESTATE = 5 /* call out of order (e.g. no nodes loaded) */
+} qs_status;
+
+typedef enum qs_qos { QS_QOS_BESTEFFORT = 0, QS_QOS_BURSTABLE = 1, QS_QOS_GUARANTEED = 2 } qs_qos;
+
+typedef enum qs_mode { QS_MODE_EXACT = 0, QS_MODE_BATCHED = 1 } qs_mode;
+
+/* Which device engine runs the exact stream (all are bit-exact; AUTO picks the fastest). */
+typedef enum qs_engine {
+    QS_ENGINE_AUTO = 0,
+    QS_ENGINE_PERSISTENT = 1, /* one resident workgroup, node rows in registers (N <= 8192) */
+    QS_ENGINE_SCAN = 2,       /* per-pod grid scan + finalize/reserve launch chain (any N) */
+    QS_ENGINE_LOOKAHEAD = 3   /* exact top-K lookahead: chip-wide stale scan + sequential resolve */
+} qs_engine;
+
+typedef struct qs_config {
+    uint32_t abi_version;        /* = QS_ABI_VERSION */
+    int32_t engine;              /* qs_engine */
+    int64_t fit_weight_cpu;      /* NodeResourcesFitArgs.ScoringStrategy.Resources cpu weight (1) */
+    int64_t fit_weight_mem;      /* ... memory weight (1) */
+    int32_t w_fit[3];            /* NodeResourcesFit plugin weight per QoS class [BE, Bu, G] */
+    int32_t w_bal[3];            /* NodeResourcesBalancedAllocation weight per QoS class */
+    int32_t w_taint;             /* TaintToleration weight (3) */
+    int32_t w_affinity;          /* NodeAffinity weight (2) */
+    int32_t enable_taint;        /* TaintToleration filter+score on */
+    int32_t enable_affinity;     /* NodeAffinity filter+score on */
+    int32_t balanced_skip_besteffort; /* 0 = v1.32 behaviour */
+    int32_t qos_sort;            /* 1 = QoSSort order (spec S8), 0 = arrival order */
+    int32_t lookahead;           /* pods per lookahead window (0 = default) */
+    int32_t record_timestamps;   /* 1 = per-pod device timestamps for p50/p99 cycle latency */
+    int32_t reserved[8];
+} qs_config;
+
+/* Canonical node table, structure of arrays, n entries each.  alloc_ext/req_ext are [n][QS_MAX_EXT],
+ * label_bits is [n][2].  Optional columns may be NULL (read as 0). */
+typedef struct qs_node_soa {
+    const int64_t *alloc_cpu, *alloc_mem, *alloc_ext, *max_pods;
+    const int64_t *req_cpu, *req_mem, *req_ext, *nz_cpu, *nz_mem, *pods;
+    const uint64_t *taint_hard, *taint_soft, *label_bits;
+} qs_node_soa;
+
+/* Same layout, writable (qs_nodes_read, qs_synth_generate). */
+typedef struct qs_node_soa_out {
+    int64_t *alloc_cpu, *alloc_mem, *alloc_ext, *max_pods;
+    int64_t *req_cpu, *req_mem, *req_ext, *nz_cpu, *nz_mem, *pods;
+    uint64_t *taint_hard, *taint_soft, *label_bits;
+} qs_node_soa_out;
+
+typedef struct qs_node_row {
+    int64_t alloc_cpu, alloc_mem, alloc_ext[QS_MAX_EXT], max_pods;
+    int64_t req_cpu, req_mem, req_ext[QS_MAX_EXT], nz_cpu, nz_mem, pods;
+    uint64_t taint_hard, taint_soft, label_bits[2];
+} qs_node_row;
+
+/* One pod, precomputed on the host (spec S2/S3; qs_pod_from_containers helps). */
+typedef struct qs_pod {
+    int64_t req_cpu, req_mem, req_ext[QS_MAX_EXT]; /* effective requests, missing -> 0 */
+    int64_t nz_cpu, nz_mem;                        /* non-zero requests (defaults 100m / 200Mi) */
+    int32_t qos;                                   /* qs_qos */
+    int32_t priority;
+    uint64_t tol_hard; /* interned taint bits tolerated for NoSchedule/NoExecute */
+    uint64_t tol_soft; /* interned taint bits tolerated for PreferNoSchedule */
+    uint64_t sel[2];   /* nodeSelector requirement bits (all must hold) */
+    int32_t n_req_terms, n_pref_terms;
+    uint64_t req_terms[QS_MAX_TERMS][2];  /* required node-affinity terms (OR of ANDs) */
+    uint64_t pref_terms[QS_MAX_TERMS][2]; /* preferred terms */
+    int32_t pref_weight[QS_MAX_TERMS];
+} qs_pod;
+
+/* One container of a pod spec for qs_pod_from_containers (spec S2/S3). has_* = 0 means missing. */
+typedef struct qs_container {
+    int32_t kind; /* 0 regular, 1 init, 2 restartable init (sidecar) */
+    int32_t has_req_cpu, has_req_mem, has_lim_cpu, has_lim_mem;
+    int64_t req_cpu, req_mem, lim_cpu, lim_mem;
+    int64_t req_ext[QS_MAX_EXT];
+} qs_container;
+
+typedef struct qs_stats {
+    uint64_t pods, placed, unschedulable, evals;
+    uint64_t batches, truncations;  /* lookahead windows run / windows cut early */
+    double wall_s;                  /* qs_stream_run wall, device-resident inputs */
+    double h2d_s, d2h_s;            /* host<->device copies around it (qs_schedule_stream) */
+    double p50_cycle_us, p99_cycle_us, max_cycle_us; /* per-pod decision interval (record_timestamps) */
+    int32_t engine_used;
+    int32_t reserved[7];
+} qs_stats;
+
+typedef struct qs_ctx qs_ctx;
+typedef struct qs_stream qs_stream;
+
+/* ---- lifecycle ---- */
+void qs_config_default(qs_config *cfg);
+qs_status qs_open(const qs_config *cfg, int device, qs_ctx **out);
+/* Sharded context for one rank of `world` (one process per GPU).  nccl_id = 128 bytes from
+ * qs_dist_unique_id on rank 0, broadcast by the caller.  The node table is sharded by contiguous
+ * ranges; the per-window exchange runs on RCCL over xGMI. */
+qs_status qs_open_shard(const qs_config *cfg, int device, int rank, int world,
+                        const uint8_t nccl_id[128], qs_ctx **out);
+qs_status qs_dist_unique_id(uint8_t out[128]);
+qs_status qs_close(qs_ctx *ctx);
+const char *qs_last_error(const qs_ctx *ctx);
+const char *qs_version(void);
+
+/* ---- node table (device-resident SoA, host mirror authoritative) ---- */
+qs_status qs_nodes_load(qs_ctx *ctx, const qs_node_soa *nodes, uint32_t n);
+qs_status qs_nodes_read(qs_ctx *ctx, const qs_node_soa_out *out, uint32_t n);
+qs_status qs_node_upsert(qs_ctx *ctx, uint32_t idx, const qs_node_row *row, uint64_t generation);
+/* Device-side snapshot of the whole node table (checkpoint/resume; bench resets between steps). */
+qs_status qs_table_save(qs_ctx *ctx);
+qs_status qs_table_restore(qs_ctx *ctx);
+qs_status qs_reserve(qs_ctx *ctx, uint32_t node, const qs_pod *pod);
+qs_status qs_unreserve(qs_ctx *ctx, uint32_t node, const qs_pod *pod);
+
+/* ---- one pod, all nodes (framework-embedded path) ----
+ * feasible_n (nullable): 1/0 per node; score_n (nullable): [n][4] {LeastAllocated, Balanced,
+ * TaintToleration, NodeAffinity} normalized plugin scores (0 where infeasible); total_n (nullable):
+ * QoS-weighted total per node (-1 where infeasible); best: node index of spec S7 or -1. */
+qs_status qs_score_pod(qs_ctx *ctx, const qs_pod *pod, uint8_t *feasible_n, int32_t *score_n,
+                       int32_t *total_n, int32_t *best);
+
+/* ---- exact stream ---- */
+qs_status qs_schedule_stream(qs_ctx *ctx, const qs_pod *pods, uint32_t p, qs_mode mode,
+                             int32_t *placement_p, qs_stats *stats);
+/* Split form: prepare (host precompute + H2D), run (device only, timed; may run again, e.g. after
+ * qs_table_restore), results (D2H of the last run). */
+qs_status qs_stream_prepare(qs_ctx *ctx, const qs_pod *pods, uint32_t p, qs_stream **out);
+qs_status qs_stream_run(qs_ctx *ctx, qs_stream *s, qs_mode mode, qs_stats *stats);
+qs_status qs_stream_results(qs_ctx *ctx, qs_stream *s, int32_t *placement_p, uint64_t *best_key_p);
+qs_status qs_stream_free(qs_ctx *ctx, qs_stream *s);
+/* Per-pod device timestamps (100 MHz s_memrealtime ticks, stream order; record_timestamps = 1). */
+qs_status qs_stream_stamps(qs_ctx *ctx, qs_stream *s, uint64_t *stamps_p);
+
+/* ---- host helpers (spec S2/S3, spec/synth.md) ---- */
+qs_status qs_pod_from_containers(const qs_container *c, uint32_t nc, const int64_t *overhead_cpu_mem,
+                                 qs_pod *out);
+int32_t qs_compute_qos(const qs_container *c, uint32_t nc);
+/* sizeof of the ABI structs for binding self-checks: 0 config, 1 node_soa, 2 node_row, 3 pod,
+ * 4 container, 5 stats. */
+size_t qs_struct_size(int which);
+qs_status qs_synth_generate(int config, uint64_t seed, uint32_t n, uint32_t p,
+                            const qs_node_soa_out *nodes, qs_pod *pods);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QSCHED_H */

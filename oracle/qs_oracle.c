@@ -1,0 +1,363 @@
+/*
+ * qs_oracle.c — CPU ORACLE (test infrastructure; see qs_oracle.h header for the parity status:
+ * PARITY UNPINNED by the reference, which has no code; pinned by spec/kat.md KATs and the
+ * independent oracle/oracle.py restatement).
+ *
+ * Straight-line restatement of spec/semantics.md, one pod × one node at a time, int64 integer
+ * arithmetic and IEEE binary64 where upstream uses float64.  Every function names the upstream
+ * kube-scheduler v1.32 symbol it restates.
+ *
+ * Build: oracle/Makefile -> oracle/liboracle.so (gcc -O2 -fopenmp -ffp-contract=off).
+ */
+#include "qs_oracle.h"
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define MAX_NODE_SCORE 100 /* UP framework/interface.go#MaxNodeScore */
+
+/* UP noderesources/least_allocated.go#leastRequestedScore */
+static int64_t least_requested_score(int64_t requested, int64_t capacity) {
+    if (capacity == 0) return 0;
+    if (requested > capacity) return 0;
+    return ((capacity - requested) * MAX_NODE_SCORE) / capacity;
+}
+
+/* UP noderesources/least_allocated.go#leastResourceScorer over resources [cpu, memory];
+ * requested = NonZeroRequested + pod non-zero request (resource_allocation.go#score,
+ * calculateResourceAllocatableRequest with useRequested=false). */
+int64_t or_least_allocated(int64_t alloc_c, int64_t reqd_c, int64_t alloc_m, int64_t reqd_m,
+                           int64_t wc, int64_t wm) {
+    int64_t alloc[2] = {alloc_c, alloc_m}, reqd[2] = {reqd_c, reqd_m}, w[2] = {wc, wm};
+    int64_t node_score = 0, weight_sum = 0;
+    for (int i = 0; i < 2; i++) {
+        if (alloc[i] == 0) continue;
+        node_score += least_requested_score(reqd[i], alloc[i]) * w[i];
+        weight_sum += w[i];
+    }
+    if (weight_sum == 0) return 0;
+    return node_score / weight_sum;
+}
+
+/* UP noderesources/balanced_allocation.go#balancedResourceScorer over [cpu, memory];
+ * requested = Requested + pod request (useRequested=true). */
+int64_t or_balanced(int64_t alloc_c, int64_t req_c, int64_t alloc_m, int64_t req_m) {
+    int64_t alloc[2] = {alloc_c, alloc_m}, reqd[2] = {req_c, req_m};
+    double fr[2];
+    int cnt = 0;
+    for (int i = 0; i < 2; i++) {
+        if (alloc[i] == 0) continue;
+        volatile double f = (double)reqd[i] / (double)alloc[i];
+        double ff = f;
+        if (ff > 1) ff = 1;
+        fr[cnt++] = ff;
+    }
+    double std = 0.0;
+    if (cnt == 2) {
+        volatile double d = (fr[0] - fr[1]) / 2;
+        std = fabs(d);
+    }
+    volatile double one_minus = 1 - std;
+    volatile double scaled = one_minus * (double)MAX_NODE_SCORE;
+    return (int64_t)scaled;
+}
+
+/* UP noderesources/fit.go#fitsRequest (+ TooManyPods check) */
+static int fits_request(const or_nodes *nd, const or_pods *pd, uint32_t n, uint32_t j) {
+    if (nd->pods[n] + 1 > nd->max_pods[n]) return 0;
+    int any_ext = 0;
+    for (int k = 0; k < OR_MAX_EXT; k++) any_ext |= pd->req_ext[j * OR_MAX_EXT + k] != 0;
+    if (pd->req_cpu[j] == 0 && pd->req_mem[j] == 0 && !any_ext) return 1;
+    if (pd->req_cpu[j] > 0 && pd->req_cpu[j] > nd->alloc_cpu[n] - nd->req_cpu[n]) return 0;
+    if (pd->req_mem[j] > 0 && pd->req_mem[j] > nd->alloc_mem[n] - nd->req_mem[n]) return 0;
+    for (int k = 0; k < OR_MAX_EXT; k++) {
+        int64_t q = pd->req_ext[j * OR_MAX_EXT + k];
+        if (q == 0) continue;
+        if (q > nd->alloc_ext[n * OR_MAX_EXT + k] - nd->req_ext[n * OR_MAX_EXT + k]) return 0;
+    }
+    return 1;
+}
+
+/* UP tainttoleration/taint_toleration.go#Filter on interned bitmasks (spec S5) */
+static int taint_filter(const or_nodes *nd, const or_pods *pd, uint32_t n, uint32_t j) {
+    return (nd->taint_hard[n] & ~pd->tol_hard[j]) == 0;
+}
+/* UP tainttoleration/taint_toleration.go#Score: count of intolerable PreferNoSchedule taints */
+static int64_t taint_raw(const or_nodes *nd, const or_pods *pd, uint32_t n, uint32_t j) {
+    return (int64_t)__builtin_popcountll(nd->taint_soft[n] & ~pd->tol_soft[j]);
+}
+static int mask_subset(const uint64_t *m, const uint64_t *bits) {
+    return (m[0] & bits[0]) == m[0] && (m[1] & bits[1]) == m[1];
+}
+/* UP nodeaffinity/node_affinity.go#Filter (nodeSelector + required terms, OR over terms) */
+static int affinity_filter(const or_nodes *nd, const or_pods *pd, uint32_t n, uint32_t j) {
+    const uint64_t *lb = &nd->label_bits[n * 2];
+    if (!mask_subset(&pd->sel[j * 2], lb)) return 0;
+    int nt = pd->n_req_terms[j];
+    if (nt == 0) return 1;
+    for (int t = 0; t < nt; t++)
+        if (mask_subset(&pd->req_terms[(j * OR_MAX_TERMS + t) * 2], lb)) return 1;
+    return 0;
+}
+/* UP nodeaffinity/node_affinity.go#Score: sum of weights of matching preferred terms */
+static int64_t affinity_raw(const or_nodes *nd, const or_pods *pd, uint32_t n, uint32_t j) {
+    const uint64_t *lb = &nd->label_bits[n * 2];
+    int64_t s = 0;
+    for (int t = 0; t < pd->n_pref_terms[j]; t++)
+        if (mask_subset(&pd->pref_terms[(j * OR_MAX_TERMS + t) * 2], lb))
+            s += pd->pref_weight[j * OR_MAX_TERMS + t];
+    return s;
+}
+
+static int feasible(const or_config *cfg, const or_nodes *nd, const or_pods *pd, uint32_t n,
+                    uint32_t j) {
+    if (!fits_request(nd, pd, n, j)) return 0;
+    if (cfg->enable_taint && !taint_filter(nd, pd, n, j)) return 0;
+    if (cfg->enable_affinity && !affinity_filter(nd, pd, n, j)) return 0;
+    return 1;
+}
+
+/* UP helper/normalize_score.go#DefaultNormalizeScore(100, reverse, scores) for one score */
+static int64_t normalize(int64_t raw, int64_t max_count, int reverse) {
+    if (max_count == 0) return reverse ? MAX_NODE_SCORE : raw;
+    int64_t s = MAX_NODE_SCORE * raw / max_count;
+    return reverse ? MAX_NODE_SCORE - s : s;
+}
+
+/* One pod's key for node n given the per-pod normalization maxima (spec S5-S7). */
+static uint64_t node_key(const or_config *cfg, const or_nodes *nd, const or_pods *pd, uint32_t n,
+                         uint32_t j, int64_t mt, int64_t ma, int64_t *sc) {
+    if (!feasible(cfg, nd, pd, n, j)) return 0;
+    int q = pd->qos[j];
+    int64_t la = or_least_allocated(nd->alloc_cpu[n], nd->nz_cpu[n] + pd->nz_cpu[j],
+                                    nd->alloc_mem[n], nd->nz_mem[n] + pd->nz_mem[j], cfg->wc,
+                                    cfg->wm);
+    int64_t ba = or_balanced(nd->alloc_cpu[n], nd->req_cpu[n] + pd->req_cpu[j], nd->alloc_mem[n],
+                             nd->req_mem[n] + pd->req_mem[j]);
+    if (cfg->balanced_skip_besteffort && q == 0) ba = 0;
+    int64_t tt = 0, na = 0;
+    if (cfg->enable_taint) tt = normalize(taint_raw(nd, pd, n, j), mt, 1);
+    if (cfg->enable_affinity) na = normalize(affinity_raw(nd, pd, n, j), ma, 0);
+    int64_t total = cfg->w_fit[q] * la + cfg->w_bal[q] * ba + cfg->w_tt * tt * (cfg->enable_taint != 0) +
+                    cfg->w_na * na * (cfg->enable_affinity != 0);
+    if (sc) { sc[0] = la; sc[1] = ba; sc[2] = tt; sc[3] = na; }
+    return ((uint64_t)(total + 1) << 32) | (uint64_t)(0xFFFFFFFFu - n);
+}
+
+/* NormalizeScore maxima over the nodes that passed Filter (UP framework/runtime/framework.go#
+ * RunScorePlugins -> NormalizeScore runs over the feasible node list only). */
+static void norm_maxima(const or_config *cfg, const or_nodes *nd, const or_pods *pd, uint32_t j,
+                        int64_t *mt, int64_t *ma, int nthreads) {
+    int64_t t = 0, a = 0;
+    if (cfg->enable_taint || cfg->enable_affinity) {
+        int64_t n_ = nd->n;
+#pragma omp parallel for reduction(max : t, a) num_threads(nthreads) if (nthreads > 1)
+        for (int64_t n = 0; n < n_; n++) {
+            if (!feasible(cfg, nd, pd, (uint32_t)n, j)) continue;
+            if (cfg->enable_taint) { int64_t r = taint_raw(nd, pd, (uint32_t)n, j); if (r > t) t = r; }
+            if (cfg->enable_affinity) { int64_t r = affinity_raw(nd, pd, (uint32_t)n, j); if (r > a) a = r; }
+        }
+    }
+    *mt = t;
+    *ma = a;
+}
+
+void or_score_pod(const or_config *cfg, const or_nodes *nd, const or_pods *pd, uint32_t j,
+                  uint64_t *keys, int64_t *scores) {
+    int64_t mt, ma;
+    norm_maxima(cfg, nd, pd, j, &mt, &ma, 1);
+    for (uint32_t n = 0; n < nd->n; n++)
+        keys[n] = node_key(cfg, nd, pd, n, j, mt, ma, scores ? &scores[(size_t)n * 4] : NULL);
+}
+
+/* UP schedule_one.go#assume -> framework/types.go#NodeInfo.AddPod/RemovePod (update ±1) */
+void or_reserve(or_nodes *nd, const or_pods *pd, uint32_t j, uint32_t n, int sign) {
+    nd->req_cpu[n] += sign * pd->req_cpu[j];
+    nd->req_mem[n] += sign * pd->req_mem[j];
+    for (int k = 0; k < OR_MAX_EXT; k++)
+        nd->req_ext[n * OR_MAX_EXT + k] += sign * pd->req_ext[j * OR_MAX_EXT + k];
+    nd->nz_cpu[n] += sign * pd->nz_cpu[j];
+    nd->nz_mem[n] += sign * pd->nz_mem[j];
+    nd->pods[n] += sign;
+}
+
+/* spec S8: stable order by (qos desc, priority desc, arrival asc) — bottom-up stable merge sort
+ * (shape of UP queuesort/priority_sort.go#Less with QoS rank ahead of priority). */
+static void order_pods(const or_config *cfg, const or_pods *pd, uint32_t *order) {
+    uint32_t P = pd->p;
+    for (uint32_t j = 0; j < P; j++) order[j] = j;
+    if (!cfg->qos_sort) return;
+    uint32_t *tmp = (uint32_t *)malloc(sizeof(uint32_t) * (P ? P : 1));
+    for (uint32_t j = 0; j < P; j++) tmp[j] = j;
+    uint32_t *a = tmp, *b = order;
+    for (uint32_t width = 1; width < P; width *= 2) {
+        for (uint32_t lo = 0; lo < P; lo += 2 * width) {
+            uint32_t mid = lo + width < P ? lo + width : P;
+            uint32_t hi = lo + 2 * width < P ? lo + 2 * width : P;
+            uint32_t i = lo, k = mid, o = lo;
+            while (i < mid && k < hi) {
+                uint32_t x = a[i], y = a[k];
+                /* compare (qos desc, priority desc); equal -> take left (stable) */
+                int64_t rx = (int64_t)pd->qos[x] * 4294967296LL + pd->priority[x];
+                int64_t ry = (int64_t)pd->qos[y] * 4294967296LL + pd->priority[y];
+                if (ry > rx) b[o++] = a[k++]; else b[o++] = a[i++];
+            }
+            while (i < mid) b[o++] = a[i++];
+            while (k < hi) b[o++] = a[k++];
+        }
+        uint32_t *t = a; a = b; b = t;
+    }
+    if (a != order) memcpy(order, a, sizeof(uint32_t) * P);
+    free(tmp);
+}
+
+void or_schedule(const or_config *cfg, or_nodes *nd, const or_pods *pd, int32_t *placement,
+                 uint64_t *best_key, uint32_t *order_out, int nthreads) {
+    uint32_t P = pd->p;
+    uint32_t *order = (uint32_t *)malloc(sizeof(uint32_t) * (P ? P : 1));
+    order_pods(cfg, pd, order);
+    if (nthreads < 1) nthreads = 1;
+    for (uint32_t s = 0; s < P; s++) {
+        uint32_t j = order[s];
+        int64_t mt, ma;
+        norm_maxima(cfg, nd, pd, j, &mt, &ma, nthreads);
+        uint64_t best = 0;
+        int64_t n_ = nd->n;
+        /* UP schedule_one.go#findNodesThatPassFilters + prioritizeNodes (Parallelizer over
+         * nodes) fused with the deterministic selectHost of spec S7 (max of unique keys). */
+#pragma omp parallel for reduction(max : best) num_threads(nthreads) if (nthreads > 1)
+        for (int64_t n = 0; n < n_; n++) {
+            uint64_t k = node_key(cfg, nd, pd, (uint32_t)n, j, mt, ma, NULL);
+            if (k > best) best = k;
+        }
+        if (best_key) best_key[j] = best;
+        if (best == 0) {
+            placement[j] = -1;
+        } else {
+            uint32_t n = 0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFu);
+            placement[j] = (int32_t)n;
+            or_reserve(nd, pd, j, n, +1);
+        }
+    }
+    if (order_out) memcpy(order_out, order, sizeof(uint32_t) * P);
+    free(order);
+}
+
+/* ---------------- spec/synth.md generator (independent restatement) ---------------- */
+static uint64_t sm_at(uint64_t seed, uint64_t c) {
+    uint64_t z = seed + (c + 1) * 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+static uint32_t pick(uint64_t seed, uint64_t c, uint32_t k) { return (uint32_t)((sm_at(seed, c) >> 33) % k); }
+
+static const int64_t NODE_CPU[6] = {4000, 8000, 16000, 32000, 64000, 96000};
+static const int64_t NODE_MPC[3] = {2, 4, 8};
+static const int64_t POD_CPU[6] = {500, 1000, 1500, 2000, 4000, 8000};
+static const int64_t POD_MEM[7] = {128, 256, 512, 1024, 2048, 4096, 8192};
+static const int64_t GPU_CNT[4] = {1, 2, 4, 8};
+#define GIB (1LL << 30)
+#define MIB (1LL << 20)
+#define DEF_CPU 100
+#define DEF_MEM (200 * MIB)
+
+static int pair_bit(int za, int zb) { /* za < zb, lexicographic index of the pair, + 3 */
+    int idx = 0;
+    for (int a = 0; a < za; a++) idx += 9 - a;
+    return 3 + idx + (zb - za - 1);
+}
+
+void or_generate(int config, uint64_t seed, or_nodes *nd, or_pods *pd) {
+    uint32_t N = nd->n, P = pd->p;
+    int c4 = (config == 4);
+    for (uint32_t i = 0; i < N; i++) {
+        uint64_t c = 8ULL * i;
+        int64_t cpu = NODE_CPU[pick(seed, c + 0, 6)];
+        int64_t mpc = NODE_MPC[pick(seed, c + 1, 3)];
+        nd->alloc_cpu[i] = cpu;
+        nd->alloc_mem[i] = (cpu / 1000) * mpc * GIB;
+        nd->max_pods[i] = 110;
+        nd->req_cpu[i] = nd->req_mem[i] = nd->nz_cpu[i] = nd->nz_mem[i] = nd->pods[i] = 0;
+        for (int k = 0; k < OR_MAX_EXT; k++) nd->alloc_ext[i * OR_MAX_EXT + k] = nd->req_ext[i * OR_MAX_EXT + k] = 0;
+        nd->taint_hard[i] = nd->taint_soft[i] = 0;
+        nd->label_bits[2 * i] = nd->label_bits[2 * i + 1] = 0;
+        if (c4) {
+            int gpu = pick(seed, c + 2, 10) == 0;
+            int maint = pick(seed, c + 3, 20) == 0;
+            int zone = (int)pick(seed, c + 4, 10);
+            int pool = gpu ? 2 : (int)pick(seed, c + 5, 2); /* 0 general, 1 highmem, 2 gpu */
+            int ssd = pick(seed, c + 6, 2) == 0;
+            uint64_t lo = 0, hi = 0;
+            if (gpu) { nd->alloc_ext[i * OR_MAX_EXT] = 8; nd->taint_hard[i] |= 1ULL << 0; }
+            if (maint) nd->taint_soft[i] |= 1ULL << 1;
+            if (pool == 2) lo |= 1ULL << 0;
+            if (ssd) lo |= 1ULL << 1;
+            if (pool == 1) lo |= 1ULL << 2;
+            for (int a = 0; a < 10; a++)
+                for (int b = a + 1; b < 10; b++)
+                    if (a == zone || b == zone) {
+                        int bit = pair_bit(a, b);
+                        if (bit < 64) lo |= 1ULL << bit; else hi |= 1ULL << (bit - 64);
+                    }
+            nd->label_bits[2 * i] = lo;
+            nd->label_bits[2 * i + 1] = hi;
+        }
+    }
+    for (uint32_t j = 0; j < P; j++) {
+        uint64_t c = 8ULL * N + 16ULL * j;
+        uint32_t qd = pick(seed, c + 0, 10);
+        int64_t cpu = POD_CPU[pick(seed, c + 1, 6)];
+        int64_t mem = POD_MEM[pick(seed, c + 2, 7)] * MIB;
+        uint32_t memmode = pick(seed, c + 3, 4);
+        (void)pick(seed, c + 4, 2); /* limmode: affects the emitted limits only, not S2/S3 */
+        int q = qd < 2 ? 2 : (qd < 7 ? 1 : 0);
+        int64_t rc = 0, rm = 0, zc = DEF_CPU, zm = DEF_MEM;
+        if (q == 2) { rc = zc = cpu; rm = zm = mem; }
+        else if (q == 1) { rc = zc = cpu; if (memmode != 0) { rm = zm = mem; } }
+        pd->req_cpu[j] = rc; pd->req_mem[j] = rm; pd->nz_cpu[j] = zc; pd->nz_mem[j] = zm;
+        pd->qos[j] = q; pd->priority[j] = 0;
+        for (int k = 0; k < OR_MAX_EXT; k++) pd->req_ext[j * OR_MAX_EXT + k] = 0;
+        pd->tol_hard[j] = pd->tol_soft[j] = 0;
+        pd->sel[2 * j] = pd->sel[2 * j + 1] = 0;
+        pd->n_req_terms[j] = pd->n_pref_terms[j] = 0;
+        for (int t = 0; t < OR_MAX_TERMS; t++) {
+            size_t o = ((size_t)j * OR_MAX_TERMS + t) * 2;
+            pd->req_terms[o] = pd->req_terms[o + 1] = pd->pref_terms[o] = pd->pref_terms[o + 1] = 0;
+            pd->pref_weight[j * OR_MAX_TERMS + t] = 0;
+        }
+        if (c4) {
+            if (pick(seed, c + 5, 20) == 0) {
+                pd->req_ext[j * OR_MAX_EXT] = GPU_CNT[pick(seed, c + 6, 4)];
+                pd->tol_hard[j] |= 1ULL << 0;
+                pd->sel[2 * j] |= 1ULL << 0;
+            }
+            if (pick(seed, c + 7, 5) == 0) {
+                int za = (int)pick(seed, c + 8, 10);
+                int zb = (za + 1 + (int)pick(seed, c + 9, 9)) % 10;
+                int a = za < zb ? za : zb, b = za < zb ? zb : za;
+                int bit = pair_bit(a, b);
+                size_t o = ((size_t)j * OR_MAX_TERMS) * 2;
+                if (bit < 64) pd->req_terms[o] |= 1ULL << bit; else pd->req_terms[o + 1] |= 1ULL << (bit - 64);
+                pd->n_req_terms[j] = 1;
+            }
+            if (pick(seed, c + 10, 5) == 0) {
+                uint32_t which = pick(seed, c + 11, 3);
+                int t = 0;
+                if (which == 0 || which == 2) {
+                    pd->pref_terms[((size_t)j * OR_MAX_TERMS + t) * 2] = 1ULL << 1;
+                    pd->pref_weight[j * OR_MAX_TERMS + t] = 50; t++;
+                }
+                if (which == 1 || which == 2) {
+                    pd->pref_terms[((size_t)j * OR_MAX_TERMS + t) * 2] = 1ULL << 2;
+                    pd->pref_weight[j * OR_MAX_TERMS + t] = 20; t++;
+                }
+                pd->n_pref_terms[j] = t;
+            }
+            if (pick(seed, c + 12, 10) == 0) pd->tol_soft[j] |= 1ULL << 1;
+        }
+    }
+}

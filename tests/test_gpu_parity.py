@@ -1,0 +1,91 @@
+"""GPU parity: libqsched.so (through the C ABI) vs the CPU oracle, bit-exact.
+
+Placements, per-pod best keys (spec S7 packed (total, index)) and the final node table must be
+identical to oracle/ on the same seeded inputs (spec/synth.md generator).  Parity is unpinned by
+the reference (it has no code); the oracle itself is pinned by spec/kat.md (tests/test_oracle_kat.py).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+from qsched import Scheduler, pods_from_struct, synth_generate  # noqa: E402
+
+CFG4 = dict(enable_taint=1, enable_affinity=1)
+
+
+def run_gpu(nodes, pods, cfg, engine, lookahead=0):
+    with Scheduler(dict(cfg, engine=engine, lookahead=lookahead)) as s:
+        s.load_nodes(nodes)
+        st = s.prepare(pods)
+        stats = st.run()
+        pl, keys = st.results()
+        st.free()
+        final = s.read_nodes()
+    return pl, keys, final, stats
+
+
+def run_oracle(oracle, nodes, pods, cfg, nthreads=16):
+    on = {k: v.copy() for k, v in nodes.items()}
+    pl, keys, _ = oracle.schedule(on, pods_from_struct(pods), cfg, nthreads=nthreads)
+    return pl, keys, on
+
+
+def assert_same(g, o, final_g, final_o):
+    pl_g, keys_g = g
+    pl_o, keys_o = o
+    bad = np.nonzero(pl_g != pl_o)[0]
+    assert bad.size == 0, f"{bad.size} placements differ; first at pod {bad[0]}: gpu {pl_g[bad[0]]} oracle {pl_o[bad[0]]}"
+    assert np.array_equal(keys_g, keys_o)
+    for k in final_o:
+        assert np.array_equal(final_g[k], final_o[k]), k
+
+
+@pytest.mark.parametrize("engine", ["persistent", "scan", "lookahead"])
+@pytest.mark.parametrize("config,n,p", [(1, 100, 1000), (2, 700, 9000), (2, 5000, 3000)])
+def test_stream_parity(oracle, engine, config, n, p):
+    nodes, pods = synth_generate(config, n, p)
+    g = run_gpu(nodes, pods, {}, engine)
+    o = run_oracle(oracle, nodes, pods, {})
+    assert_same(g[:2], o[:2], g[2], o[2])
+
+
+@pytest.mark.parametrize("K", [1, 2, 7, 33, 64])
+def test_lookahead_windows(oracle, K):
+    nodes, pods = synth_generate(2, 1500, 6000)
+    g = run_gpu(nodes, pods, {}, "lookahead", lookahead=K)
+    o = run_oracle(oracle, nodes, pods, {})
+    assert_same(g[:2], o[:2], g[2], o[2])
+
+
+@pytest.mark.parametrize("engine", ["persistent", "scan"])
+def test_config4_parity(oracle, engine):
+    nodes, pods = synth_generate(4, 2000, 6000)
+    g = run_gpu(nodes, pods, CFG4, engine)
+    o = run_oracle(oracle, nodes, pods, CFG4)
+    assert_same(g[:2], o[:2], g[2], o[2])
+
+
+def test_config2_full_lookahead(oracle):
+    """BASELINE.json configs[1]: 5,000 nodes x 100,000 pods, every placement bit-exact."""
+    nodes, pods = synth_generate(2, 5000, 100000)
+    g = run_gpu(nodes, pods, {}, "lookahead")
+    o = run_oracle(oracle, nodes, pods, {})
+    assert_same(g[:2], o[:2], g[2], o[2])
+    assert 0.01 <= (g[0] < 0).mean() <= 0.05  # spec/synth.md G4: 1-5 % unschedulable
+
+
+def test_config2_full_persistent(oracle):
+    nodes, pods = synth_generate(2, 5000, 100000)
+    g = run_gpu(nodes, pods, {}, "persistent")
+    o = run_oracle(oracle, nodes, pods, {})
+    assert_same(g[:2], o[:2], g[2], o[2])
+
+
+@pytest.mark.parametrize("engine", ["persistent", "scan", "lookahead"])
+def test_ext_resources_without_taints(oracle, engine):
+    """amd.com/gpu requests in Filter with the Fit+Balanced profile (no taint/affinity plugins)."""
+    nodes, pods = synth_generate(4, 1800, 5000)
+    g = run_gpu(nodes, pods, {}, engine)
+    o = run_oracle(oracle, nodes, pods, {})
+    assert_same(g[:2], o[:2], g[2], o[2])
