@@ -1,10 +1,9 @@
 // qs_device.hpp — device-side data layout and the per-(pod, node) evaluation shared by every
 // gfx950 kernel of libqsched.  Semantics: spec/semantics.md (S4–S7); exactness arguments: S10.
 //
-// Layout in HBM: the node table is a structure of arrays of int32 columns in
-// compacted units (cpu millicores, memory 2^u bytes), plus per-node reciprocals precomputed at
-// load time (RN_f64(1/alloc) for BalancedAllocation, RN_f32(1/alloc) for LeastAllocated) and, for
-// profiles with TaintToleration / NodeAffinity / extended resources, mask and ext columns.
+// Layout in HBM: the node table is an array of 64-byte rows of int32 fields in
+// compacted units (cpu millicores, memory 2^u bytes) plus per-node reciprocals RN_f64(1/alloc)
+// precomputed at load time, and a parallel array of 32-byte taint/label mask rows.
 // Everything here is compiled with -ffp-contract=off: the float64 path must round exactly like
 // Go's float64 (spec S5, kat K7).
 #pragma once
@@ -16,16 +15,24 @@ namespace qs {
 
 constexpr int kWave = 64;
 
-// ---- device node table (SoA, n entries each) ------------------------------------------------
+// ---- device node table: one 64-byte row per node (+ a 32-byte mask row) -----------------------
+// Row-major so that a lane gathering one node (the resolver's candidate / dirty rows) touches one
+// cache line with four 16-byte loads; a 64-lane scan over consecutive nodes still uses whole lines.
+struct alignas(16) DRow {
+    int32_t ac, am;          // Allocatable cpu (m), memory (2^u B)
+    int32_t rc, rm;          // Requested
+    int32_t zc, zm;          // NonZeroRequested
+    int32_t np, mp;          // pod count, AllowedPodNumber
+    double yc, ym;           // RN_f64(1/alloc) (0 where alloc == 0)
+    int32_t ae0, re0, ae1, re1;  // extended resources
+};
+struct alignas(16) DMask {
+    uint64_t th, ts;         // taint_hard, taint_soft
+    uint64_t lb0, lb1;       // label requirement bits
+};
 struct DevTable {
-    int32_t *ac, *am;          // Allocatable cpu (m), memory (2^u B)
-    int32_t *rc, *rm;          // Requested
-    int32_t *zc, *zm;          // NonZeroRequested
-    int32_t *np, *mp;          // pod count, AllowedPodNumber
-    double *yc, *ym;           // RN_f64(1/alloc) (0 where alloc == 0)
-    int32_t *ae0, *re0, *ae1, *re1;  // extended resources (feature bit kFeatExt)
-    uint64_t *th, *ts;         // taint_hard, taint_soft
-    uint64_t *lb0, *lb1;       // label requirement bits
+    DRow *rows;
+    DMask *masks;
     uint32_t n;
 };
 
@@ -66,10 +73,13 @@ struct RowX {
 };
 
 __device__ __forceinline__ Row load_row(const DevTable &t, uint32_t i) {
+    const int4 *q = reinterpret_cast<const int4 *>(t.rows + i);
+    const int4 a = q[0], b = q[1];
+    const double2 y = reinterpret_cast<const double2 *>(t.rows + i)[2];
     Row r;
-    r.ac = t.ac[i]; r.am = t.am[i]; r.rc = t.rc[i]; r.rm = t.rm[i];
-    r.zc = t.zc[i]; r.zm = t.zm[i]; r.np = t.np[i]; r.mp = t.mp[i];
-    r.yc = t.yc[i]; r.ym = t.ym[i];
+    r.ac = a.x; r.am = a.y; r.rc = a.z; r.rm = a.w;
+    r.zc = b.x; r.zm = b.y; r.np = b.z; r.mp = b.w;
+    r.yc = y.x; r.ym = y.y;
     return r;
 }
 __device__ __forceinline__ Row empty_row() {
@@ -79,22 +89,49 @@ __device__ __forceinline__ Row empty_row() {
     r.yc = r.ym = 0.0;
     return r;
 }
+// Per-field select (a ternary on whole structs is lowered through scratch memory).
+__device__ __forceinline__ Row sel_row(bool c, const Row &a, const Row &b) {
+    Row r;
+    r.ac = c ? a.ac : b.ac; r.am = c ? a.am : b.am; r.rc = c ? a.rc : b.rc; r.rm = c ? a.rm : b.rm;
+    r.zc = c ? a.zc : b.zc; r.zm = c ? a.zm : b.zm; r.np = c ? a.np : b.np; r.mp = c ? a.mp : b.mp;
+    r.yc = c ? a.yc : b.yc; r.ym = c ? a.ym : b.ym;
+    return r;
+}
+__device__ __forceinline__ RowX sel_rowx(bool c, const RowX &a, const RowX &b) {
+    RowX r;
+    r.ae0 = c ? a.ae0 : b.ae0; r.re0 = c ? a.re0 : b.re0; r.ae1 = c ? a.ae1 : b.ae1;
+    r.re1 = c ? a.re1 : b.re1; r.th = c ? a.th : b.th; r.ts = c ? a.ts : b.ts;
+    r.lb0 = c ? a.lb0 : b.lb0; r.lb1 = c ? a.lb1 : b.lb1;
+    return r;
+}
 template <uint32_t F>
 __device__ __forceinline__ RowX load_rowx(const DevTable &t, uint32_t i) {
     RowX x;
     x.ae0 = x.re0 = x.ae1 = x.re1 = 0;
     x.th = x.ts = x.lb0 = x.lb1 = 0;
-    if (F & kFeatExt) { x.ae0 = t.ae0[i]; x.re0 = t.re0[i]; x.ae1 = t.ae1[i]; x.re1 = t.re1[i]; }
-    if (F & kFeatTaint) { x.th = t.th[i]; x.ts = t.ts[i]; }
-    if (F & kFeatAffinity) { x.lb0 = t.lb0[i]; x.lb1 = t.lb1[i]; }
+    if (F & kFeatExt) {
+        const int4 e = reinterpret_cast<const int4 *>(t.rows + i)[3];
+        x.ae0 = e.x; x.re0 = e.y; x.ae1 = e.z; x.re1 = e.w;
+    }
+    if (F & (kFeatTaint | kFeatAffinity)) {
+        const DMask m = t.masks[i];
+        x.th = m.th; x.ts = m.ts; x.lb0 = m.lb0; x.lb1 = m.lb1;
+    }
     return x;
 }
 __device__ __forceinline__ void store_dyn(const DevTable &t, uint32_t i, const Row &r) {
-    t.rc[i] = r.rc; t.rm[i] = r.rm; t.zc[i] = r.zc; t.zm[i] = r.zm; t.np[i] = r.np;
+    int32_t *w = reinterpret_cast<int32_t *>(t.rows + i);
+    *reinterpret_cast<int2 *>(w + 2) = make_int2(r.rc, r.rm);
+    *reinterpret_cast<int2 *>(w + 4) = make_int2(r.zc, r.zm);
+    w[6] = r.np;
 }
 template <uint32_t F>
 __device__ __forceinline__ void store_dynx(const DevTable &t, uint32_t i, const RowX &x) {
-    if (F & kFeatExt) { t.re0[i] = x.re0; t.re1[i] = x.re1; }
+    if (F & kFeatExt) {
+        int32_t *w = reinterpret_cast<int32_t *>(t.rows + i);
+        w[13] = x.re0;
+        w[15] = x.re1;
+    }
 }
 // Reserve (spec S7; UP framework/types.go#NodeInfo.update(+1))
 __device__ __forceinline__ void reserve(Row &r, RowX &x, const DPod &p, int sign) {
@@ -185,7 +222,13 @@ __device__ __forceinline__ uint32_t node_total(const Row &r, const RowX &x, cons
     const uint32_t wce = hc ? (uint32_t)c.wc : 0u, wme = hm ? (uint32_t)c.wm : 0u;
     const uint32_t num = __umul24(sc_c, wce) + __umul24(sc_m, wme);
     const uint32_t den = wce + wme;
-    const double yd = (hc & hm) ? c.yd_both : (hc ? c.yd_c : c.yd_m);
+    // select the weight-sum reciprocal with bit masks (a ternary on the kernel-argument doubles
+    // was lowered to a per-lane load from the kernarg segment, stalling on vmcnt(0))
+    const uint64_t mb = 0ull - (uint64_t)(hc & hm), mc = 0ull - (uint64_t)(hc & !hm),
+                   mm = 0ull - (uint64_t)(!hc & hm);
+    const double yd = __builtin_bit_cast(
+        double, (__builtin_bit_cast(uint64_t, c.yd_both) & mb) |
+                    (__builtin_bit_cast(uint64_t, c.yd_c) & mc) | (__builtin_bit_cast(uint64_t, c.yd_m) & mm));
     const uint32_t la = den ? floor_div(num, yd) : 0u;
     // BalancedAllocation (UP balanced_allocation.go#balancedResourceScorer), Requested + pod req
     const double f0 = fraction(r.ac, r.rc + p.rc, r.yc);

@@ -215,24 +215,20 @@ HostRow compact_row(const Mirror &m, uint32_t i, int shift) {
     return r;
 }
 
-// Column layout inside ctx->tbl: 256-byte aligned columns of cap entries.  Returns the size;
-// assigns the column pointers when base != nullptr.
+// Table layout inside ctx->tbl: cap rows of 64 B, then cap mask rows of 32 B.  Returns the size;
+// assigns the pointers when base != nullptr.
 size_t carve(DevTable &t, uint32_t cap, char *base) {
-    size_t off = 0;
-    auto col = [&](size_t elem) {
-        char *p = base ? base + off : nullptr;
-        off += ((size_t)cap * elem + 255) & ~(size_t)255;
-        return (void *)p;
-    };
-    t.ac = (int32_t *)col(4); t.am = (int32_t *)col(4); t.rc = (int32_t *)col(4);
-    t.rm = (int32_t *)col(4); t.zc = (int32_t *)col(4); t.zm = (int32_t *)col(4);
-    t.np = (int32_t *)col(4); t.mp = (int32_t *)col(4);
-    t.yc = (double *)col(8); t.ym = (double *)col(8);
-    t.ae0 = (int32_t *)col(4); t.re0 = (int32_t *)col(4); t.ae1 = (int32_t *)col(4);
-    t.re1 = (int32_t *)col(4);
-    t.th = (uint64_t *)col(8); t.ts = (uint64_t *)col(8);
-    t.lb0 = (uint64_t *)col(8); t.lb1 = (uint64_t *)col(8);
-    return off;
+    t.rows = base ? (DRow *)base : nullptr;
+    t.masks = base ? (DMask *)(base + (size_t)cap * sizeof(DRow)) : nullptr;
+    return (size_t)cap * (sizeof(DRow) + sizeof(DMask));
+}
+
+DRow to_drow(const HostRow &r) {
+    DRow d;
+    d.ac = r.ac; d.am = r.am; d.rc = r.rc; d.rm = r.rm; d.zc = r.zc; d.zm = r.zm;
+    d.np = r.np; d.mp = r.mp; d.yc = r.yc; d.ym = r.ym;
+    d.ae0 = r.ae0; d.re0 = r.re0; d.ae1 = r.ae1; d.re1 = r.re1;
+    return d;
 }
 
 // Upload the whole mirror (compacted) to the device.
@@ -245,29 +241,17 @@ void upload_table(qs_ctx *c) {
     }
     carve(c->dt, c->cap, c->tbl.as<char>());
     c->dt.n = n;
-    std::vector<double> yc(n), ym(n);
-    std::vector<int32_t> ac(n), am(n), rc(n), rm(n), zc(n), zm(n), np(n), mp(n), ae0(n), re0(n),
-        ae1(n), re1(n);
-    std::vector<uint64_t> th(n), ts(n), lb0(n), lb1(n);
+    std::vector<DRow> rows(n);
+    std::vector<DMask> masks(n);
     for (uint32_t i = 0; i < n; i++) {
         const HostRow r = compact_row(c->m, i, c->shift);
-        ac[i] = r.ac; am[i] = r.am; rc[i] = r.rc; rm[i] = r.rm; zc[i] = r.zc; zm[i] = r.zm;
-        np[i] = r.np; mp[i] = r.mp; yc[i] = r.yc; ym[i] = r.ym;
-        ae0[i] = r.ae0; re0[i] = r.re0; ae1[i] = r.ae1; re1[i] = r.re1;
-        th[i] = r.th; ts[i] = r.ts; lb0[i] = r.lb0; lb1[i] = r.lb1;
+        rows[i] = to_drow(r);
+        masks[i] = DMask{r.th, r.ts, r.lb0, r.lb1};
     }
-    const DevTable &t = c->dt;
-    auto up = [&](void *dst, const void *src, size_t b) {
-        if (b) HIPCHK(hipMemcpyAsync(dst, src, b, hipMemcpyHostToDevice, c->stream));
-    };
-    up(t.ac, ac.data(), 4 * n); up(t.am, am.data(), 4 * n); up(t.rc, rc.data(), 4 * n);
-    up(t.rm, rm.data(), 4 * n); up(t.zc, zc.data(), 4 * n); up(t.zm, zm.data(), 4 * n);
-    up(t.np, np.data(), 4 * n); up(t.mp, mp.data(), 4 * n);
-    up(t.yc, yc.data(), 8 * n); up(t.ym, ym.data(), 8 * n);
-    up(t.ae0, ae0.data(), 4 * n); up(t.re0, re0.data(), 4 * n);
-    up(t.ae1, ae1.data(), 4 * n); up(t.re1, re1.data(), 4 * n);
-    up(t.th, th.data(), 8 * n); up(t.ts, ts.data(), 8 * n);
-    up(t.lb0, lb0.data(), 8 * n); up(t.lb1, lb1.data(), 8 * n);
+    if (n) {
+        HIPCHK(hipMemcpyAsync(c->dt.rows, rows.data(), n * sizeof(DRow), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(c->dt.masks, masks.data(), n * sizeof(DMask), hipMemcpyHostToDevice, c->stream));
+    }
     HIPCHK(hipStreamSynchronize(c->stream));
     c->dev_valid = true;
 }
@@ -286,24 +270,18 @@ void push_row(qs_ctx *c, uint32_t i) {
 void sync_mirror(qs_ctx *c) {
     if (!c->mirror_stale || !c->dev_valid) return;
     const uint32_t n = c->m.n;
-    std::vector<int32_t> rc(n), rm(n), zc(n), zm(n), np(n), re0(n), re1(n);
-    const DevTable &t = c->dt;
-    auto dn = [&](void *dst, const void *src, size_t b) {
-        if (b) HIPCHK(hipMemcpyAsync(dst, src, b, hipMemcpyDeviceToHost, c->stream));
-    };
-    dn(rc.data(), t.rc, 4 * n); dn(rm.data(), t.rm, 4 * n); dn(zc.data(), t.zc, 4 * n);
-    dn(zm.data(), t.zm, 4 * n); dn(np.data(), t.np, 4 * n); dn(re0.data(), t.re0, 4 * n);
-    dn(re1.data(), t.re1, 4 * n);
+    std::vector<DRow> rows(n);
+    if (n) HIPCHK(hipMemcpyAsync(rows.data(), c->dt.rows, n * sizeof(DRow), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     Mirror &m = c->m;
     for (uint32_t i = 0; i < n; i++) {
-        m.rc[i] = rc[i];
-        m.rm[i] = (int64_t)rm[i] << c->shift;
-        m.zc[i] = zc[i];
-        m.zm[i] = (int64_t)zm[i] << c->shift;
-        m.np[i] = np[i];
-        m.re[(size_t)i * QS_MAX_EXT] = re0[i];
-        m.re[(size_t)i * QS_MAX_EXT + 1] = re1[i];
+        m.rc[i] = rows[i].rc;
+        m.rm[i] = (int64_t)rows[i].rm << c->shift;
+        m.zc[i] = rows[i].zc;
+        m.zm[i] = (int64_t)rows[i].zm << c->shift;
+        m.np[i] = rows[i].np;
+        m.re[(size_t)i * QS_MAX_EXT] = rows[i].re0;
+        m.re[(size_t)i * QS_MAX_EXT + 1] = rows[i].re1;
     }
     c->mirror_stale = false;
 }
@@ -728,7 +706,9 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                                            nullptr, nullptr, nullptr, true, c->stream));
                 batches = P;
             } else {
-                const LaGeom geo = la_geometry(n, la_window(c));
+                LaGeom geo = la_geometry(n, la_window(c));
+                static const char *rw = getenv("QS_RESOLVER_WAVES");  // 1 = single-wave resolver
+                geo.waves = (rw && rw[0] == '1') ? 1u : 4u;
                 if (geo.G == 0) fail(QS_EINVAL, "no lookahead geometry for this table size");
                 const size_t lbytes = 8ull * geo.K * 64 * geo.epl;
                 c->lists.ensure(lbytes);
@@ -751,7 +731,8 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                     HIPCHK(hipMemcpyAsync(h, diag, 48, hipMemcpyDeviceToHost, c->stream));
                     HIPCHK(hipStreamSynchronize(c->stream));
                     const double np = h[5] ? (double)h[5] : 1.0;
-                    fprintf(stderr, "QS_DIAG resolve cycles/pod: cand %.0f issue %.0f fresh %.0f wmax %.0f commit %.0f (pods %llu, G=%u E=%u epl=%u)\n",
+                    fprintf(stderr, geo.waves == 1 ? "QS_DIAG resolve cycles/pod: cand %.0f issue %.0f fresh %.0f wmax %.0f commit %.0f (pods %llu, G=%u E=%u epl=%u)\n"
+                                                   : "QS_DIAG resolve4 busy cycles/pod: D %.0f A %.0f B %.0f C %.0f (-) %.0f (pods %llu, G=%u E=%u epl=%u)\n",
                             h[0] / np, h[1] / np, h[2] / np, h[3] / np, h[4] / np,
                             (unsigned long long)h[5], geo.G, geo.E, geo.epl);
                 }

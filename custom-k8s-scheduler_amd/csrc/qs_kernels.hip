@@ -363,36 +363,62 @@ __global__ __launch_bounds__(64) void k_la_resolve(DevTable t, const DPod *__res
     uint32_t didx = 0xFFFFFFFFu;
     uint32_t nd = 0;
     uint64_t res_key = 0, res_stamp = 0;
-    uint64_t ent[EPL];
+    // Software pipeline (three pods in flight):
+    //   pod i:   clean candidate = top-1 of the lane's entries, or top-2 when top-1 is the previous
+    //            pod's winner (both rows loaded one pod earlier: no memory or LDS on the path);
+    //   pod i+1: top-2 clean entries against the current dirty set (LDS bitmap) + their row loads;
+    //   pod i+2: list entries loaded.
+    uint64_t ent1[EPL], ent2[EPL];
 #pragma unroll
-    for (int m = 0; m < EPL; ++m) ent[m] = lists[lane + 64 * m];
+    for (int m = 0; m < EPL; ++m) ent1[m] = lists[lane + 64 * m];
+#pragma unroll
+    for (int m = 0; m < EPL; ++m) ent2[m] = kend > 1 ? lists[(size_t)GLp + lane + 64 * m] : 0ull;
     __syncthreads();
+    // top-2 clean entries of a pod's list against the dirty bitmap
+    auto top2 = [&](const uint64_t (&e)[EPL], uint64_t &c1, uint64_t &c2) {
+        uint32_t word[EPL];
+#pragma unroll
+        for (int m = 0; m < EPL; ++m) {
+            const uint32_t nidx = e[m] ? key_node(e[m]) : 0u;
+            word[m] = dirty[nidx >> 5] >> (nidx & 31);
+        }
+        c1 = 0;
+        c2 = 0;
+#pragma unroll
+        for (int m = 0; m < EPL; ++m) {
+            const uint64_t x = (word[m] & 1u) ? 0ull : e[m];
+            const bool gt1 = x > c1;
+            c2 = gt1 ? c1 : (x > c2 ? x : c2);
+            c1 = gt1 ? x : c1;
+        }
+    };
+    uint64_t c1, c2;
+    top2(ent1, c1, c2);
+    Row r1 = load_row(t, c1 ? key_node(c1) : 0u), r2 = load_row(t, c2 ? key_node(c2) : 0u);
+    RowX x1 = load_rowx<F>(t, c1 ? key_node(c1) : 0u), x2 = load_rowx<F>(t, c2 ? key_node(c2) : 0u);
+    uint32_t wprev = 0xFFFFFFFFu;
     if (DIAG) tprev = diag_stamp();
     for (uint32_t i = 0; i < kend; ++i) {
         const DPod p = pn;
         if (i + 1 < kend) pn = pods[s0 + i + 1];
-        // best clean stale candidate of this lane: all bitmap reads issued together
-        uint32_t word[EPL];
-#pragma unroll
-        for (int m = 0; m < EPL; ++m) {
-            const uint32_t nidx = ent[m] ? key_node(ent[m]) : 0u;
-            word[m] = dirty[nidx >> 5] >> (nidx & 31);
-        }
-        uint64_t cand = 0;
-#pragma unroll
-        for (int m = 0; m < EPL; ++m) {
-            const uint64_t e = (word[m] & 1u) ? 0ull : ent[m];
-            cand = e > cand ? e : cand;
-        }
+        // this pod's clean candidate: the previous winner is the only node dirtied since top2()
+        const bool use2 = c1 && key_node(c1) == wprev;
+        const uint64_t cand = use2 ? c2 : c1;
+        const Row crow = sel_row(use2, r2, r1);
+        const RowX cx = sel_rowx(use2, x2, x1);
         QS_STAMP(0)
-        // prefetch the candidate's row (used only if it wins) and the next pod's entries
-        const uint32_t cidx = cand ? key_node(cand) : 0u;
-        const Row crow = load_row(t, cidx);
-        const RowX cx = load_rowx<F>(t, cidx);
+        // next pod: top-2 clean entries and their rows; the pod after: its list entries
         if (i + 1 < kend) {
-            const uint64_t *nl = lists + (size_t)(i + 1) * GLp;
+            top2(ent2, c1, c2);
+            r1 = load_row(t, c1 ? key_node(c1) : 0u);
+            r2 = load_row(t, c2 ? key_node(c2) : 0u);
+            x1 = load_rowx<F>(t, c1 ? key_node(c1) : 0u);
+            x2 = load_rowx<F>(t, c2 ? key_node(c2) : 0u);
+        }
+        if (i + 2 < kend) {
+            const uint64_t *nl = lists + (size_t)(i + 2) * GLp;
 #pragma unroll
-            for (int m = 0; m < EPL; ++m) ent[m] = nl[lane + 64 * m];
+            for (int m = 0; m < EPL; ++m) ent2[m] = nl[lane + 64 * m];
         }
         QS_STAMP(1)
         // fresh keys of the dirty slots
@@ -426,6 +452,7 @@ __global__ __launch_bounds__(64) void k_la_resolve(DevTable t, const DPod *__res
                 ++nd;
             }
         }
+        wprev = ks ? key_node(ks) : 0xFFFFFFFFu;
         QS_STAMP(4)
         if ((uint32_t)lane == i) {
             res_key = ks;
@@ -445,16 +472,256 @@ __global__ __launch_bounds__(64) void k_la_resolve(DevTable t, const DPod *__res
     if ((uint32_t)lane < nd) { store_dyn(t, didx, dr); store_dynx<F>(t, didx, dx); }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Four-wave pipelined resolver (one wave per SIMD).  Pod i's dirty-slot keys never wait for an
+// evaluation: they were computed during pod i-1 for both outcomes —
+//   wave A: A_l = key_{i+1}(slot_l)              (slot l not the winner of pod i)
+//   wave B: B_l = key_{i+1}(slot_l + pod i)      (slot l wins pod i)
+//   wave C: C_l = key_{i+1}(cand_l(i) + pod i)   (lane l's clean candidate wins pod i: new slot),
+//           plus the top-2 clean list entries of pod i+1 and their rows (loaded one pod ahead);
+//   wave D: picks pod i's keys from A/B/C with pod i-1's winner, argmax, publishes the winner.
+// One LDS exchange + one s_barrier per pod.  Slot rows are replicated in waves A and B; a new
+// slot's row comes from wave C's staging copy of its candidate row.
+struct alignas(16) ResPub {
+    uint64_t ks;     // packed key of the winner (0 = unschedulable)
+    uint32_t w;      // winner node
+    int32_t slot;    // existing dirty slot that won, or -1
+    int32_t src;     // lane whose clean candidate won (new slot)
+    uint32_t nd_old; // lane of the new slot
+    uint32_t pad[2];
+};
+
+template <uint32_t F, int EPL, bool DIAG>
+__global__ __launch_bounds__(256) void k_la_resolve4(DevTable t, const DPod *__restrict__ pods,
+                                                     DevCfg c, uint32_t s0, uint32_t P,
+                                                     uint32_t K, uint32_t GLp,
+                                                     const uint64_t *__restrict__ lists,
+                                                     int32_t *__restrict__ out_node,
+                                                     uint64_t *__restrict__ out_key,
+                                                     uint64_t *__restrict__ stamps,
+                                                     uint64_t *__restrict__ diag) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t nwords = (t.n + 31) / 32;
+    uint32_t *dirty = lds;
+    char *base = (char *)(lds + ((nwords + 3) & ~3u));
+    uint64_t(*keyA)[64] = (uint64_t(*)[64])base; base += 2 * 64 * 8;
+    uint64_t(*keyB)[64] = (uint64_t(*)[64])base; base += 2 * 64 * 8;
+    uint64_t(*keyC)[64] = (uint64_t(*)[64])base; base += 2 * 64 * 8;
+    uint64_t(*C1)[64] = (uint64_t(*)[64])base; base += 2 * 64 * 8;
+    uint64_t(*C2)[64] = (uint64_t(*)[64])base; base += 2 * 64 * 8;
+    Row(*stage)[64] = (Row(*)[64])base; base += 2 * 64 * sizeof(Row);
+    int4(*stagex)[64] = (int4(*)[64])base; base += 2 * 64 * sizeof(int4);
+    ResPub *pub = (ResPub *)base; base += 2 * sizeof(ResPub);
+    uint32_t *slotnode = (uint32_t *)base; base += 64 * 4;
+    DPod *wpods = (DPod *)base;  // the window's pod records (K <= 64)
+
+    for (uint32_t i = threadIdx.x; i < nwords; i += 256) dirty[i] = 0;
+    if (threadIdx.x == 0) pub[1] = ResPub{0, 0xFFFFFFFFu, -1, -1, 0, {0, 0}};
+    const uint32_t kend = min(K, P - s0);
+    if (threadIdx.x < kend) wpods[threadIdx.x] = pods[s0 + threadIdx.x];
+    const DPodX px{};
+    __syncthreads();
+    if (kend == 0) return;
+    uint64_t dsum = 0, tprev = 0;
+#define QS_DIAG_BEGIN() if (DIAG) tprev = diag_stamp();
+#define QS_DIAG_END() if (DIAG) { const uint64_t t_ = diag_stamp(); dsum += t_ - tprev; }
+
+    // Each role runs its own loop; every wave executes one s_barrier per pod (+1 prologue), so
+    // the barriers pair up.  Roles never share registers, which keeps waitcnt placement local.
+    if (wv == 0) {
+        // ---- D: pod i's winner from the precomputed keys ---------------------------------------
+        uint32_t nd = 0, didx = 0xFFFFFFFFu;
+        uint64_t res_key = 0, res_stamp = 0;
+        __syncthreads();  // prologue barrier (wave C publishes pod 0's candidates)
+        for (uint32_t i = 0; i < kend; ++i) {
+            QS_DIAG_BEGIN()
+            const int par = i & 1, pp = par ^ 1;
+            const ResPub pv = pub[pp];
+            const bool pnew = pv.ks != 0 && pv.slot < 0;
+            uint64_t fk = 0;
+            if ((uint32_t)lane < nd) {
+                const uint64_t a = keyA[pp][lane], b = keyB[pp][lane];
+                const uint64_t sc = (lane == pv.slot) ? b : a;
+                fk = sc ? (sc | (uint64_t)(0xFFFFFFFFu - didx)) : 0ull;
+                if (pnew && (uint32_t)lane == pv.nd_old) fk = keyC[pp][pv.src];
+            }
+            const uint64_t e1 = C1[pp][lane], e2 = C2[pp][lane];
+            const uint64_t cand = (pv.ks != 0 && e1 != 0 && key_node(e1) == pv.w) ? e2 : e1;
+            const uint64_t best = fk > cand ? fk : cand;
+            const uint64_t ks = wave_max_u64(best);
+            ResPub np{ks, ks ? key_node(ks) : 0xFFFFFFFFu, -1, -1, nd, {0, 0}};
+            if (ks) {
+                const uint64_t own = __ballot((uint32_t)lane < nd && didx == np.w);
+                if (own) {
+                    np.slot = (int32_t)__builtin_ctzll(own);
+                } else {
+                    np.src = (int32_t)__builtin_ctzll(__ballot(cand == ks));
+                    if ((uint32_t)lane == nd) didx = np.w;
+                    if (lane == 0) dirty[np.w >> 5] |= 1u << (np.w & 31);
+                    ++nd;
+                }
+            }
+            if (lane == 0) pub[par] = np;
+            if ((uint32_t)lane == i) {
+                res_key = ks;
+                if (stamps) res_stamp = __builtin_amdgcn_s_memrealtime();
+            }
+            QS_DIAG_END()
+            __syncthreads();
+        }
+        if ((uint32_t)lane < kend) {
+            const uint32_t s = s0 + lane;
+            out_node[s] = res_key ? (int32_t)key_node(res_key) : -1;
+            if (out_key) out_key[s] = res_key;
+            if (stamps) stamps[s] = res_stamp;
+        }
+        if ((uint32_t)lane < nd) slotnode[lane] = didx;
+    } else if (wv <= 2) {
+        // ---- A / B: apply pod i-1 to the slot copy, then the next pod's keys --------------------
+        Row S = empty_row();
+        RowX SX{};
+        uint32_t nd = 0;
+        auto apply = [&](const ResPub &pv, int pp, const DPod &pprev) {
+            if (pv.ks == 0) return;
+            if (pv.slot >= 0) {
+                if (lane == pv.slot) reserve(S, SX, pprev, +1);
+            } else {
+                if ((uint32_t)lane == pv.nd_old) {
+                    S = stage[pp][pv.src];
+                    if (F & kFeatExt) {
+                        const int4 e = stagex[pp][pv.src];
+                        SX.ae0 = e.x; SX.re0 = e.y; SX.ae1 = e.z; SX.re1 = e.w;
+                    }
+                    reserve(S, SX, pprev, +1);
+                }
+                ++nd;
+            }
+        };
+        __syncthreads();
+        for (uint32_t i = 0; i < kend; ++i) {
+            QS_DIAG_BEGIN()
+            const int par = i & 1, pp = par ^ 1;
+            const ResPub pv = pub[pp];
+            if (i > 0) apply(pv, pp, wpods[i - 1]);
+            if (i + 1 < kend) {
+                const DPod pn1 = wpods[i + 1];
+                Row s2 = S;
+                RowX x2s = SX;
+                if (wv == 2) reserve(s2, x2s, wpods[i], +1);
+                const bool f = feasible<F>(s2, x2s, pn1, px);
+                const uint32_t tot = node_total<F>(s2, x2s, pn1, px, c, 0, 0.0, 0, 0.0, nullptr);
+                // score half only: wave D owns the slot -> node map and fills the index half
+                const uint64_t k = ((uint32_t)lane < nd && f) ? ((uint64_t)(tot + 1) << 32) : 0ull;
+                (wv == 1 ? keyA : keyB)[par][lane] = k;
+            }
+            QS_DIAG_END()
+            __syncthreads();
+        }
+        if (wv == 1) apply(pub[(kend - 1) & 1], (kend - 1) & 1, wpods[kend - 1]);
+        __syncthreads();  // slotnode written by wave D
+        if (wv == 1 && (uint32_t)lane < nd) {
+            const uint32_t node = slotnode[lane];
+            store_dyn(t, node, S);
+            store_dynx<F>(t, node, SX);
+        }
+    } else {
+        // ---- C: candidate rows, C keys, next pod's top-2 ------------------------------------
+        auto top2 = [&](const uint64_t(&e)[EPL], uint64_t &a, uint64_t &b) {
+            uint32_t word[EPL];
+#pragma unroll
+            for (int m = 0; m < EPL; ++m) {
+                const uint32_t nidx = e[m] ? key_node(e[m]) : 0u;
+                word[m] = dirty[nidx >> 5] >> (nidx & 31);
+            }
+            a = 0;
+            b = 0;
+#pragma unroll
+            for (int m = 0; m < EPL; ++m) {
+                const uint64_t x = (word[m] & 1u) ? 0ull : e[m];
+                const bool gt = x > a;
+                b = gt ? a : (x > b ? x : b);
+                a = gt ? x : a;
+            }
+        };
+        auto load_ent = [&](uint64_t(&e)[EPL], uint32_t pod) {
+            const uint64_t *l = lists + (size_t)pod * GLp;
+#pragma unroll
+            for (int m = 0; m < EPL; ++m) e[m] = pod < kend ? l[lane + 64 * m] : 0ull;
+        };
+        uint64_t c1, c2;
+        uint64_t eX[EPL], eY[EPL];  // ping-pong: entries consumed two pods after their load
+        {
+            uint64_t e0[EPL];
+            load_ent(e0, 0);
+            top2(e0, c1, c2);
+        }
+        load_ent(eX, 1);
+        load_ent(eY, 2);
+        C1[1][lane] = c1;
+        C2[1][lane] = c2;
+        Row r1 = load_row(t, c1 ? key_node(c1) : 0u), r2 = load_row(t, c2 ? key_node(c2) : 0u);
+        RowX x1 = load_rowx<F>(t, c1 ? key_node(c1) : 0u), x2 = load_rowx<F>(t, c2 ? key_node(c2) : 0u);
+        __syncthreads();
+        auto step = [&](uint32_t i, uint64_t(&en)[EPL]) {
+            QS_DIAG_BEGIN()
+            const int par = i & 1, pp = par ^ 1;
+            const ResPub pv = pub[pp];
+            const bool use2 = pv.ks != 0 && c1 != 0 && key_node(c1) == pv.w;
+            const uint64_t cc = use2 ? c2 : c1;
+            const Row crow = sel_row(use2, r2, r1);
+            const RowX cx = sel_rowx(use2, x2, x1);
+            stage[par][lane] = crow;
+            if (F & kFeatExt) stagex[par][lane] = make_int4(cx.ae0, cx.re0, cx.ae1, cx.re1);
+            if (i + 1 < kend) {
+                const DPod p = wpods[i], pn1 = wpods[i + 1];
+                top2(en, c1, c2);  // pod i+1 against the dirty set through pod i-1
+                C1[par][lane] = c1;
+                C2[par][lane] = c2;
+                r1 = load_row(t, c1 ? key_node(c1) : 0u);
+                r2 = load_row(t, c2 ? key_node(c2) : 0u);
+                x1 = load_rowx<F>(t, c1 ? key_node(c1) : 0u);
+                x2 = load_rowx<F>(t, c2 ? key_node(c2) : 0u);
+                load_ent(en, i + 3);
+                Row cr = crow;
+                RowX crx = cx;
+                reserve(cr, crx, p, +1);
+                const bool f = feasible<F>(cr, crx, pn1, px);
+                const uint32_t tot = node_total<F>(cr, crx, pn1, px, c, 0, 0.0, 0, 0.0, nullptr);
+                keyC[par][lane] = (cc != 0 && f) ? pack_key(tot + 1, key_node(cc)) : 0ull;
+            }
+            QS_DIAG_END()
+            __syncthreads();
+        };
+        uint32_t i = 0;
+        for (; i + 1 < kend; i += 2) {
+            step(i, eX);
+            step(i + 1, eY);
+        }
+        if (i < kend) step(i, eX);
+        __syncthreads();
+    }
+    if (DIAG && lane == 0) {
+        atomicAdd((unsigned long long *)&diag[wv], (unsigned long long)dsum);
+        if (wv == 0) atomicAdd((unsigned long long *)&diag[5], (unsigned long long)kend);
+    }
+    if (wv == 0) __syncthreads();  // pairs with the post-loop barrier of waves A/B and C
+#undef QS_DIAG_BEGIN
+#undef QS_DIAG_END
+}
+
 // =============================================================================================
 // small row kernels (qs_node_upsert / qs_reserve / qs_unreserve)
 // =============================================================================================
 __global__ void k_set_row(DevTable t, uint32_t i, HostRow v, uint32_t feat) {
-    t.ac[i] = v.ac; t.am[i] = v.am; t.rc[i] = v.rc; t.rm[i] = v.rm;
-    t.zc[i] = v.zc; t.zm[i] = v.zm; t.np[i] = v.np; t.mp[i] = v.mp;
-    t.yc[i] = v.yc; t.ym[i] = v.ym;
-    if (feat & kFeatExt) { t.ae0[i] = v.ae0; t.re0[i] = v.re0; t.ae1[i] = v.ae1; t.re1[i] = v.re1; }
-    if (feat & kFeatTaint) { t.th[i] = v.th; t.ts[i] = v.ts; }
-    if (feat & kFeatAffinity) { t.lb0[i] = v.lb0; t.lb1[i] = v.lb1; }
+    (void)feat;
+    DRow r;
+    r.ac = v.ac; r.am = v.am; r.rc = v.rc; r.rm = v.rm; r.zc = v.zc; r.zm = v.zm;
+    r.np = v.np; r.mp = v.mp; r.yc = v.yc; r.ym = v.ym;
+    r.ae0 = v.ae0; r.re0 = v.re0; r.ae1 = v.ae1; r.re1 = v.re1;
+    t.rows[i] = r;
+    t.masks[i] = DMask{v.th, v.ts, v.lb0, v.lb1};
 }
 
 // =============================================================================================
@@ -471,8 +738,9 @@ static hipError_t persistent_t(const DevTable &t, const DPod *pods, const DPodX 
     return hipGetLastError();
 }
 
-// Largest node count per feature set that keeps every row in VGPRs without scratch spills
-// (checked with -Rpass-analysis=kernel-resource-usage at 1024 threads, 4 waves/SIMD).
+// Largest node count per feature set for the register-resident rows (1024 threads, 4 waves/SIMD;
+// the largest NPT of each set spills a few dwords to scratch: correct, slower — the LOOKAHEAD
+// engine is the fast path at these sizes).
 template <uint32_t F>
 static constexpr uint32_t persistent_cap() {
     return F == 0 ? 6144u : (F == kFeatExt ? 5120u : 2048u);
@@ -569,10 +837,18 @@ static hipError_t la_window_f(const DevTable &t, const DPod *pods, uint32_t s0, 
         default: return hipErrorInvalidValue;
     }
     QS_RET(hipGetLastError());
-    const size_t lds = (((t.n + 31) / 32 + 3) & ~3u) * 4 + sizeof(Row) + sizeof(RowX);
+    const size_t bm = (((t.n + 31) / 32 + 3) & ~3u) * 4;
+    const size_t lds = bm + sizeof(Row) + sizeof(RowX);
+    const size_t lds4 = bm + 5 * 2 * 64 * 8 + 2 * 64 * (sizeof(Row) + sizeof(int4)) + 2 * sizeof(ResPub) + 64 * 4 + 64 * sizeof(DPod);
     switch (geo.epl) {
-#define QS_RES(EP) case EP: if (diag) hipLaunchKernelGGL((k_la_resolve<F, EP, true>), dim3(1), dim3(64), lds, stream, t, pods, c, s0, P, K, GLp, lists, on, ok, st, diag); \
-                            else hipLaunchKernelGGL((k_la_resolve<F, EP, false>), dim3(1), dim3(64), lds, stream, t, pods, c, s0, P, K, GLp, lists, on, ok, st, diag); break;
+#define QS_RES(EP) case EP: \
+        if (geo.waves == 1) { \
+            if (diag) hipLaunchKernelGGL((k_la_resolve<F, EP, true>), dim3(1), dim3(64), lds, stream, t, pods, c, s0, P, K, GLp, lists, on, ok, st, diag); \
+            else hipLaunchKernelGGL((k_la_resolve<F, EP, false>), dim3(1), dim3(64), lds, stream, t, pods, c, s0, P, K, GLp, lists, on, ok, st, diag); \
+        } else { \
+            if (diag) hipLaunchKernelGGL((k_la_resolve4<F, EP, true>), dim3(1), dim3(256), lds4, stream, t, pods, c, s0, P, K, GLp, lists, on, ok, st, diag); \
+            else hipLaunchKernelGGL((k_la_resolve4<F, EP, false>), dim3(1), dim3(256), lds4, stream, t, pods, c, s0, P, K, GLp, lists, on, ok, st, diag); \
+        } break;
         QS_RES(1) QS_RES(2) QS_RES(4) QS_RES(8) QS_RES(16)
 #undef QS_RES
         default: return hipErrorInvalidValue;

@@ -22,8 +22,9 @@ struct HostRow {
 // Lookahead geometry: window K pods, list length L (= K), G node chunks of `chunk` nodes per pod,
 // E nodes per lane in the select kernel (256-thread blocks).
 // epl = list entries per resolver lane (power of two); a pod's lists occupy 64*epl entries.
+// waves = resolver geometry: 1 (single-wave) or 4 (pipelined four-wave resolver).
 struct LaGeom {
-    uint32_t K, L, G, E, chunk, epl;
+    uint32_t K, L, G, E, chunk, epl, waves;
 };
 
 hipError_t launch_persistent(const DevTable &t, const DPod *pods, const DPodX *podx, uint32_t P,
