@@ -35,6 +35,12 @@
 extern "C" {
 #endif
 
+#if defined(__GNUC__)
+#define QS_API __attribute__((visibility("default")))
+#else
+#define QS_API
+#endif
+
 #define QS_ABI_VERSION 1
 #define QS_MAX_EXT 2   /* extended resources per node/pod (e.g. amd.com/gpu) */
 #define QS_MAX_TERMS 4 /* node-affinity terms per pod (required OR-terms, preferred terms) */
@@ -136,55 +142,55 @@ typedef struct qs_ctx qs_ctx;
 typedef struct qs_stream qs_stream;
 
 /* ---- lifecycle ---- */
-void qs_config_default(qs_config *cfg);
-qs_status qs_open(const qs_config *cfg, int device, qs_ctx **out);
+QS_API void qs_config_default(qs_config *cfg);
+QS_API qs_status qs_open(const qs_config *cfg, int device, qs_ctx **out);
 /* Sharded context for one rank of `world` (one process per GPU).  nccl_id = 128 bytes from
  * qs_dist_unique_id on rank 0, broadcast by the caller.  The node table is sharded by contiguous
  * ranges; the per-window exchange runs on RCCL over xGMI. */
-qs_status qs_open_shard(const qs_config *cfg, int device, int rank, int world,
+QS_API qs_status qs_open_shard(const qs_config *cfg, int device, int rank, int world,
                         const uint8_t nccl_id[128], qs_ctx **out);
-qs_status qs_dist_unique_id(uint8_t out[128]);
-qs_status qs_close(qs_ctx *ctx);
-const char *qs_last_error(const qs_ctx *ctx);
-const char *qs_version(void);
+QS_API qs_status qs_dist_unique_id(uint8_t out[128]);
+QS_API qs_status qs_close(qs_ctx *ctx);
+QS_API const char *qs_last_error(const qs_ctx *ctx);
+QS_API const char *qs_version(void);
 
 /* ---- node table (device-resident SoA, host mirror authoritative) ---- */
-qs_status qs_nodes_load(qs_ctx *ctx, const qs_node_soa *nodes, uint32_t n);
-qs_status qs_nodes_read(qs_ctx *ctx, const qs_node_soa_out *out, uint32_t n);
-qs_status qs_node_upsert(qs_ctx *ctx, uint32_t idx, const qs_node_row *row, uint64_t generation);
+QS_API qs_status qs_nodes_load(qs_ctx *ctx, const qs_node_soa *nodes, uint32_t n);
+QS_API qs_status qs_nodes_read(qs_ctx *ctx, const qs_node_soa_out *out, uint32_t n);
+QS_API qs_status qs_node_upsert(qs_ctx *ctx, uint32_t idx, const qs_node_row *row, uint64_t generation);
 /* Device-side snapshot of the whole node table (checkpoint/resume; bench resets between steps). */
-qs_status qs_table_save(qs_ctx *ctx);
-qs_status qs_table_restore(qs_ctx *ctx);
-qs_status qs_reserve(qs_ctx *ctx, uint32_t node, const qs_pod *pod);
-qs_status qs_unreserve(qs_ctx *ctx, uint32_t node, const qs_pod *pod);
+QS_API qs_status qs_table_save(qs_ctx *ctx);
+QS_API qs_status qs_table_restore(qs_ctx *ctx);
+QS_API qs_status qs_reserve(qs_ctx *ctx, uint32_t node, const qs_pod *pod);
+QS_API qs_status qs_unreserve(qs_ctx *ctx, uint32_t node, const qs_pod *pod);
 
 /* ---- one pod, all nodes (framework-embedded path) ----
  * feasible_n (nullable): 1/0 per node; score_n (nullable): [n][4] {LeastAllocated, Balanced,
  * TaintToleration, NodeAffinity} normalized plugin scores (0 where infeasible); total_n (nullable):
  * QoS-weighted total per node (-1 where infeasible); best: node index of spec S7 or -1. */
-qs_status qs_score_pod(qs_ctx *ctx, const qs_pod *pod, uint8_t *feasible_n, int32_t *score_n,
+QS_API qs_status qs_score_pod(qs_ctx *ctx, const qs_pod *pod, uint8_t *feasible_n, int32_t *score_n,
                        int32_t *total_n, int32_t *best);
 
 /* ---- exact stream ---- */
-qs_status qs_schedule_stream(qs_ctx *ctx, const qs_pod *pods, uint32_t p, qs_mode mode,
+QS_API qs_status qs_schedule_stream(qs_ctx *ctx, const qs_pod *pods, uint32_t p, qs_mode mode,
                              int32_t *placement_p, qs_stats *stats);
 /* Split form: prepare (host precompute + H2D), run (device only, timed; may run again, e.g. after
  * qs_table_restore), results (D2H of the last run). */
-qs_status qs_stream_prepare(qs_ctx *ctx, const qs_pod *pods, uint32_t p, qs_stream **out);
-qs_status qs_stream_run(qs_ctx *ctx, qs_stream *s, qs_mode mode, qs_stats *stats);
-qs_status qs_stream_results(qs_ctx *ctx, qs_stream *s, int32_t *placement_p, uint64_t *best_key_p);
-qs_status qs_stream_free(qs_ctx *ctx, qs_stream *s);
+QS_API qs_status qs_stream_prepare(qs_ctx *ctx, const qs_pod *pods, uint32_t p, qs_stream **out);
+QS_API qs_status qs_stream_run(qs_ctx *ctx, qs_stream *s, qs_mode mode, qs_stats *stats);
+QS_API qs_status qs_stream_results(qs_ctx *ctx, qs_stream *s, int32_t *placement_p, uint64_t *best_key_p);
+QS_API qs_status qs_stream_free(qs_ctx *ctx, qs_stream *s);
 /* Per-pod device timestamps (100 MHz s_memrealtime ticks, stream order; record_timestamps = 1). */
-qs_status qs_stream_stamps(qs_ctx *ctx, qs_stream *s, uint64_t *stamps_p);
+QS_API qs_status qs_stream_stamps(qs_ctx *ctx, qs_stream *s, uint64_t *stamps_p);
 
 /* ---- host helpers (spec S2/S3, spec/synth.md) ---- */
-qs_status qs_pod_from_containers(const qs_container *c, uint32_t nc, const int64_t *overhead_cpu_mem,
+QS_API qs_status qs_pod_from_containers(const qs_container *c, uint32_t nc, const int64_t *overhead_cpu_mem,
                                  qs_pod *out);
-int32_t qs_compute_qos(const qs_container *c, uint32_t nc);
+QS_API int32_t qs_compute_qos(const qs_container *c, uint32_t nc);
 /* sizeof of the ABI structs for binding self-checks: 0 config, 1 node_soa, 2 node_row, 3 pod,
  * 4 container, 5 stats. */
-size_t qs_struct_size(int which);
-qs_status qs_synth_generate(int config, uint64_t seed, uint32_t n, uint32_t p,
+QS_API size_t qs_struct_size(int which);
+QS_API qs_status qs_synth_generate(int config, uint64_t seed, uint32_t n, uint32_t p,
                             const qs_node_soa_out *nodes, qs_pod *pods);
 
 #ifdef __cplusplus

@@ -39,9 +39,13 @@ def test_struct_sizes():
 
 def test_no_symbols_leak_torch():
     # the boundary is plain C: no torch/c10 symbols in the library's dynamic table
-    out = os.popen(f"nm -D --defined-only {_abi.LIB_PATH}").read()
-    assert "c10" not in out and "torch" not in out
-    assert "qs_schedule_stream" in out
+    names = [ln.split()[-1] for ln in os.popen(f"nm -D --defined-only {_abi.LIB_PATH}").read().splitlines()
+             if ln.strip()]
+    assert not any("c10" in n or "torch" in n for n in names)
+    assert "qs_schedule_stream" in names
+    # only the C ABI is exported (the library builds with -fvisibility=hidden)
+    text_syms = [n for n in names if not n.startswith("_")]
+    assert all(n.startswith("qs_") for n in text_syms), text_syms
 
 
 def test_config_default():
