@@ -55,10 +55,43 @@ def cpu_baseline(nodes, pods, sample):
             "evals_per_s": round(sample * N_NODES / dt, 1)}
 
 
-def kernel_profile(sched, stream):
-    """Per-kernel average durations on the library's stream via rocprof-free HIP events is not
-    exposed by the ABI; use the whole-run event time per window instead (documented in DESIGN.md)."""
-    return None
+def kernel_profile(nodes, pods, cfg, device):
+    """Untimed run with config.profile_kernels = 1: every launch bracketed by HIP events on the
+    library's own stream.  Returns {kernel: {"s": total seconds, "launches": n}}."""
+    s = qsched.Scheduler(dict(cfg, profile_kernels=1), device=device)
+    s.load_nodes(nodes)
+    st = s.prepare(pods)
+    stats = st.run()
+    st.free()
+    s.close()
+    return stats["kernels"]
+
+
+def pmc_traffic(kernel_prefix):
+    """HBM bytes per launch of `kernel_prefix` from the committed rocprofv3 PMC passes
+    (profiles/*_pmc_fetch.csv, *_pmc_write.csv): FETCH_SIZE x 2 (gfx950 correction,
+    MI355X_MICROARCH.md:298) + WRITE_SIZE, both in KiB.  None if not collected."""
+    import csv
+    import glob
+    tot, n = {}, {}
+    for kind in ("fetch", "write"):
+        files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_{kind}.csv")))
+        if not files:
+            return None
+        for row in csv.DictReader(open(files[-1])):
+            if not row.get("Kernel_Name", "").split("(")[0].split("<")[0].endswith(kernel_prefix):
+                continue
+            name = row.get("Counter_Name", "")
+            v = float(row.get("Counter_Value", 0))
+            if name == "FETCH_SIZE":
+                tot["f"] = tot.get("f", 0.0) + 2 * v * 1024
+                n["f"] = n.get("f", 0) + 1
+            elif name == "WRITE_SIZE":
+                tot["w"] = tot.get("w", 0.0) + v * 1024
+                n["w"] = n.get("w", 0) + 1
+    if not n.get("f") or not n.get("w"):
+        return None
+    return tot["f"] / n["f"] + tot["w"] / n["w"]
 
 
 def main():
@@ -128,14 +161,21 @@ def main():
     except Exception as e:  # diagnostic only
         print(f"# timestamp run failed: {e}", file=sys.stderr)
 
+    kp = kernel_profile(nodes, pods, cfg, local) if rank == 0 else {}
     if rank == 0:
         total_pods = N_PODS * a.steps * world
         value = total_pods / elapsed
         ms_per_step = elapsed / a.steps * 1e3
-        # roofline: the whole exact stream (one qs_stream_run) as the unit of device work;
-        # algorithmic bytes = P * N * B_node per step; duration = device event time.
-        dev_step = dev_wall / a.steps
-        achieved = N_PODS * N_NODES * B_NODE / dev_step / 1e9
+        # roofline of the dominant kernel (most device time in the profiled run): algorithmic
+        # bytes = (pod x node evaluations it completes per launch) x B_node;
+        # each launch of resolve/select/persistent covers its pods against all N nodes.
+        dom = max(kp, key=lambda k: kp[k]["s"]) if kp else None
+        avg_s = kp[dom]["s"] / kp[dom]["launches"] if dom else dev_wall / a.steps
+        units = N_PODS * N_NODES / (kp[dom]["launches"] if dom else 1)
+        achieved = units * B_NODE / avg_s / 1e9
+        kname = {"resolve": "k_la_resolve4", "select": "k_la_select", "persistent": "k_persistent",
+                 "scan": "k_scan_key"}.get(dom, dom)
+        traffic = pmc_traffic(kname) if dom else None
         out = {
             "metric": "pods scheduled/sec (exact sequential stream, 5k nodes x 100k pods)",
             "value": round(value, 1), "unit": "pods/s", "n_gpus": world, "steps": a.steps,
@@ -152,9 +192,10 @@ def main():
             "unschedulable_frac": round(unsched, 5),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "traffic": None,
-                         "kernel": f"whole {last['engine_used']} stream per step "
-                                   f"({last['batches']} windows)"},
+                         "traffic": None if traffic is None else round(traffic),
+                         "kernel": kname, "avg_launch_us": round(avg_s * 1e6, 3),
+                         "bytes_per_launch": round(units * B_NODE)},
+            "kernels_us_per_step": {k: round(v["s"] * 1e6, 1) for k, v in kp.items()},
         }
         if not a.no_cpu:
             out["cpu_baseline"] = cpu_baseline(nodes, pods, a.cpu_sample)

@@ -390,6 +390,43 @@ qs_status guarded(qs_ctx *c, F &&f) {
     }
 }
 
+// Per-launch HIP-event timing on the library's stream (config.profile_kernels).
+struct KernelTimer {
+    bool on;
+    hipStream_t stream;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[4];
+    double secs[4] = {0, 0, 0, 0};
+    uint64_t count[4] = {0, 0, 0, 0};
+    KernelTimer(bool o, hipStream_t s) : on(o), stream(s) {}
+    void begin(int k) {
+        if (!on) return;
+        hipEvent_t a, b;
+        HIPCHK(hipEventCreate(&a));
+        HIPCHK(hipEventCreate(&b));
+        HIPCHK(hipEventRecord(a, stream));
+        ev[k].push_back({a, b});
+    }
+    void end(int k) {
+        if (!on) return;
+        HIPCHK(hipEventRecord(ev[k].back().second, stream));
+    }
+    void finish() {
+        if (!on) return;
+        HIPCHK(hipStreamSynchronize(stream));
+        for (int k = 0; k < 4; k++) {
+            for (auto &e : ev[k]) {
+                float ms = 0.f;
+                HIPCHK(hipEventElapsedTime(&ms, e.first, e.second));
+                secs[k] += ms * 1e-3;
+                count[k]++;
+                (void)hipEventDestroy(e.first);
+                (void)hipEventDestroy(e.second);
+            }
+            ev[k].clear();
+        }
+    }
+};
+
 int pick_engine(const qs_ctx *c, uint32_t n) {
     int e = c->cfg.engine;
     const uint32_t feat = c->dc.feat;
@@ -407,7 +444,7 @@ int pick_engine(const qs_ctx *c, uint32_t n) {
 }
 
 uint32_t la_window(const qs_ctx *c) {
-    int K = c->cfg.lookahead > 0 ? c->cfg.lookahead : 64;
+    int K = c->cfg.lookahead > 0 ? c->cfg.lookahead : 32;  // measured best on config 2
     return (uint32_t)std::min(64, std::max(1, K));
 }
 
@@ -689,6 +726,8 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
         hipEvent_t e0, e1;
         HIPCHK(hipEventCreate(&e0));
         HIPCHK(hipEventCreate(&e1));
+        // config.profile_kernels: bracket every launch with events (untimed diagnostic runs)
+        KernelTimer kt(c->cfg.profile_kernels != 0, c->stream);
         HIPCHK(hipEventRecord(e0, c->stream));
         if (P > 0 && n == 0) {
             HIPCHK(hipMemsetAsync(on, 0xFF, 4 * (size_t)P, c->stream));
@@ -697,13 +736,18 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
             const DPod *dp = s->d_pods.as<DPod>();
             const DPodX *dx = s->d_podx.as<DPodX>();
             if (eng == QS_ENGINE_PERSISTENT) {
+                kt.begin(0);
                 HIPCHK(launch_persistent(c->dt, dp, dx, P, c->dc, on, ok, st, c->stream));
+                kt.end(0);
                 batches = 1;
             } else if (eng == QS_ENGINE_SCAN) {
                 HIPCHK(hipMemsetAsync(c->scratch.p, 0, scan_scratch_bytes(), c->stream));
-                for (uint32_t k = 0; k < P; k++)
+                for (uint32_t k = 0; k < P; k++) {
+                    kt.begin(1);
                     HIPCHK(launch_scan_pod(c->dt, dp, dx, k, c->dc, c->scratch.p, on, ok, st,
                                            nullptr, nullptr, nullptr, true, c->stream));
+                    kt.end(1);
+                }
                 batches = P;
             } else {
                 LaGeom geo = la_geometry(n, la_window(c));
@@ -722,8 +766,14 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                     diag = c->diag.as<uint64_t>();
                 }
                 for (uint32_t s0 = 0; s0 < P; s0 += geo.K) {
+                    kt.begin(2);
                     HIPCHK(launch_la_window(c->dt, dp, s0, P, c->dc, geo, c->lists.as<uint64_t>(), on,
-                                            ok, st, diag, c->stream));
+                                            ok, st, diag, c->stream, 1));
+                    kt.end(2);
+                    kt.begin(3);
+                    HIPCHK(launch_la_window(c->dt, dp, s0, P, c->dc, geo, c->lists.as<uint64_t>(), on,
+                                            ok, st, diag, c->stream, 2));
+                    kt.end(3);
                     ++batches;
                 }
                 if (diag_on) {
@@ -746,8 +796,13 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
         (void)hipEventDestroy(e1);
         s->ran = true;
         c->mirror_stale = true;
+        kt.finish();
         if (stats) {
             std::memset(stats, 0, sizeof(*stats));
+            for (int k = 0; k < 4; k++) {
+                stats->kernel_s[k] = kt.secs[k];
+                stats->kernel_launches[k] = kt.count[k];
+            }
             stats->pods = P;
             stats->evals = (uint64_t)P * n;
             stats->wall_s = ms * 1e-3;

@@ -826,42 +826,48 @@ size_t scan_scratch_bytes() { return sizeof(ScanScratch); }
 template <uint32_t F>
 static hipError_t la_window_f(const DevTable &t, const DPod *pods, uint32_t s0, uint32_t P,
                               const DevCfg &c, const LaGeom &geo, uint64_t *lists, int32_t *on,
-                              uint64_t *ok, uint64_t *st, uint64_t *diag, hipStream_t stream) {
+                              uint64_t *ok, uint64_t *st, uint64_t *diag, hipStream_t stream,
+                              int part) {
     const uint32_t K = geo.K, G = geo.G, L = geo.L, GLp = geo.epl * 64;
     const uint32_t kw = min(K, P - s0);
-    const dim3 grid(kw * G);
-    switch (geo.E) {
+    if (part & 1) {
+        const dim3 grid(kw * G);
+        switch (geo.E) {
 #define QS_SEL(EE) case EE: hipLaunchKernelGGL((k_la_select<256, EE, F>), grid, dim3(256), 0, stream, t, pods, c, s0, P, G, L, geo.chunk, GLp, lists); break;
-        QS_SEL(1) QS_SEL(2) QS_SEL(3) QS_SEL(4) QS_SEL(5) QS_SEL(6) QS_SEL(8) QS_SEL(10) QS_SEL(12) QS_SEL(16)
+            QS_SEL(1) QS_SEL(2) QS_SEL(3) QS_SEL(4) QS_SEL(5) QS_SEL(6) QS_SEL(8) QS_SEL(10) QS_SEL(12) QS_SEL(16)
 #undef QS_SEL
-        default: return hipErrorInvalidValue;
+            default: return hipErrorInvalidValue;
+        }
+        QS_RET(hipGetLastError());
     }
-    QS_RET(hipGetLastError());
-    const size_t bm = (((t.n + 31) / 32 + 3) & ~3u) * 4;
-    const size_t lds = bm + sizeof(Row) + sizeof(RowX);
-    const size_t lds4 = bm + 5 * 2 * 64 * 8 + 2 * 64 * (sizeof(Row) + sizeof(int4)) + 2 * sizeof(ResPub) + 64 * 4 + 64 * sizeof(DPod);
-    switch (geo.epl) {
+    if (part & 2) {
+        const size_t bm = (((t.n + 31) / 32 + 3) & ~3u) * 4;
+        const size_t lds = bm + sizeof(Row) + sizeof(RowX);
+        const size_t lds4 = bm + 5 * 2 * 64 * 8 + 2 * 64 * (sizeof(Row) + sizeof(int4)) + 2 * sizeof(ResPub) + 64 * 4 + 64 * sizeof(DPod);
+        switch (geo.epl) {
 #define QS_RES(EP) case EP: \
-        if (geo.waves == 1) { \
-            if (diag) hipLaunchKernelGGL((k_la_resolve<F, EP, true>), dim3(1), dim3(64), lds, stream, t, pods, c, s0, P, K, GLp, lists, on, ok, st, diag); \
-            else hipLaunchKernelGGL((k_la_resolve<F, EP, false>), dim3(1), dim3(64), lds, stream, t, pods, c, s0, P, K, GLp, lists, on, ok, st, diag); \
-        } else { \
-            if (diag) hipLaunchKernelGGL((k_la_resolve4<F, EP, true>), dim3(1), dim3(256), lds4, stream, t, pods, c, s0, P, K, GLp, lists, on, ok, st, diag); \
-            else hipLaunchKernelGGL((k_la_resolve4<F, EP, false>), dim3(1), dim3(256), lds4, stream, t, pods, c, s0, P, K, GLp, lists, on, ok, st, diag); \
-        } break;
-        QS_RES(1) QS_RES(2) QS_RES(4) QS_RES(8) QS_RES(16)
+            if (geo.waves == 1) { \
+                if (diag) hipLaunchKernelGGL((k_la_resolve<F, EP, true>), dim3(1), dim3(64), lds, stream, t, pods, c, s0, P, K, GLp, lists, on, ok, st, diag); \
+                else hipLaunchKernelGGL((k_la_resolve<F, EP, false>), dim3(1), dim3(64), lds, stream, t, pods, c, s0, P, K, GLp, lists, on, ok, st, diag); \
+            } else { \
+                if (diag) hipLaunchKernelGGL((k_la_resolve4<F, EP, true>), dim3(1), dim3(256), lds4, stream, t, pods, c, s0, P, K, GLp, lists, on, ok, st, diag); \
+                else hipLaunchKernelGGL((k_la_resolve4<F, EP, false>), dim3(1), dim3(256), lds4, stream, t, pods, c, s0, P, K, GLp, lists, on, ok, st, diag); \
+            } break;
+            QS_RES(1) QS_RES(2) QS_RES(4) QS_RES(8) QS_RES(16)
 #undef QS_RES
-        default: return hipErrorInvalidValue;
+            default: return hipErrorInvalidValue;
+        }
     }
     return hipGetLastError();
 }
 
 hipError_t launch_la_window(const DevTable &t, const DPod *pods, uint32_t s0, uint32_t P,
                             const DevCfg &c, const LaGeom &geo, uint64_t *lists, int32_t *on,
-                            uint64_t *ok, uint64_t *st, uint64_t *diag, hipStream_t stream) {
+                            uint64_t *ok, uint64_t *st, uint64_t *diag, hipStream_t stream,
+                            int part) {
     if (c.feat & kFeatNorm) return hipErrorInvalidValue;
-    if (c.feat & kFeatExt) return la_window_f<kFeatExt>(t, pods, s0, P, c, geo, lists, on, ok, st, diag, stream);
-    return la_window_f<0>(t, pods, s0, P, c, geo, lists, on, ok, st, diag, stream);
+    if (c.feat & kFeatExt) return la_window_f<kFeatExt>(t, pods, s0, P, c, geo, lists, on, ok, st, diag, stream, part);
+    return la_window_f<0>(t, pods, s0, P, c, geo, lists, on, ok, st, diag, stream, part);
 }
 
 LaGeom la_geometry(uint32_t n, uint32_t K) {

@@ -42,7 +42,7 @@ LaGeom la_geometry(uint32_t n, uint32_t K);
 hipError_t launch_la_window(const DevTable &t, const DPod *pods, uint32_t s0, uint32_t P,
                             const DevCfg &c, const LaGeom &geo, uint64_t *lists, int32_t *out_node,
                             uint64_t *out_key, uint64_t *stamps, uint64_t *diag,
-                            hipStream_t stream);
+                            hipStream_t stream, int part = 3);  // part: 1 select, 2 resolve
 
 __global__ void k_set_row(DevTable t, uint32_t i, HostRow v, uint32_t feat);
 

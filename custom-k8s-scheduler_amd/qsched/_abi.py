@@ -46,7 +46,7 @@ class QsConfig(ctypes.Structure):
                 ("enable_taint", ctypes.c_int32), ("enable_affinity", ctypes.c_int32),
                 ("balanced_skip_besteffort", ctypes.c_int32), ("qos_sort", ctypes.c_int32),
                 ("lookahead", ctypes.c_int32), ("record_timestamps", ctypes.c_int32),
-                ("reserved", ctypes.c_int32 * 8)]
+                ("profile_kernels", ctypes.c_int32), ("reserved", ctypes.c_int32 * 7)]
 
 
 _NODE_COLS = ["alloc_cpu", "alloc_mem", "alloc_ext", "max_pods", "req_cpu", "req_mem", "req_ext",
@@ -82,11 +82,17 @@ class QsStats(ctypes.Structure):
                 ("wall_s", ctypes.c_double), ("h2d_s", ctypes.c_double), ("d2h_s", ctypes.c_double),
                 ("p50_cycle_us", ctypes.c_double), ("p99_cycle_us", ctypes.c_double),
                 ("max_cycle_us", ctypes.c_double), ("engine_used", ctypes.c_int32),
-                ("reserved", ctypes.c_int32 * 7)]
+                ("reserved", ctypes.c_int32 * 7), ("kernel_s", ctypes.c_double * 4),
+                ("kernel_launches", ctypes.c_uint64 * 4)]
+
+    KERNELS = ("persistent", "scan", "select", "resolve")
 
     def as_dict(self):
-        d = {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved"}
+        d = {f: getattr(self, f) for f, _ in self._fields_
+             if f not in ("reserved", "kernel_s", "kernel_launches")}
         d["engine_used"] = ENGINE_NAMES.get(self.engine_used, self.engine_used)
+        d["kernels"] = {k: {"s": self.kernel_s[i], "launches": int(self.kernel_launches[i])}
+                        for i, k in enumerate(self.KERNELS) if self.kernel_launches[i]}
         return d
 
 

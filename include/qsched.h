@@ -81,7 +81,8 @@ typedef struct qs_config {
     int32_t qos_sort;            /* 1 = QoSSort order (spec S8), 0 = arrival order */
     int32_t lookahead;           /* pods per lookahead window (0 = default) */
     int32_t record_timestamps;   /* 1 = per-pod device timestamps for p50/p99 cycle latency */
-    int32_t reserved[8];
+    int32_t profile_kernels;     /* 1 = time every kernel launch with HIP events (qs_stats.kernel_s) */
+    int32_t reserved[7];
 } qs_config;
 
 /* Canonical node table, structure of arrays, n entries each.  alloc_ext/req_ext are [n][QS_MAX_EXT],
@@ -136,6 +137,10 @@ typedef struct qs_stats {
     double p50_cycle_us, p99_cycle_us, max_cycle_us; /* per-pod decision interval (record_timestamps) */
     int32_t engine_used;
     int32_t reserved[7];
+    /* per-kernel device time (config.profile_kernels = 1; HIP events on the library's stream):
+     * [0] persistent, [1] scan (all per-pod kernels), [2] lookahead select, [3] lookahead resolve */
+    double kernel_s[4];
+    uint64_t kernel_launches[4];
 } qs_stats;
 
 typedef struct qs_ctx qs_ctx;
