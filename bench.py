@@ -68,30 +68,18 @@ def kernel_profile(nodes, pods, cfg, device):
 
 
 def pmc_traffic(kernel_prefix):
-    """HBM bytes per launch of `kernel_prefix` from the committed rocprofv3 PMC passes
-    (profiles/*_pmc_fetch.csv, *_pmc_write.csv): FETCH_SIZE x 2 (gfx950 correction,
-    MI355X_MICROARCH.md:298) + WRITE_SIZE, both in KiB.  None if not collected."""
+    """HBM bytes per launch of `kernel_prefix` from the committed rocprofv3 PMC summary
+    (profiles/*_pmc_summary.csv, tools/summarize_pmc.py: separate FETCH_SIZE and WRITE_SIZE
+    passes, 2 x FETCH_SIZE + WRITE_SIZE per MI355X_MICROARCH.md:298).  None if not collected."""
     import csv
     import glob
-    tot, n = {}, {}
-    for kind in ("fetch", "write"):
-        files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_{kind}.csv")))
-        if not files:
-            return None
-        for row in csv.DictReader(open(files[-1])):
-            if not row.get("Kernel_Name", "").split("(")[0].split("<")[0].endswith(kernel_prefix):
-                continue
-            name = row.get("Counter_Name", "")
-            v = float(row.get("Counter_Value", 0))
-            if name == "FETCH_SIZE":
-                tot["f"] = tot.get("f", 0.0) + 2 * v * 1024
-                n["f"] = n.get("f", 0) + 1
-            elif name == "WRITE_SIZE":
-                tot["w"] = tot.get("w", 0.0) + v * 1024
-                n["w"] = n.get("w", 0) + 1
-    if not n.get("f") or not n.get("w"):
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.csv")))
+    if not files:
         return None
-    return tot["f"] / n["f"] + tot["w"] / n["w"]
+    for row in csv.DictReader(open(files[-1])):
+        if row["kernel"].split("<")[0].endswith(kernel_prefix):
+            return float(row["hbm_bytes_per_launch"])
+    return None
 
 
 def main():
