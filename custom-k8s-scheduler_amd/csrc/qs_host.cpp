@@ -753,6 +753,9 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                 LaGeom geo = la_geometry(n, la_window(c));
                 static const char *rw = getenv("QS_RESOLVER_WAVES");  // 1 = single-wave resolver
                 geo.waves = (rw && rw[0] == '1') ? 1u : 4u;
+                int64_t wmax = 0;
+                for (int q = 0; q < 3; q++) wmax = std::max<int64_t>(wmax, (int64_t)c->cfg.w_fit[q] + c->cfg.w_bal[q]);
+                geo.k32 = (100 * wmax + 1 < 1024 && n <= (1u << 22)) ? 1u : 0u;
                 if (geo.G == 0) fail(QS_EINVAL, "no lookahead geometry for this table size");
                 const size_t lbytes = 8ull * geo.K * 64 * geo.epl;
                 c->lists.ensure(lbytes);

@@ -490,8 +490,22 @@ struct alignas(16) ResPub {
     uint32_t nd_old; // lane of the new slot
     uint32_t pad[2];
 };
+// One 32-byte LDS read of the published winner (two ds_read_b128 issued together; reading the
+// fields lazily under branches serialised four LDS round trips).
+__device__ __forceinline__ ResPub read_pub(const ResPub *p) {
+    const uint4 a = reinterpret_cast<const uint4 *>(p)[0];
+    const uint4 b = reinterpret_cast<const uint4 *>(p)[1];
+    ResPub r;
+    r.ks = ((uint64_t)a.y << 32) | a.x;
+    r.w = a.z;
+    r.slot = (int32_t)a.w;
+    r.src = (int32_t)b.x;
+    r.nd_old = b.y;
+    r.pad[0] = r.pad[1] = 0;
+    return r;
+}
 
-template <uint32_t F, int EPL, bool DIAG>
+template <uint32_t F, int EPL, bool DIAG, bool K32>
 __global__ __launch_bounds__(256) void k_la_resolve4(DevTable t, const DPod *__restrict__ pods,
                                                      DevCfg c, uint32_t s0, uint32_t P,
                                                      uint32_t K, uint32_t GLp,
@@ -534,23 +548,33 @@ __global__ __launch_bounds__(256) void k_la_resolve4(DevTable t, const DPod *__r
         // ---- D: pod i's winner from the precomputed keys ---------------------------------------
         uint32_t nd = 0, didx = 0xFFFFFFFFu;
         uint64_t res_key = 0, res_stamp = 0;
+        ResPub pv{0, 0xFFFFFFFFu, -1, -1, 0, {0, 0}};  // D produced it: kept in registers
         __syncthreads();  // prologue barrier (wave C publishes pod 0's candidates)
         for (uint32_t i = 0; i < kend; ++i) {
             QS_DIAG_BEGIN()
             const int par = i & 1, pp = par ^ 1;
-            const ResPub pv = pub[pp];
-            const bool pnew = pv.ks != 0 && pv.slot < 0;
-            uint64_t fk = 0;
-            if ((uint32_t)lane < nd) {
-                const uint64_t a = keyA[pp][lane], b = keyB[pp][lane];
-                const uint64_t sc = (lane == pv.slot) ? b : a;
-                fk = sc ? (sc | (uint64_t)(0xFFFFFFFFu - didx)) : 0ull;
-                if (pnew && (uint32_t)lane == pv.nd_old) fk = keyC[pp][pv.src];
-            }
+            // every LDS read of the step is independent of this step: one batch, one wait
+            const uint64_t a = keyA[pp][lane], b = keyB[pp][lane], cl = keyC[pp][lane];
             const uint64_t e1 = C1[pp][lane], e2 = C2[pp][lane];
+            const bool pnew = pv.ks != 0 && pv.slot < 0;
+            const uint64_t sc = (lane == pv.slot) ? b : a;
+            uint64_t fk = ((uint32_t)lane < nd && sc) ? (sc | (uint64_t)(0xFFFFFFFFu - didx)) : 0ull;
+            if (pnew) {
+                const uint64_t cw = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(cl >> 32), pv.src) << 32) |
+                                    (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)cl, pv.src);
+                if ((uint32_t)lane == pv.nd_old) fk = cw;
+            }
             const uint64_t cand = (pv.ks != 0 && e1 != 0 && key_node(e1) == pv.w) ? e2 : e1;
             const uint64_t best = fk > cand ? fk : cand;
-            const uint64_t ks = wave_max_u64(best);
+            uint64_t ks;
+            if (K32) {  // (score+1) < 2^10 and n <= 2^22: one 32-bit reduction
+                const uint32_t tv = (uint32_t)(best >> 32);
+                const uint32_t k32 = tv ? (tv << 22) | (0x3FFFFFu - key_node(best)) : 0u;
+                const uint32_t m = wave_max_u32(k32);
+                ks = m ? (((uint64_t)(m >> 22) << 32) | (uint64_t)(0xFFFFFFFFu - (0x3FFFFFu - (m & 0x3FFFFFu)))) : 0ull;
+            } else {
+                ks = wave_max_u64(best);
+            }
             ResPub np{ks, ks ? key_node(ks) : 0xFFFFFFFFu, -1, -1, nd, {0, 0}};
             if (ks) {
                 const uint64_t own = __ballot((uint32_t)lane < nd && didx == np.w);
@@ -559,10 +583,10 @@ __global__ __launch_bounds__(256) void k_la_resolve4(DevTable t, const DPod *__r
                 } else {
                     np.src = (int32_t)__builtin_ctzll(__ballot(cand == ks));
                     if ((uint32_t)lane == nd) didx = np.w;
-                    if (lane == 0) dirty[np.w >> 5] |= 1u << (np.w & 31);
                     ++nd;
                 }
             }
+            pv = np;
             if (lane == 0) pub[par] = np;
             if ((uint32_t)lane == i) {
                 res_key = ks;
@@ -603,7 +627,7 @@ __global__ __launch_bounds__(256) void k_la_resolve4(DevTable t, const DPod *__r
         for (uint32_t i = 0; i < kend; ++i) {
             QS_DIAG_BEGIN()
             const int par = i & 1, pp = par ^ 1;
-            const ResPub pv = pub[pp];
+            const ResPub pv = read_pub(&pub[pp]);
             if (i > 0) apply(pv, pp, wpods[i - 1]);
             if (i + 1 < kend) {
                 const DPod pn1 = wpods[i + 1];
@@ -619,7 +643,7 @@ __global__ __launch_bounds__(256) void k_la_resolve4(DevTable t, const DPod *__r
             QS_DIAG_END()
             __syncthreads();
         }
-        if (wv == 1) apply(pub[(kend - 1) & 1], (kend - 1) & 1, wpods[kend - 1]);
+        if (wv == 1) apply(read_pub(&pub[(kend - 1) & 1]), (kend - 1) & 1, wpods[kend - 1]);
         __syncthreads();  // slotnode written by wave D
         if (wv == 1 && (uint32_t)lane < nd) {
             const uint32_t node = slotnode[lane];
@@ -667,7 +691,8 @@ __global__ __launch_bounds__(256) void k_la_resolve4(DevTable t, const DPod *__r
         auto step = [&](uint32_t i, uint64_t(&en)[EPL]) {
             QS_DIAG_BEGIN()
             const int par = i & 1, pp = par ^ 1;
-            const ResPub pv = pub[pp];
+            const ResPub pv = read_pub(&pub[pp]);
+            if (lane == 0 && pv.ks != 0 && pv.slot < 0) dirty[pv.w >> 5] |= 1u << (pv.w & 31);
             const bool use2 = pv.ks != 0 && c1 != 0 && key_node(c1) == pv.w;
             const uint64_t cc = use2 ? c2 : c1;
             const Row crow = sel_row(use2, r2, r1);
@@ -850,8 +875,9 @@ static hipError_t la_window_f(const DevTable &t, const DPod *pods, uint32_t s0, 
                 if (diag) hipLaunchKernelGGL((k_la_resolve<F, EP, true>), dim3(1), dim3(64), lds, stream, t, pods, c, s0, P, K, GLp, lists, on, ok, st, diag); \
                 else hipLaunchKernelGGL((k_la_resolve<F, EP, false>), dim3(1), dim3(64), lds, stream, t, pods, c, s0, P, K, GLp, lists, on, ok, st, diag); \
             } else { \
-                if (diag) hipLaunchKernelGGL((k_la_resolve4<F, EP, true>), dim3(1), dim3(256), lds4, stream, t, pods, c, s0, P, K, GLp, lists, on, ok, st, diag); \
-                else hipLaunchKernelGGL((k_la_resolve4<F, EP, false>), dim3(1), dim3(256), lds4, stream, t, pods, c, s0, P, K, GLp, lists, on, ok, st, diag); \
+                if (diag) hipLaunchKernelGGL((k_la_resolve4<F, EP, true, false>), dim3(1), dim3(256), lds4, stream, t, pods, c, s0, P, K, GLp, lists, on, ok, st, diag); \
+                else if (geo.k32) hipLaunchKernelGGL((k_la_resolve4<F, EP, false, true>), dim3(1), dim3(256), lds4, stream, t, pods, c, s0, P, K, GLp, lists, on, ok, st, diag); \
+                else hipLaunchKernelGGL((k_la_resolve4<F, EP, false, false>), dim3(1), dim3(256), lds4, stream, t, pods, c, s0, P, K, GLp, lists, on, ok, st, diag); \
             } break;
             QS_RES(1) QS_RES(2) QS_RES(4) QS_RES(8) QS_RES(16)
 #undef QS_RES

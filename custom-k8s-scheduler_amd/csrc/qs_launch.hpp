@@ -23,8 +23,9 @@ struct HostRow {
 // E nodes per lane in the select kernel (256-thread blocks).
 // epl = list entries per resolver lane (power of two); a pod's lists occupy 64*epl entries.
 // waves = resolver geometry: 1 (single-wave) or 4 (pipelined four-wave resolver).
+// k32 = keys fit 32 bits ((max total + 1) < 2^10, n <= 2^22): one 32-bit wave reduction per pod.
 struct LaGeom {
-    uint32_t K, L, G, E, chunk, epl, waves;
+    uint32_t K, L, G, E, chunk, epl, waves, k32;
 };
 
 hipError_t launch_persistent(const DevTable &t, const DPod *pods, const DPodX *podx, uint32_t P,

@@ -89,3 +89,21 @@ def test_ext_resources_without_taints(oracle, engine):
     g = run_gpu(nodes, pods, {}, engine)
     o = run_oracle(oracle, nodes, pods, {})
     assert_same(g[:2], o[:2], g[2], o[2])
+
+
+@pytest.mark.parametrize("engine", ["persistent", "scan", "lookahead"])
+def test_custom_weights_parity(oracle, engine):
+    """Non-default plugin / resource weights (also exercises the 64-bit key reduction path)."""
+    cfg = dict(w_fit=(10, 20, 30), w_bal=(5, 7, 9), fit_weight_cpu=2, fit_weight_mem=3)
+    ocfg = dict(wc=2, wm=3, w_fit=(10, 20, 30), w_bal=(5, 7, 9))
+    nodes, pods = synth_generate(2, 1500, 6000)
+    g = run_gpu(nodes, pods, cfg, engine)
+    o = run_oracle(oracle, nodes, pods, ocfg)
+    assert_same(g[:2], o[:2], g[2], o[2])
+
+
+def test_balanced_skip_besteffort(oracle):
+    nodes, pods = synth_generate(2, 800, 4000)
+    g = run_gpu(nodes, pods, dict(balanced_skip_besteffort=1), "lookahead")
+    o = run_oracle(oracle, nodes, pods, dict(balanced_skip_besteffort=1))
+    assert_same(g[:2], o[:2], g[2], o[2])
