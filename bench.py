@@ -1,14 +1,20 @@
-"""bench.py — BASELINE.json metric: pods scheduled/s (+ pod×node evals/s, p99 pod latency) for the
-exact sequential stream at 5,000 nodes × 100,000 pods (configs[1]) on MI355X.
+"""bench.py — BASELINE.json metric: pods scheduled/s (+ pod×node evals/s, p99 pod latency) of the
+exact sequential stream, measured through libqsched's C ABI on MI355X.
+
+Workloads (BASELINE.json configs):
+  * N = 1 (default): configs[1] — 5,000 nodes × 100,000 pods on one GPU (the metric's config).
+    The line also carries a ``config3`` object: the 50,000-node × 1,000,000-pod stream on the same
+    single GPU, the N = 1 point of the config-3 scaling curve.
+  * N > 1 (torchrun, one rank per GPU): configs[2] — 50,000 nodes × 1,000,000 pods with the node
+    table sharded across the N ranks (qs_open_shard: contiguous node ranges, one RCCL all-gather of
+    top-L lists per lookahead window over xGMI).  Total work is fixed: ``scaling`` = "strong".
+  ``--workload config2|config3`` overrides (config2 at N > 1 = independent replicas, weak scaling).
 
 A *step* = restore the empty cluster on the device (qs_table_restore, a D2D copy) + run the whole
-100,000-pod exact stream through libqsched (qs_stream_run): inputs resident in HBM, every pod
-scheduled, placements left in HBM.  Timed: K steps bracketed by barrier + device sync; MAX over
-ranks.  N > 1 (torchrun): every rank runs its own independent config-2 cluster (replicas; the
-node-sharded config-3 path is DESIGN.md §6) and value = all ranks' pods / max time.
+exact stream (qs_stream_run): inputs resident in HBM, every pod scheduled, placements left in HBM.
+Timed: K steps bracketed by barrier + device sync on both sides; MAX over ranks.
 """
 import argparse
-import ctypes
 import json
 import os
 import sys
@@ -22,9 +28,17 @@ sys.path.insert(0, os.path.join(ROOT, "custom-k8s-scheduler_amd"))
 
 import qsched  # noqa: E402
 
-N_NODES, N_PODS = 5000, 100000
+WORKLOADS = {
+    # name: (generator config, nodes, pods, description)
+    "config2": (2, 5000, 100000, "config2: 5,000 nodes x 100,000 pods, exact sequential, "
+                                 "Fit+Balanced+QoS weights, percentageOfNodesToScore=100"),
+    "config3": (3, 50000, 1000000, "config3: 50,000 nodes x 1,000,000 pods, exact sequential, "
+                                   "node table sharded across ranks (RCCL all-gather per window)"),
+}
 B_NODE = 32  # algorithmic bytes per pod×node evaluation (8 int32 columns)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md:36 (spec); 6,290 GB/s measured
+KERNEL_NAMES = {"resolve": "k_la_resolve4", "select": "k_la_select", "persistent": "k_persistent",
+                "scan": "k_scan_key"}
 
 
 def parse():
@@ -32,39 +46,93 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="auto", choices=["auto", "config2", "config3"])
     ap.add_argument("--engine", default="auto")
     ap.add_argument("--lookahead", type=int, default=0)
     ap.add_argument("--cpu-sample", type=int, default=20000, help="pods in the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--no-config3", action="store_true", help="skip the N=1 config-3 reference point")
     return ap.parse_args()
 
 
-def cpu_baseline(nodes, pods, sample):
-    """Oracle (C restatement, 1 thread) on the first `sample` pods of the same config-2 stream."""
-    from oracle import oracle as O
+class Ctx:
+    """Process-group plumbing: rank/world from the torchrun env, RCCL id broadcast, barriers."""
 
-    sub = qsched.pods_from_struct(pods[:sample])
-    on = {k: v.copy() for k, v in nodes.items()}
-    t0 = time.perf_counter()
-    pl, _, _ = O.schedule(on, sub, nthreads=1)
-    dt = time.perf_counter() - t0
-    return {"value": round(sample / dt, 1), "unit": "pods/s", "cores": 1, "kind": "port",
-            "sample": f"first {sample} of the 100,000 config-2 pods (QoS-sorted within the sample) "
-                      f"onto the empty 5,000-node cluster, oracle/qs_oracle.c 1 thread, {dt:.2f} s",
-            "evals_per_s": round(sample * N_NODES / dt, 1)}
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.dist = None
+        if self.world > 1:
+            import torch
+            import torch.distributed as dist
+
+            torch.cuda.set_device(self.local)
+            dist.init_process_group("nccl", init_method="env://")
+            self.dist = dist
+
+    def barrier(self):
+        if self.dist is not None:
+            import torch
+            self.dist.barrier()
+            torch.cuda.synchronize()
+
+    def max(self, v):
+        if self.dist is None:
+            return v
+        import torch
+        t = torch.tensor([v], dtype=torch.float64, device=f"cuda:{self.local}")
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def shard(self):
+        """(rank, world, RCCL unique id) for qs_open_shard; the id is made on rank 0."""
+        import torch
+        uid = qsched.dist_unique_id() if self.rank == 0 else bytes(128)
+        t = torch.tensor(list(uid), dtype=torch.uint8, device=f"cuda:{self.local}")
+        self.dist.broadcast(t, 0)
+        return (self.rank, self.world, bytes(t.cpu().numpy().tolist()))
 
 
-def kernel_profile(nodes, pods, cfg, device):
-    """Untimed run with config.profile_kernels = 1: every launch bracketed by HIP events on the
-    library's own stream.  Returns {kernel: {"s": total seconds, "launches": n}}."""
-    s = qsched.Scheduler(dict(cfg, profile_kernels=1), device=device)
-    s.load_nodes(nodes)
-    st = s.prepare(pods)
-    stats = st.run()
-    st.free()
-    s.close()
-    return stats["kernels"]
+def open_sched(cx, cfg, sharded):
+    return qsched.Scheduler(cfg, device=cx.local, shard=cx.shard() if sharded else None)
+
+
+def diag_runs(cx, nodes, pods, cfg, sharded):
+    """Untimed diagnostic runs: per-pod device timestamps (p50/p99 decision interval) and per-kernel
+    HIP-event times on the library's own stream (config.profile_kernels)."""
+    p50 = p99 = None
+    s2 = open_sched(cx, dict(cfg, record_timestamps=1), sharded)
+    s2.load_nodes(nodes)
+    st2 = s2.prepare(pods)
+    st2.run()
+    d = np.diff(st2.stamps().astype(np.int64)) * 0.01  # 100 MHz s_memrealtime ticks -> us
+    p50, p99 = float(np.percentile(d, 50)), float(np.percentile(d, 99))
+    st2.free()
+    s2.close()
+    s3 = open_sched(cx, dict(cfg, profile_kernels=1), sharded)
+    s3.load_nodes(nodes)
+    st3 = s3.prepare(pods)
+    kp = st3.run()["kernels"]
+    st3.free()
+    s3.close()
+    return p50, p99, kp
+
+
+def roofline(kp, n_nodes, n_pods, fallback_s):
+    """Dominant kernel (most device time in the profiled run): algorithmic bytes per launch =
+    (pod x node evaluations it completes per launch) x B_node / mean launch time."""
+    dom = max(kp, key=lambda k: kp[k]["s"]) if kp else None
+    avg_s = kp[dom]["s"] / kp[dom]["launches"] if dom else fallback_s
+    units = n_pods * n_nodes / (kp[dom]["launches"] if dom else 1)
+    achieved = units * B_NODE / avg_s / 1e9
+    kname = KERNEL_NAMES.get(dom, dom)
+    traffic = pmc_traffic(kname) if dom else None
+    return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5),
+            "traffic": None if traffic is None else round(traffic),
+            "kernel": kname, "avg_launch_us": round(avg_s * 1e6, 3),
+            "bytes_per_launch": round(units * B_NODE)}
 
 
 def pmc_traffic(kernel_prefix):
@@ -82,21 +150,29 @@ def pmc_traffic(kernel_prefix):
     return None
 
 
-def main():
-    a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as dist
+def cpu_baseline(nodes, pods, n_nodes, n_pods, sample):
+    """Oracle (C restatement, 1 thread) on the first `sample` pods of the same stream."""
+    from oracle import oracle as O
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", init_method="env://")
-    nodes, pods = qsched.synth_generate(2, N_NODES, N_PODS, seed=0x5EED0002 + rank)
+    sub = qsched.pods_from_struct(pods[:sample])
+    on = {k: v.copy() for k, v in nodes.items()}
+    t0 = time.perf_counter()
+    O.schedule(on, sub, nthreads=1)
+    dt = time.perf_counter() - t0
+    return {"value": round(sample / dt, 1), "unit": "pods/s", "cores": 1, "kind": "port",
+            "sample": f"first {sample} of the {n_pods:,} pods (QoS-sorted within the sample) onto "
+                      f"the empty {n_nodes:,}-node cluster, oracle/qs_oracle.c 1 thread, {dt:.2f} s",
+            "evals_per_s": round(sample * n_nodes / dt, 1)}
+
+
+def measure(cx, a, workload, steps, warmup, with_diag=True):
+    """Timed exact stream of `workload`; returns a dict of measurements (rank-0 meaningful)."""
+    gen, n_nodes, n_pods, desc = WORKLOADS[workload]
+    sharded = workload == "config3" and cx.world > 1
+    seed = 0x5EED0000 + gen + (cx.rank if (cx.world > 1 and not sharded) else 0)
+    nodes, pods = qsched.synth_generate(gen, n_nodes, n_pods, seed=seed)
     cfg = {"engine": a.engine, "lookahead": a.lookahead}
-    s = qsched.Scheduler(cfg, device=local)
+    s = open_sched(cx, cfg, sharded)
     s.load_nodes(nodes)
     s.save_table()
     st = s.prepare(pods)
@@ -105,93 +181,73 @@ def main():
         s.restore_table()
         return st.run()
 
-    def barrier():
-        if dist is not None:
-            import torch
-            dist.barrier()
-            torch.cuda.synchronize()
-
-    for _ in range(a.warmup):
+    for _ in range(warmup):
         step()
-    barrier()
+    cx.barrier()
     t0 = time.perf_counter()
-    dev_wall = 0.0
     last = None
-    for _ in range(a.steps):
+    for _ in range(steps):
         last = step()
-        dev_wall += last["wall_s"]
-    barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    placement, keys = st.results()
-
-    # parity spot check of the measured run against the oracle on a prefix is in tests/; here we
-    # only check internal consistency (unschedulable fraction of spec/synth.md G4).
-    unsched = float((placement < 0).mean())
-
-    # p99 per-pod decision interval: separate diagnostic run with device timestamps
-    p99 = p50 = None
-    try:
-        s2 = qsched.Scheduler(dict(cfg, record_timestamps=1), device=local)
-        s2.load_nodes(nodes)
-        st2 = s2.prepare(pods)
-        st2.run()
-        ts = st2.stamps().astype(np.int64)
-        d = np.diff(ts) * 0.01  # 100 MHz s_memrealtime ticks -> us
-        p50, p99 = float(np.percentile(d, 50)), float(np.percentile(d, 99))
-        st2.free()
-        s2.close()
-    except Exception as e:  # diagnostic only
-        print(f"# timestamp run failed: {e}", file=sys.stderr)
-
-    kp = kernel_profile(nodes, pods, cfg, local) if rank == 0 else {}
-    if rank == 0:
-        total_pods = N_PODS * a.steps * world
-        value = total_pods / elapsed
-        ms_per_step = elapsed / a.steps * 1e3
-        # roofline of the dominant kernel (most device time in the profiled run): algorithmic
-        # bytes = (pod x node evaluations it completes per launch) x B_node;
-        # each launch of resolve/select/persistent covers its pods against all N nodes.
-        dom = max(kp, key=lambda k: kp[k]["s"]) if kp else None
-        avg_s = kp[dom]["s"] / kp[dom]["launches"] if dom else dev_wall / a.steps
-        units = N_PODS * N_NODES / (kp[dom]["launches"] if dom else 1)
-        achieved = units * B_NODE / avg_s / 1e9
-        kname = {"resolve": "k_la_resolve4", "select": "k_la_select", "persistent": "k_persistent",
-                 "scan": "k_scan_key"}.get(dom, dom)
-        traffic = pmc_traffic(kname) if dom else None
-        out = {
-            "metric": "pods scheduled/sec (exact sequential stream, 5k nodes x 100k pods)",
-            "value": round(value, 1), "unit": "pods/s", "n_gpus": world, "steps": a.steps,
-            "warmup": a.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "int32+f64",
-            "data": "synthetic (spec/synth.md, seed 0x5EED0002+rank)",
-            "config": {"workload": "config2: 5,000 nodes x 100,000 pods, exact sequential, "
-                                   "Fit+Balanced+QoS weights, percentageOfNodesToScore=100",
-                       "engine": last["engine_used"], "lookahead": a.lookahead or 64,
-                       "parallelism": "replicas" if world > 1 else "single"},
-            "evals_per_s": round(value * N_NODES, 1),
-            "p50_pod_latency_us": None if p50 is None else round(p50, 4),
-            "p99_pod_latency_us": None if p99 is None else round(p99, 4),
-            "unschedulable_frac": round(unsched, 5),
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "traffic": None if traffic is None else round(traffic),
-                         "kernel": kname, "avg_launch_us": round(avg_s * 1e6, 3),
-                         "bytes_per_launch": round(units * B_NODE)},
-            "kernels_us_per_step": {k: round(v["s"] * 1e6, 1) for k, v in kp.items()},
-        }
-        if not a.no_cpu:
-            out["cpu_baseline"] = cpu_baseline(nodes, pods, a.cpu_sample)
-        print(json.dumps(out))
+    cx.barrier()
+    elapsed = cx.max(time.perf_counter() - t0)
+    placement, _ = st.results()
     st.free()
     s.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    ranks_work = cx.world if (cx.world > 1 and not sharded) else 1  # replicas multiply the work
+    value = n_pods * steps * ranks_work / elapsed
+    out = {"value": value, "ms_per_step": elapsed / steps * 1e3, "engine": last["engine_used"],
+           "unschedulable_frac": float((placement < 0).mean()), "n_nodes": n_nodes,
+           "n_pods": n_pods, "desc": desc, "sharded": sharded, "nodes": nodes, "pods": pods,
+           "replicas": ranks_work}
+    if with_diag:
+        out["p50"], out["p99"], out["kp"] = diag_runs(cx, nodes, pods, cfg, sharded)
+        out["wall_fallback"] = last["wall_s"]
+    return out
+
+
+def main():
+    a = parse()
+    cx = Ctx()
+    workload = a.workload if a.workload != "auto" else ("config2" if cx.world == 1 else "config3")
+    m = measure(cx, a, workload, a.steps, a.warmup)
+    c3 = None
+    if cx.world == 1 and workload == "config2" and not a.no_config3:
+        c3 = measure(cx, a, "config3", 1, 1, with_diag=False)
+    if cx.rank == 0:
+        rl = roofline(m["kp"], m["n_nodes"], m["n_pods"], m["wall_fallback"])
+        if m["sharded"]:
+            par, scaling = f"node-sharded x{cx.world} (RCCL all-gather per window)", "strong"
+        elif cx.world > 1:
+            par, scaling = f"replicas x{cx.world}", "weak"
+        else:
+            par, scaling = "single", "weak"
+        out = {
+            "metric": f"pods scheduled/sec (exact sequential stream, {m['n_nodes']:,} nodes x "
+                      f"{m['n_pods']:,} pods)",
+            "value": round(m["value"], 1), "unit": "pods/s", "n_gpus": cx.world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(m["ms_per_step"], 3), "higher_is_better": True,
+            "scaling": scaling, "vs_baseline": None, "dtype": "int32+f64",
+            "data": f"synthetic (spec/synth.md generator, config {WORKLOADS[workload][0]})",
+            "config": {"workload": m["desc"], "engine": m["engine"],
+                       "lookahead": a.lookahead or 32, "parallelism": par},
+            "evals_per_s": round(m["value"] * m["n_nodes"], 1),
+            "p50_pod_latency_us": round(m["p50"], 4), "p99_pod_latency_us": round(m["p99"], 4),
+            "unschedulable_frac": round(m["unschedulable_frac"], 5),
+            "roofline": rl,
+            "kernels_us_per_step": {k: round(v["s"] * 1e6, 1) for k, v in m["kp"].items()},
+        }
+        if c3 is not None:
+            out["config3"] = {"workload": c3["desc"] + " (1 GPU: the N=1 point of the curve)",
+                              "value": round(c3["value"], 1), "unit": "pods/s",
+                              "evals_per_s": round(c3["value"] * c3["n_nodes"], 1),
+                              "ms_per_step": round(c3["ms_per_step"], 3), "steps": 1,
+                              "engine": c3["engine"]}
+        if cx.world == 1 and not a.no_cpu:
+            out["cpu_baseline"] = cpu_baseline(m["nodes"], m["pods"], m["n_nodes"], m["n_pods"],
+                                               a.cpu_sample)
+        print(json.dumps(out), flush=True)
+    if cx.dist is not None:
+        cx.dist.destroy_process_group()
 
 
 if __name__ == "__main__":

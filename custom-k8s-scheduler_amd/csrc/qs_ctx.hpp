@@ -1,0 +1,122 @@
+// qs_ctx.hpp — internal host-side state shared by the libqsched translation units (qs_host.cpp,
+// qs_dist.cpp): the context behind the opaque qs_ctx handle, prepared streams, device buffers.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/qsched.h"
+#include "qs_device.hpp"
+#include "qs_launch.hpp"
+
+namespace qs_host {
+
+constexpr int64_t kLimit = (1LL << 24) - 1;  // 24-bit multiplier range of the kernels (spec S10)
+
+struct QsError {
+    qs_status st;
+    std::string msg;
+};
+
+#define HIPCHK(x)                                                                          \
+    do {                                                                                   \
+        hipError_t e_ = (x);                                                               \
+        if (e_ != hipSuccess)                                                              \
+            throw QsError{QS_EDEVICE, std::string(#x) + ": " + hipGetErrorString(e_)};     \
+    } while (0)
+
+[[noreturn]] inline void fail(qs_status st, const std::string &m) { throw QsError{st, m}; }
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+    void ensure(size_t b) {
+        if (b <= bytes) return;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        HIPCHK(hipMalloc(&p, b));
+        bytes = b;
+    }
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+    template <class T>
+    T *as() const { return (T *)p; }
+};
+
+// Host mirror of the canonical table.
+struct Mirror {
+    uint32_t n = 0;
+    std::vector<int64_t> ac, am, mp, rc, rm, zc, zm, np;
+    std::vector<int64_t> ae, re;  // [n][QS_MAX_EXT]
+    std::vector<uint64_t> th, ts, lb;  // lb [n][2]
+    std::vector<uint64_t> gen;
+    void resize(uint32_t nn) {
+        n = nn;
+        for (auto *v : {&ac, &am, &mp, &rc, &rm, &zc, &zm, &np}) v->assign(nn, 0);
+        ae.assign((size_t)nn * QS_MAX_EXT, 0);
+        re.assign((size_t)nn * QS_MAX_EXT, 0);
+        th.assign(nn, 0);
+        ts.assign(nn, 0);
+        lb.assign((size_t)nn * 2, 0);
+        gen.assign(nn, 0);
+    }
+};
+
+inline int ctz64(int64_t v) { return v == 0 ? 64 : __builtin_ctzll((uint64_t)v); }
+
+}  // namespace qs_host
+
+struct qs_stream {
+    uint32_t p = 0;
+    uint32_t feat = 0;  // kFeat* bits of this stream (profile + extended resources in use)
+    std::vector<qs_pod> pods;      // canonical, arrival order
+    std::vector<uint32_t> order;   // stream position -> arrival index
+    qs_host::DevBuf d_pods, d_podx, d_node, d_key, d_stamp;
+    bool ran = false;
+    int shift = 0;
+};
+
+struct qs_ctx {
+    std::mutex mu;
+    qs_config cfg{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    qs_host::Mirror m;
+    int shift = 20;  // memory unit 2^shift bytes on the device
+    bool dev_valid = false;
+    qs::DevTable dt{};
+    qs::DevCfg dc{};
+    qs_host::DevBuf tbl;  // all columns in one allocation
+    qs_host::DevBuf tbl_saved;  // qs_table_save snapshot (whole allocation)
+    bool saved = false;
+    bool mirror_stale = false;  // device ran a stream since the last mirror sync
+    qs_host::DevBuf diag;
+    qs_host::DevBuf scratch, lists, one_pod, one_podx, out_feas, out_score, out_total;
+    uint32_t cap = 0;
+    // sharding (qs_open_shard): RCCL communicator of this rank, nullptr when unsharded
+    int rank = 0, world = 1;
+    ncclComm_t comm = nullptr;
+};
+
+namespace qs_host {
+// Node shards of the LOOKAHEAD select for this context: W shards in total, this process scores
+// shards [v0, v0 + nv).  qs_open_shard: (world, rank, 1); cfg.virtual_shards = V > 1: (V, 0, V).
+struct ShardPlan {
+    uint32_t W, v0, nv;
+};
+inline ShardPlan shard_plan(const qs_ctx *c) {
+    if (c->world > 1) return {(uint32_t)c->world, (uint32_t)c->rank, 1u};
+    if (c->cfg.virtual_shards > 1) return {(uint32_t)c->cfg.virtual_shards, 0u, (uint32_t)c->cfg.virtual_shards};
+    return {1u, 0u, 1u};
+}
+// The per-window exchange of the sharded engine (qs_dist.cpp): all-gather of each rank's
+// [K][GLp] list block into [world][K][GLp] (in place), on the context's stream.
+void exchange_lists(qs_ctx *c, uint64_t *lists, size_t per_rank_entries);
+}  // namespace qs_host
+

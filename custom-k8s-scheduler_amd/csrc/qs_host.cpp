@@ -24,101 +24,11 @@
 #include <string>
 #include <vector>
 
-#include "qs_device.hpp"
-#include "qs_launch.hpp"
+#include "qs_ctx.hpp"
 
 using namespace qs;
 
-namespace {
-
-constexpr int64_t kLimit = (1LL << 24) - 1;  // 24-bit multiplier range of the kernels (spec S10)
-
-struct QsError {
-    qs_status st;
-    std::string msg;
-};
-
-#define HIPCHK(x)                                                                          \
-    do {                                                                                   \
-        hipError_t e_ = (x);                                                               \
-        if (e_ != hipSuccess)                                                              \
-            throw QsError{QS_EDEVICE, std::string(#x) + ": " + hipGetErrorString(e_)};     \
-    } while (0)
-
-static void fail(qs_status st, const std::string &m) { throw QsError{st, m}; }
-
-struct DevBuf {
-    void *p = nullptr;
-    size_t bytes = 0;
-    void ensure(size_t b) {
-        if (b <= bytes) return;
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        bytes = 0;
-        HIPCHK(hipMalloc(&p, b));
-        bytes = b;
-    }
-    ~DevBuf() {
-        if (p) (void)hipFree(p);
-    }
-    template <class T>
-    T *as() const { return (T *)p; }
-};
-
-// Host mirror of the canonical table.
-struct Mirror {
-    uint32_t n = 0;
-    std::vector<int64_t> ac, am, mp, rc, rm, zc, zm, np;
-    std::vector<int64_t> ae, re;  // [n][QS_MAX_EXT]
-    std::vector<uint64_t> th, ts, lb;  // lb [n][2]
-    std::vector<uint64_t> gen;
-    void resize(uint32_t nn) {
-        n = nn;
-        for (auto *v : {&ac, &am, &mp, &rc, &rm, &zc, &zm, &np}) v->assign(nn, 0);
-        ae.assign((size_t)nn * QS_MAX_EXT, 0);
-        re.assign((size_t)nn * QS_MAX_EXT, 0);
-        th.assign(nn, 0);
-        ts.assign(nn, 0);
-        lb.assign((size_t)nn * 2, 0);
-        gen.assign(nn, 0);
-    }
-};
-
-static int ctz64(int64_t v) { return v == 0 ? 64 : __builtin_ctzll((uint64_t)v); }
-
-}  // namespace
-
-struct qs_stream {
-    uint32_t p = 0;
-    uint32_t feat = 0;  // kFeat* bits of this stream (profile + extended resources in use)
-    std::vector<qs_pod> pods;      // canonical, arrival order
-    std::vector<uint32_t> order;   // stream position -> arrival index
-    DevBuf d_pods, d_podx, d_node, d_key, d_stamp;
-    bool ran = false;
-    int shift = 0;
-};
-
-struct qs_ctx {
-    std::mutex mu;
-    qs_config cfg{};
-    int device = 0;
-    hipStream_t stream = nullptr;
-    std::string err;
-    Mirror m;
-    int shift = 20;  // memory unit 2^shift bytes on the device
-    bool dev_valid = false;
-    DevTable dt{};
-    DevCfg dc{};
-    DevBuf tbl;  // all columns in one allocation
-    DevBuf tbl_saved;  // qs_table_save snapshot (whole allocation)
-    bool saved = false;
-    bool mirror_stale = false;  // device ran a stream since the last mirror sync
-    DevBuf diag;
-    DevBuf scratch, lists, one_pod, one_podx, out_feas, out_score, out_total;
-    uint32_t cap = 0;
-    // sharding (qs_open_shard)
-    int rank = 0, world = 1;
-};
+using namespace qs_host;
 
 namespace {
 
@@ -427,11 +337,15 @@ struct KernelTimer {
     }
 };
 
+uint32_t la_window(const qs_ctx *c);
+
 int pick_engine(const qs_ctx *c, uint32_t n) {
     int e = c->cfg.engine;
     const uint32_t feat = c->dc.feat;
     if (e == QS_ENGINE_AUTO) {
-        if (!(feat & (kFeatTaint | kFeatAffinity)) && n > 0) e = QS_ENGINE_LOOKAHEAD;
+        if (!(feat & (kFeatTaint | kFeatAffinity)) && n > 0 &&
+            la_geometry(n, la_window(c), shard_plan(c).W).G > 0)
+            e = QS_ENGINE_LOOKAHEAD;
         else if (n <= persistent_max_nodes(feat)) e = QS_ENGINE_PERSISTENT;
         else e = QS_ENGINE_SCAN;
     }
@@ -441,6 +355,14 @@ int pick_engine(const qs_ctx *c, uint32_t n) {
     if (e == QS_ENGINE_LOOKAHEAD && (feat & (kFeatTaint | kFeatAffinity)))
         fail(QS_EINVAL, "LOOKAHEAD engine does not support TaintToleration/NodeAffinity yet");
     return e;
+}
+
+LaGeom lookahead_geometry(const qs_ctx *c, uint32_t n) {
+    const ShardPlan sp = shard_plan(c);
+    LaGeom geo = la_geometry(n, la_window(c), sp.W);
+    geo.v0 = sp.v0;
+    geo.nv = sp.nv;
+    return geo;
 }
 
 uint32_t la_window(const qs_ctx *c) {
@@ -516,6 +438,8 @@ qs_status qs_close(qs_ctx *c) {
         std::lock_guard<std::mutex> lk(c->mu);
         (void)hipSetDevice(c->device);
         if (c->stream) (void)hipStreamSynchronize(c->stream);
+        if (c->comm) (void)ncclCommDestroy(c->comm);
+        c->comm = nullptr;
     }
     hipStream_t s = c->stream;
     delete c;  // DevBuf destructors free device memory
@@ -750,14 +674,15 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                 }
                 batches = P;
             } else {
-                LaGeom geo = la_geometry(n, la_window(c));
+                LaGeom geo = lookahead_geometry(c, n);
                 static const char *rw = getenv("QS_RESOLVER_WAVES");  // 1 = single-wave resolver
                 geo.waves = (rw && rw[0] == '1') ? 1u : 4u;
                 int64_t wmax = 0;
                 for (int q = 0; q < 3; q++) wmax = std::max<int64_t>(wmax, (int64_t)c->cfg.w_fit[q] + c->cfg.w_bal[q]);
                 geo.k32 = (100 * wmax + 1 < 1024 && n <= (1u << 22)) ? 1u : 0u;
                 if (geo.G == 0) fail(QS_EINVAL, "no lookahead geometry for this table size");
-                const size_t lbytes = 8ull * geo.K * 64 * geo.epl;
+                const size_t rank_entries = (size_t)geo.K * 64 * geo.eplr;  // [K][GLp] per shard
+                const size_t lbytes = 8ull * geo.W * rank_entries;
                 c->lists.ensure(lbytes);
                 HIPCHK(hipMemsetAsync(c->lists.p, 0, lbytes, c->stream));  // padding entries stay 0
                 // QS_DIAG=1: diagnostic resolver with per-segment shader-clock stamps (stderr)
@@ -773,6 +698,7 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                     HIPCHK(launch_la_window(c->dt, dp, s0, P, c->dc, geo, c->lists.as<uint64_t>(), on,
                                             ok, st, diag, c->stream, 1));
                     kt.end(2);
+                    if (c->comm) exchange_lists(c, c->lists.as<uint64_t>(), rank_entries);
                     kt.begin(3);
                     HIPCHK(launch_la_window(c->dt, dp, s0, P, c->dc, geo, c->lists.as<uint64_t>(), on,
                                             ok, st, diag, c->stream, 2));

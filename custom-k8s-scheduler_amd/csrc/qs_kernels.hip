@@ -217,20 +217,25 @@ __device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t (*buf)[NW], i
 // is (wave, j, lane) order and tie ranks come from ballots + one cross-wave prefix.
 template <int BS, int E, uint32_t F>
 __global__ __launch_bounds__(BS) void k_la_select(DevTable t, const DPod *__restrict__ pods,
-                                                  DevCfg c, uint32_t s0, uint32_t P, uint32_t G,
-                                                  uint32_t L, uint32_t chunk, uint32_t GLp,
-                                                  uint64_t *__restrict__ lists) {
+                                                  DevCfg c, uint32_t s0, uint32_t P, LaShard sh,
+                                                  uint32_t G, uint32_t L, uint32_t chunk,
+                                                  uint32_t GLp, uint64_t *__restrict__ lists) {
     constexpr int NW = BS / kWave;
     __shared__ uint32_t cnt[2][NW];
     __shared__ uint32_t slot_ctr;
-    const uint32_t k = blockIdx.x / G, g = blockIdx.x % G;
+    // block -> (shard v, pod k, chunk g); shard v owns nodes [v*n/W, (v+1)*n/W)
+    const uint32_t per = sh.kw * G;
+    const uint32_t v = sh.v0 + blockIdx.x / per, rem = blockIdx.x % per;
+    const uint32_t k = rem / G, g = rem % G;
     const uint32_t s = s0 + k;
     if (s >= P) return;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const DPod p = pods[s];
     const DPodX px{};
-    const uint32_t start = g * chunk;
-    const uint32_t end = min(t.n, start + chunk);
+    const uint32_t lo = (uint32_t)((uint64_t)v * t.n / sh.W);
+    const uint32_t hi = (uint32_t)((uint64_t)(v + 1) * t.n / sh.W);
+    const uint32_t start = lo + g * chunk;
+    const uint32_t end = min(hi, start + chunk);
     const uint32_t base = start + (uint32_t)w * E * kWave + lane;
     uint32_t tv[E];
     uint32_t lmax = 0;
@@ -299,7 +304,7 @@ __global__ __launch_bounds__(BS) void k_la_select(DevTable t, const DPod *__rest
         rank += i < w ? v : 0u;
         ties_total += v;
     }
-    uint64_t *out = lists + (size_t)k * GLp + (size_t)g * L;
+    uint64_t *out = lists + (size_t)v * sh.RS + (size_t)k * GLp + (size_t)g * L;
     const uint64_t lane_mask_lt = (1ull << lane) - 1ull;
 #pragma unroll
     for (int j = 0; j < E; ++j) {
@@ -315,6 +320,18 @@ __global__ __launch_bounds__(BS) void k_la_select(DevTable t, const DPod *__rest
     }
     const uint32_t written = c_gt + (ties_total < need ? ties_total : need);
     for (uint32_t i = written + tid; i < L; i += BS) out[i] = 0;
+}
+
+// Entry m (0 <= m < EPL) of resolver lane `lane` for window pod `pod`.  Lists are laid out
+// [shard][pod][GLp] (GLp = 64 * 2^lr entries per pod and shard: the all-gathered layout of the
+// sharded engine); entries of shards >= W read as empty.
+__device__ __forceinline__ uint64_t list_ent(const uint64_t *__restrict__ lists, uint32_t pod,
+                                             uint32_t GLp, uint32_t lr, const LaShard &sh, int m,
+                                             int lane) {
+    const uint32_t q = (uint32_t)m >> lr;
+    if (q >= sh.W) return 0ull;
+    return lists[(size_t)q * sh.RS + (size_t)pod * GLp + (uint32_t)lane +
+                 64u * ((uint32_t)m & ((1u << lr) - 1u))];
 }
 
 // One wave resolves the window sequentially (spec S7 order).  Dirty (modified-in-window) node
@@ -341,7 +358,8 @@ __device__ __forceinline__ uint64_t diag_stamp() {
 template <uint32_t F, int EPL, bool DIAG>
 __global__ __launch_bounds__(64) void k_la_resolve(DevTable t, const DPod *__restrict__ pods,
                                                    DevCfg c, uint32_t s0, uint32_t P, uint32_t K,
-                                                   uint32_t GLp, const uint64_t *__restrict__ lists,
+                                                   uint32_t GLp, uint32_t lr, LaShard sh,
+                                                   const uint64_t *__restrict__ lists,
                                                    int32_t *__restrict__ out_node,
                                                    uint64_t *__restrict__ out_key,
                                                    uint64_t *__restrict__ stamps,
@@ -370,9 +388,9 @@ __global__ __launch_bounds__(64) void k_la_resolve(DevTable t, const DPod *__res
     //   pod i+2: list entries loaded.
     uint64_t ent1[EPL], ent2[EPL];
 #pragma unroll
-    for (int m = 0; m < EPL; ++m) ent1[m] = lists[lane + 64 * m];
+    for (int m = 0; m < EPL; ++m) ent1[m] = list_ent(lists, 0, GLp, lr, sh, m, lane);
 #pragma unroll
-    for (int m = 0; m < EPL; ++m) ent2[m] = kend > 1 ? lists[(size_t)GLp + lane + 64 * m] : 0ull;
+    for (int m = 0; m < EPL; ++m) ent2[m] = kend > 1 ? list_ent(lists, 1, GLp, lr, sh, m, lane) : 0ull;
     __syncthreads();
     // top-2 clean entries of a pod's list against the dirty bitmap
     auto top2 = [&](const uint64_t (&e)[EPL], uint64_t &c1, uint64_t &c2) {
@@ -416,9 +434,8 @@ __global__ __launch_bounds__(64) void k_la_resolve(DevTable t, const DPod *__res
             x2 = load_rowx<F>(t, c2 ? key_node(c2) : 0u);
         }
         if (i + 2 < kend) {
-            const uint64_t *nl = lists + (size_t)(i + 2) * GLp;
 #pragma unroll
-            for (int m = 0; m < EPL; ++m) ent2[m] = nl[lane + 64 * m];
+            for (int m = 0; m < EPL; ++m) ent2[m] = list_ent(lists, i + 2, GLp, lr, sh, m, lane);
         }
         QS_STAMP(1)
         // fresh keys of the dirty slots
@@ -508,7 +525,8 @@ __device__ __forceinline__ ResPub read_pub(const ResPub *p) {
 template <uint32_t F, int EPL, bool DIAG, bool K32>
 __global__ __launch_bounds__(256) void k_la_resolve4(DevTable t, const DPod *__restrict__ pods,
                                                      DevCfg c, uint32_t s0, uint32_t P,
-                                                     uint32_t K, uint32_t GLp,
+                                                     uint32_t K, uint32_t GLp, uint32_t lr,
+                                                     LaShard sh,
                                                      const uint64_t *__restrict__ lists,
                                                      int32_t *__restrict__ out_node,
                                                      uint64_t *__restrict__ out_key,
@@ -670,9 +688,8 @@ __global__ __launch_bounds__(256) void k_la_resolve4(DevTable t, const DPod *__r
             }
         };
         auto load_ent = [&](uint64_t(&e)[EPL], uint32_t pod) {
-            const uint64_t *l = lists + (size_t)pod * GLp;
 #pragma unroll
-            for (int m = 0; m < EPL; ++m) e[m] = pod < kend ? l[lane + 64 * m] : 0ull;
+            for (int m = 0; m < EPL; ++m) e[m] = pod < kend ? list_ent(lists, pod, GLp, lr, sh, m, lane) : 0ull;
         };
         uint64_t c1, c2;
         uint64_t eX[EPL], eY[EPL];  // ping-pong: entries consumed two pods after their load
@@ -853,12 +870,13 @@ static hipError_t la_window_f(const DevTable &t, const DPod *pods, uint32_t s0, 
                               const DevCfg &c, const LaGeom &geo, uint64_t *lists, int32_t *on,
                               uint64_t *ok, uint64_t *st, uint64_t *diag, hipStream_t stream,
                               int part) {
-    const uint32_t K = geo.K, G = geo.G, L = geo.L, GLp = geo.epl * 64;
+    const uint32_t K = geo.K, G = geo.G, L = geo.L, GLp = geo.eplr * 64;
     const uint32_t kw = min(K, P - s0);
+    LaShard sh{geo.W, geo.v0, kw, 0u, (uint64_t)K * GLp};
     if (part & 1) {
-        const dim3 grid(kw * G);
+        const dim3 grid(geo.nv * kw * G);
         switch (geo.E) {
-#define QS_SEL(EE) case EE: hipLaunchKernelGGL((k_la_select<256, EE, F>), grid, dim3(256), 0, stream, t, pods, c, s0, P, G, L, geo.chunk, GLp, lists); break;
+#define QS_SEL(EE) case EE: hipLaunchKernelGGL((k_la_select<256, EE, F>), grid, dim3(256), 0, stream, t, pods, c, s0, P, sh, G, L, geo.chunk, GLp, lists); break;
             QS_SEL(1) QS_SEL(2) QS_SEL(3) QS_SEL(4) QS_SEL(5) QS_SEL(6) QS_SEL(8) QS_SEL(10) QS_SEL(12) QS_SEL(16)
 #undef QS_SEL
             default: return hipErrorInvalidValue;
@@ -872,12 +890,12 @@ static hipError_t la_window_f(const DevTable &t, const DPod *pods, uint32_t s0, 
         switch (geo.epl) {
 #define QS_RES(EP) case EP: \
             if (geo.waves == 1) { \
-                if (diag) hipLaunchKernelGGL((k_la_resolve<F, EP, true>), dim3(1), dim3(64), lds, stream, t, pods, c, s0, P, K, GLp, lists, on, ok, st, diag); \
-                else hipLaunchKernelGGL((k_la_resolve<F, EP, false>), dim3(1), dim3(64), lds, stream, t, pods, c, s0, P, K, GLp, lists, on, ok, st, diag); \
+                if (diag) hipLaunchKernelGGL((k_la_resolve<F, EP, true>), dim3(1), dim3(64), lds, stream, t, pods, c, s0, P, K, GLp, geo.lr, sh, lists, on, ok, st, diag); \
+                else hipLaunchKernelGGL((k_la_resolve<F, EP, false>), dim3(1), dim3(64), lds, stream, t, pods, c, s0, P, K, GLp, geo.lr, sh, lists, on, ok, st, diag); \
             } else { \
-                if (diag) hipLaunchKernelGGL((k_la_resolve4<F, EP, true, false>), dim3(1), dim3(256), lds4, stream, t, pods, c, s0, P, K, GLp, lists, on, ok, st, diag); \
-                else if (geo.k32) hipLaunchKernelGGL((k_la_resolve4<F, EP, false, true>), dim3(1), dim3(256), lds4, stream, t, pods, c, s0, P, K, GLp, lists, on, ok, st, diag); \
-                else hipLaunchKernelGGL((k_la_resolve4<F, EP, false, false>), dim3(1), dim3(256), lds4, stream, t, pods, c, s0, P, K, GLp, lists, on, ok, st, diag); \
+                if (diag) hipLaunchKernelGGL((k_la_resolve4<F, EP, true, false>), dim3(1), dim3(256), lds4, stream, t, pods, c, s0, P, K, GLp, geo.lr, sh, lists, on, ok, st, diag); \
+                else if (geo.k32) hipLaunchKernelGGL((k_la_resolve4<F, EP, false, true>), dim3(1), dim3(256), lds4, stream, t, pods, c, s0, P, K, GLp, geo.lr, sh, lists, on, ok, st, diag); \
+                else hipLaunchKernelGGL((k_la_resolve4<F, EP, false, false>), dim3(1), dim3(256), lds4, stream, t, pods, c, s0, P, K, GLp, geo.lr, sh, lists, on, ok, st, diag); \
             } break;
             QS_RES(1) QS_RES(2) QS_RES(4) QS_RES(8) QS_RES(16)
 #undef QS_RES
@@ -896,28 +914,41 @@ hipError_t launch_la_window(const DevTable &t, const DPod *pods, uint32_t s0, ui
     return la_window_f<0>(t, pods, s0, P, c, geo, lists, on, ok, st, diag, stream, part);
 }
 
-LaGeom la_geometry(uint32_t n, uint32_t K) {
-    // G node chunks per pod: about 1,280 nodes (E = 5 per lane of a 256-thread block) per chunk,
-    // capped so the resolver sees at most 1,024 list entries per pod (16 per lane).
+LaGeom la_geometry(uint32_t n, uint32_t K, uint32_t W) {
+    // Per shard (W shards of <= ceil(n/W) nodes; W = 1 unsharded): G node chunks per pod of about
+    // 1,280 nodes (E = 5 per lane of a 256-thread block), capped so the resolver sees at most
+    // 1,024 list entries per pod in total (16 per lane) over all shards.
     static const uint32_t Es[] = {1, 2, 3, 4, 5, 6, 8, 10, 12, 16};
     LaGeom g{};
     g.K = K;
     g.L = K;
-    const uint32_t gmax = std::max(1u, 1024u / g.L);
-    uint32_t G = std::max(1u, std::min(gmax, (n + 1279) / 1280));
-    const uint32_t per = (n + G - 1) / G;
+    g.W = std::max(1u, W);
+    g.v0 = 0;
+    g.nv = g.W;
+    if (g.W > 16) return g;  // G = 0: no geometry
+    uint32_t eplr_max = 1;   // largest power of two with W * eplr <= 16
+    while (g.W * eplr_max * 2 <= 16) eplr_max *= 2;
+    const uint32_t ns = (n + g.W - 1) / g.W;
+    const uint32_t gmax = (eplr_max * 64) / g.L;
+    if (gmax == 0) return g;
+    uint32_t G = std::max(1u, std::min(gmax, (ns + 1279) / 1280));
+    const uint32_t per = (ns + G - 1) / G;
     const uint32_t e_need = std::max(1u, (per + 255) / 256);
     uint32_t E = 0;
     for (uint32_t e : Es)
         if (e >= e_need) { E = e; break; }
-    if (E == 0) { g.G = 0; return g; }  // table too large for one-level lists
+    if (E == 0) return g;  // shard too large for one-level lists
     g.E = E;
     g.chunk = E * 256;
-    g.G = std::max(1u, (n + g.chunk - 1) / g.chunk);
-    const uint32_t need = (g.G * g.L + 63) / 64;  // list entries per resolver lane
+    G = std::max(1u, (ns + g.chunk - 1) / g.chunk);
+    const uint32_t need = (G * g.L + 63) / 64;  // list entries per resolver lane, per shard
+    g.eplr = 1;
+    g.lr = 0;
+    while (g.eplr < need) { g.eplr *= 2; ++g.lr; }
+    if (g.eplr > eplr_max) return g;
     g.epl = 1;
-    while (g.epl < need) g.epl *= 2;
-    if (g.epl > 16) g.G = 0;
+    while (g.epl < g.W * g.eplr) g.epl *= 2;
+    g.G = G;
     return g;
 }
 

@@ -24,8 +24,18 @@ struct HostRow {
 // epl = list entries per resolver lane (power of two); a pod's lists occupy 64*epl entries.
 // waves = resolver geometry: 1 (single-wave) or 4 (pipelined four-wave resolver).
 // k32 = keys fit 32 bits ((max total + 1) < 2^10, n <= 2^22): one 32-bit wave reduction per pod.
+// Sharding: the node table splits into W contiguous shards (shard v = nodes [v*n/W, (v+1)*n/W));
+// every shard has the same G/E/chunk and eplr = 2^lr entries per lane per pod; this process
+// selects shards [v0, v0 + nv) (nv = W for virtual shards in one process, 1 per rank with RCCL).
+// epl (total entries per resolver lane, power of two) >= W * eplr.
 struct LaGeom {
     uint32_t K, L, G, E, chunk, epl, waves, k32;
+    uint32_t W, v0, nv, eplr, lr;
+};
+// Kernel-side shard view of the lists: [W][K][GLp] uint64 keys, RS = K * GLp.
+struct LaShard {
+    uint32_t W, v0, kw, pad;
+    uint64_t RS;
 };
 
 hipError_t launch_persistent(const DevTable &t, const DPod *pods, const DPodX *podx, uint32_t P,
@@ -39,7 +49,7 @@ hipError_t launch_scan_pod(const DevTable &t, const DPod *pods, const DPodX *pod
                            bool commit, hipStream_t stream);
 size_t scan_scratch_bytes();
 
-LaGeom la_geometry(uint32_t n, uint32_t K);
+LaGeom la_geometry(uint32_t n, uint32_t K, uint32_t W = 1);
 hipError_t launch_la_window(const DevTable &t, const DPod *pods, uint32_t s0, uint32_t P,
                             const DevCfg &c, const LaGeom &geo, uint64_t *lists, int32_t *out_node,
                             uint64_t *out_key, uint64_t *stamps, uint64_t *diag,

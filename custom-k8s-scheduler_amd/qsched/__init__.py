@@ -23,7 +23,7 @@ from ._abi import (ENGINES, ENGINE_NAMES, EXPORTED, LIB_PATH, POD_DTYPE, QS_ABI_
                    load)
 
 __all__ = ["Scheduler", "Config", "POD_DTYPE", "pods_to_struct", "pods_from_struct",
-           "synth_generate", "empty_nodes", "pod_from_containers", "compute_qos", "load",
+           "synth_generate", "dist_unique_id", "empty_nodes", "pod_from_containers", "compute_qos", "load",
            "QschedError", "QschedLibraryMissing", "ENGINES", "EXPORTED", "LIB_PATH"]
 
 NODE_I64 = ["alloc_cpu", "alloc_mem", "max_pods", "req_cpu", "req_mem", "nz_cpu", "nz_mem", "pods"]
@@ -105,11 +105,19 @@ class Config(dict):
 class Scheduler:
     """One device context (``qs_ctx``) on one GPU."""
 
-    def __init__(self, config=None, device: int = 0):
+    def __init__(self, config=None, device: int = 0, shard=None):
+        """shard = (rank, world, unique_id bytes) opens a node-sharded context (qs_open_shard):
+        every rank loads the same full table and pod stream; RCCL exchanges the per-window lists."""
         self.lib = load()
         self.cfg = Config(config or {}).to_c()
         ctx = ctypes.c_void_p()
-        st = self.lib.qs_open(ctypes.byref(self.cfg), device, ctypes.byref(ctx))
+        if shard is None:
+            st = self.lib.qs_open(ctypes.byref(self.cfg), device, ctypes.byref(ctx))
+        else:
+            rank, world, uid = shard
+            buf = None if uid is None else (ctypes.c_uint8 * 128).from_buffer_copy(bytes(uid))
+            st = self.lib.qs_open_shard(ctypes.byref(self.cfg), device, rank, world, buf,
+                                        ctypes.byref(ctx))
         if st != QS_OK:
             raise QschedError(st, "qs_open failed (no HIP device?)")
         self.ctx = ctx
@@ -232,6 +240,16 @@ class Stream:
         if self.h:
             self.s._chk(self.s.lib.qs_stream_free(self.s.ctx, self.h))
             self.h = None
+
+
+def dist_unique_id() -> bytes:
+    """128-byte RCCL unique id (qs_dist_unique_id) for qs_open_shard; create on rank 0 only."""
+    lib = load()
+    buf = (ctypes.c_uint8 * 128)()
+    st = lib.qs_dist_unique_id(buf)
+    if st != QS_OK:
+        raise QschedError(st, "qs_dist_unique_id failed")
+    return bytes(buf)
 
 
 def synth_generate(config: int, n: int, p: int, seed=None):

@@ -82,7 +82,10 @@ typedef struct qs_config {
     int32_t lookahead;           /* pods per lookahead window (0 = default) */
     int32_t record_timestamps;   /* 1 = per-pod device timestamps for p50/p99 cycle latency */
     int32_t profile_kernels;     /* 1 = time every kernel launch with HIP events (qs_stats.kernel_s) */
-    int32_t reserved[7];
+    int32_t virtual_shards;      /* >1: run the sharded LOOKAHEAD protocol with this many node shards
+                                    inside one process (no collective; parity testing of the
+                                    multi-GPU layout on one device).  Ignored by qs_open_shard. */
+    int32_t reserved[6];
 } qs_config;
 
 /* Canonical node table, structure of arrays, n entries each.  alloc_ext/req_ext are [n][QS_MAX_EXT],
@@ -149,9 +152,13 @@ typedef struct qs_stream qs_stream;
 /* ---- lifecycle ---- */
 QS_API void qs_config_default(qs_config *cfg);
 QS_API qs_status qs_open(const qs_config *cfg, int device, qs_ctx **out);
-/* Sharded context for one rank of `world` (one process per GPU).  nccl_id = 128 bytes from
- * qs_dist_unique_id on rank 0, broadcast by the caller.  The node table is sharded by contiguous
- * ranges; the per-window exchange runs on RCCL over xGMI. */
+/* Sharded context for one rank of `world` (one process per GPU, world <= 16).  nccl_id = 128 bytes
+ * from qs_dist_unique_id on rank 0, broadcast by the caller (any out-of-band channel).  Every rank
+ * loads the SAME full node table (qs_nodes_load) and the SAME pod stream; rank r scores only its
+ * contiguous node shard [r*n/world, (r+1)*n/world), the per-window top-L lists are exchanged with
+ * one RCCL all-gather over xGMI, and every rank resolves the window identically, so placements and
+ * the node table stay identical on all ranks.  Collective calls happen inside
+ * qs_stream_run: all ranks must call it with the same stream. */
 QS_API qs_status qs_open_shard(const qs_config *cfg, int device, int rank, int world,
                         const uint8_t nccl_id[128], qs_ctx **out);
 QS_API qs_status qs_dist_unique_id(uint8_t out[128]);

@@ -1,0 +1,64 @@
+"""GPU parity of the node-sharded LOOKAHEAD engine.
+
+Two ways to exercise the sharded layout on the single-GPU box:
+  * ``virtual_shards = W``: one process runs the select of all W node shards into the
+    [shard][pod][GLp] list layout the RCCL all-gather produces, then the same resolver — this is the
+    multi-GPU data path minus the collective, checked bit-exact against the oracle for W up to 8;
+  * ``qs_open_shard`` with world = 1 and a real RCCL unique id: the communicator is built and the
+    in-place all-gather runs every window (one rank), so the RCCL call path itself is exercised.
+The multi-rank protocol (lists gathered across processes, replicated resolve) is checked on CPU
+with world-size-2 gloo in tests/test_lookahead_model.py.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+from qsched import Scheduler, dist_unique_id, synth_generate  # noqa: E402
+
+from test_gpu_parity import assert_same, run_oracle  # noqa: E402
+
+
+def run_sharded(nodes, pods, cfg, shard=None):
+    with Scheduler(dict(cfg, engine="lookahead"), shard=shard) as s:
+        s.load_nodes(nodes)
+        st = s.prepare(pods)
+        stats = st.run()
+        pl, keys = st.results()
+        st.free()
+        final = s.read_nodes()
+    return pl, keys, final, stats
+
+
+@pytest.mark.parametrize("W", [2, 3, 4, 8])
+@pytest.mark.parametrize("n,p", [(5000, 3000), (777, 4000)])
+def test_virtual_shards_parity(oracle, W, n, p):
+    nodes, pods = synth_generate(2, n, p)
+    g = run_sharded(nodes, pods, dict(virtual_shards=W))
+    assert g[3]["engine_used"] == "lookahead"
+    o = run_oracle(oracle, nodes, pods, {})
+    assert_same(g[:2], o[:2], g[2], o[2])
+
+
+@pytest.mark.parametrize("W,K", [(1, 32), (2, 32), (8, 32), (8, 64)])
+def test_config3_scale_virtual_shards(oracle, W, K):
+    """Config 3 generator (seed 0x5EED0003) at its full 50,000-node table, 3,000 pods."""
+    nodes, pods = synth_generate(3, 50000, 3000)
+    g = run_sharded(nodes, pods, dict(virtual_shards=W, lookahead=K))
+    o = run_oracle(oracle, nodes, pods, {})
+    assert_same(g[:2], o[:2], g[2], o[2])
+
+
+def test_ext_resources_virtual_shards(oracle):
+    nodes, pods = synth_generate(4, 1800, 5000)
+    g = run_sharded(nodes, pods, dict(virtual_shards=4))
+    o = run_oracle(oracle, nodes, pods, {})
+    assert_same(g[:2], o[:2], g[2], o[2])
+
+
+def test_rccl_one_rank_communicator(oracle):
+    """qs_open_shard(rank 0, world 1, id): RCCL communicator + per-window all-gather on the GPU."""
+    nodes, pods = synth_generate(3, 4000, 5000)
+    g = run_sharded(nodes, pods, {}, shard=(0, 1, dist_unique_id()))
+    o = run_oracle(oracle, nodes, pods, {})
+    assert_same(g[:2], o[:2], g[2], o[2])
