@@ -79,13 +79,20 @@ struct qs_stream {
     qs_host::DevBuf d_pods, d_podx, d_node, d_key, d_stamp;
     bool ran = false;
     int shift = 0;
+    // LOOKAHEAD window sequence as an instantiated HIP graph, valid while gkey matches
+    hipGraphExec_t gexec = nullptr;
+    std::vector<uint8_t> gkey;
+    ~qs_stream() {
+        if (gexec) (void)hipGraphExecDestroy(gexec);
+    }
 };
 
 struct qs_ctx {
     std::mutex mu;
     qs_config cfg{};
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;   // resolve chain, copies, single-kernel engines
+    hipStream_t stream2 = nullptr;  // lookahead select chain (overlapped windows)
     std::string err;
     qs_host::Mirror m;
     int shift = 20;  // memory unit 2^shift bytes on the device
@@ -97,7 +104,7 @@ struct qs_ctx {
     bool saved = false;
     bool mirror_stale = false;  // device ran a stream since the last mirror sync
     qs_host::DevBuf diag;
-    qs_host::DevBuf scratch, lists, one_pod, one_podx, out_feas, out_score, out_total;
+    qs_host::DevBuf scratch, lists, clists, dio, one_pod, one_podx, out_feas, out_score, out_total;
     uint32_t cap = 0;
     // sharding (qs_open_shard): RCCL communicator of this rank, nullptr when unsharded
     int rank = 0, world = 1;
@@ -117,6 +124,8 @@ inline ShardPlan shard_plan(const qs_ctx *c) {
 }
 // The per-window exchange of the sharded engine (qs_dist.cpp): all-gather of each rank's
 // [K][GLp] list block into [world][K][GLp] (in place), on the context's stream.
-void exchange_lists(qs_ctx *c, uint64_t *lists, size_t per_rank_entries);
+void exchange_lists(qs_ctx *c, uint64_t *lists, size_t per_rank_entries, hipStream_t stream);
+// {count, nodes[64]} dirty-set hand-off between overlapped lookahead windows (+ pad)
+constexpr size_t kDioWords = 68;
 }  // namespace qs_host
 

@@ -27,10 +27,10 @@ const char *nccl_msg(ncclResult_t r) { return ncclGetErrorString(r); }
 
 namespace qs_host {
 
-void exchange_lists(qs_ctx *c, uint64_t *lists, size_t per_rank_entries) {
+void exchange_lists(qs_ctx *c, uint64_t *lists, size_t per_rank_entries, hipStream_t stream) {
     // in place: rank r's block already sits at lists + r * per_rank_entries
     NCCLCHK(ncclAllGather(lists + (size_t)c->rank * per_rank_entries, lists, per_rank_entries,
-                          ncclUint64, c->comm, c->stream));
+                          ncclUint64, c->comm, stream));
 }
 
 }  // namespace qs_host

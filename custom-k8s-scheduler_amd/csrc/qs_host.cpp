@@ -303,26 +303,27 @@ qs_status guarded(qs_ctx *c, F &&f) {
 // Per-launch HIP-event timing on the library's stream (config.profile_kernels).
 struct KernelTimer {
     bool on;
-    hipStream_t stream;
+    hipStream_t stream, stream2;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[4];
     double secs[4] = {0, 0, 0, 0};
     uint64_t count[4] = {0, 0, 0, 0};
-    KernelTimer(bool o, hipStream_t s) : on(o), stream(s) {}
-    void begin(int k) {
+    KernelTimer(bool o, hipStream_t s, hipStream_t s2) : on(o), stream(s), stream2(s2) {}
+    void begin(int k, hipStream_t s) {
         if (!on) return;
         hipEvent_t a, b;
         HIPCHK(hipEventCreate(&a));
         HIPCHK(hipEventCreate(&b));
-        HIPCHK(hipEventRecord(a, stream));
+        HIPCHK(hipEventRecord(a, s));
         ev[k].push_back({a, b});
     }
-    void end(int k) {
+    void end(int k, hipStream_t s) {
         if (!on) return;
-        HIPCHK(hipEventRecord(ev[k].back().second, stream));
+        HIPCHK(hipEventRecord(ev[k].back().second, s));
     }
     void finish() {
         if (!on) return;
         HIPCHK(hipStreamSynchronize(stream));
+        HIPCHK(hipStreamSynchronize(stream2));
         for (int k = 0; k < 4; k++) {
             for (auto &e : ev[k]) {
                 float ms = 0.f;
@@ -338,13 +339,14 @@ struct KernelTimer {
 };
 
 uint32_t la_window(const qs_ctx *c);
+bool la_overlap(const qs_ctx *c);
 
 int pick_engine(const qs_ctx *c, uint32_t n) {
     int e = c->cfg.engine;
     const uint32_t feat = c->dc.feat;
     if (e == QS_ENGINE_AUTO) {
         if (!(feat & (kFeatTaint | kFeatAffinity)) && n > 0 &&
-            la_geometry(n, la_window(c), shard_plan(c).W).G > 0)
+            la_geometry(n, la_window(c), shard_plan(c).W, 2 * la_window(c)).G > 0)
             e = QS_ENGINE_LOOKAHEAD;
         else if (n <= persistent_max_nodes(feat)) e = QS_ENGINE_PERSISTENT;
         else e = QS_ENGINE_SCAN;
@@ -357,9 +359,18 @@ int pick_engine(const qs_ctx *c, uint32_t n) {
     return e;
 }
 
-LaGeom lookahead_geometry(const qs_ctx *c, uint32_t n) {
+// Overlapped windows (select of window w+1 beside resolve of window w): on unless
+// cfg.lookahead_serial or QS_LA_OVERLAP=0; needs 2K <= 64 dirty slots, i.e. K <= 32.
+bool la_overlap(const qs_ctx *c) {
+    static const char *env = getenv("QS_LA_OVERLAP");
+    if (env && env[0] == '0') return false;
+    return !c->cfg.lookahead_serial && la_window(c) <= 32;
+}
+
+LaGeom lookahead_geometry(const qs_ctx *c, uint32_t n, bool overlap) {
     const ShardPlan sp = shard_plan(c);
-    LaGeom geo = la_geometry(n, la_window(c), sp.W);
+    const uint32_t K = la_window(c);
+    LaGeom geo = la_geometry(n, K, sp.W, overlap ? 2 * K : K);
     geo.v0 = sp.v0;
     geo.nv = sp.nv;
     return geo;
@@ -418,6 +429,7 @@ qs_status qs_open(const qs_config *cfg, int device, qs_ctx **out) {
         if (device < 0 || device >= ndev) fail(QS_EINVAL, "no such device");
         HIPCHK(hipSetDevice(device));
         HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        HIPCHK(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
         c->dc = make_devcfg(c->cfg);
         c->scratch.ensure(scan_scratch_bytes());
         HIPCHK(hipMemset(c->scratch.p, 0, scan_scratch_bytes()));
@@ -441,9 +453,11 @@ qs_status qs_close(qs_ctx *c) {
         if (c->comm) (void)ncclCommDestroy(c->comm);
         c->comm = nullptr;
     }
-    hipStream_t s = c->stream;
+    hipStream_t s = c->stream, s2 = c->stream2;
+    if (s2) (void)hipStreamSynchronize(s2);
     delete c;  // DevBuf destructors free device memory
     if (s) (void)hipStreamDestroy(s);
+    if (s2) (void)hipStreamDestroy(s2);
     return QS_OK;
 }
 
@@ -651,7 +665,7 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
         HIPCHK(hipEventCreate(&e0));
         HIPCHK(hipEventCreate(&e1));
         // config.profile_kernels: bracket every launch with events (untimed diagnostic runs)
-        KernelTimer kt(c->cfg.profile_kernels != 0, c->stream);
+        KernelTimer kt(c->cfg.profile_kernels != 0, c->stream, c->stream2);
         HIPCHK(hipEventRecord(e0, c->stream));
         if (P > 0 && n == 0) {
             HIPCHK(hipMemsetAsync(on, 0xFF, 4 * (size_t)P, c->stream));
@@ -660,31 +674,35 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
             const DPod *dp = s->d_pods.as<DPod>();
             const DPodX *dx = s->d_podx.as<DPodX>();
             if (eng == QS_ENGINE_PERSISTENT) {
-                kt.begin(0);
+                kt.begin(0, c->stream);
                 HIPCHK(launch_persistent(c->dt, dp, dx, P, c->dc, on, ok, st, c->stream));
-                kt.end(0);
+                kt.end(0, c->stream);
                 batches = 1;
             } else if (eng == QS_ENGINE_SCAN) {
                 HIPCHK(hipMemsetAsync(c->scratch.p, 0, scan_scratch_bytes(), c->stream));
                 for (uint32_t k = 0; k < P; k++) {
-                    kt.begin(1);
+                    kt.begin(1, c->stream);
                     HIPCHK(launch_scan_pod(c->dt, dp, dx, k, c->dc, c->scratch.p, on, ok, st,
                                            nullptr, nullptr, nullptr, true, c->stream));
-                    kt.end(1);
+                    kt.end(1, c->stream);
                 }
                 batches = P;
             } else {
-                LaGeom geo = lookahead_geometry(c, n);
+                const bool overlap = la_overlap(c);
+                LaGeom geo = lookahead_geometry(c, n, overlap);
                 static const char *rw = getenv("QS_RESOLVER_WAVES");  // 1 = single-wave resolver
-                geo.waves = (rw && rw[0] == '1') ? 1u : 4u;
+                geo.waves = (rw && rw[0] == '1' && !overlap) ? 1u : 4u;
                 int64_t wmax = 0;
                 for (int q = 0; q < 3; q++) wmax = std::max<int64_t>(wmax, (int64_t)c->cfg.w_fit[q] + c->cfg.w_bal[q]);
                 geo.k32 = (100 * wmax + 1 < 1024 && n <= (1u << 22)) ? 1u : 0u;
                 if (geo.G == 0) fail(QS_EINVAL, "no lookahead geometry for this table size");
                 const size_t rank_entries = (size_t)geo.K * 64 * geo.eplr;  // [K][GLp] per shard
-                const size_t lbytes = 8ull * geo.W * rank_entries;
-                c->lists.ensure(lbytes);
-                HIPCHK(hipMemsetAsync(c->lists.p, 0, lbytes, c->stream));  // padding entries stay 0
+                const size_t lwords = geo.W * rank_entries;                 // one window's lists
+                const size_t cwords = std::max<size_t>(1, (size_t)geo.nv * geo.K * geo.G * geo.L);
+                const int nbuf = overlap ? 2 : 1;  // overlapped windows double-buffer the lists
+                c->lists.ensure(8 * lwords * nbuf);
+                c->clists.ensure(8 * cwords * nbuf);
+                c->dio.ensure(2 * kDioWords * 4);
                 // QS_DIAG=1: diagnostic resolver with per-segment shader-clock stamps (stderr)
                 static const bool diag_on = getenv("QS_DIAG") && getenv("QS_DIAG")[0] == '1';
                 uint64_t *diag = nullptr;
@@ -693,18 +711,113 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                     HIPCHK(hipMemsetAsync(c->diag.p, 0, 64, c->stream));
                     diag = c->diag.as<uint64_t>();
                 }
-                for (uint32_t s0 = 0; s0 < P; s0 += geo.K) {
-                    kt.begin(2);
-                    HIPCHK(launch_la_window(c->dt, dp, s0, P, c->dc, geo, c->lists.as<uint64_t>(), on,
-                                            ok, st, diag, c->stream, 1));
-                    kt.end(2);
-                    if (c->comm) exchange_lists(c, c->lists.as<uint64_t>(), rank_entries);
-                    kt.begin(3);
-                    HIPCHK(launch_la_window(c->dt, dp, s0, P, c->dc, geo, c->lists.as<uint64_t>(), on,
-                                            ok, st, diag, c->stream, 2));
-                    kt.end(3);
-                    ++batches;
+                uint64_t *L0 = c->lists.as<uint64_t>(), *C0 = c->clists.as<uint64_t>();
+                uint32_t *dio = c->dio.as<uint32_t>();
+                const uint32_t nwin = (P + geo.K - 1) / geo.K;
+                const auto th0 = std::chrono::steady_clock::now();
+                auto enqueue = [&]() {
+                HIPCHK(hipMemsetAsync(c->lists.p, 0, 8 * lwords * nbuf, c->stream));  // padding stays 0
+                HIPCHK(hipMemsetAsync(c->dio.p, 0, 2 * kDioWords * 4, c->stream));
+                // select (+ merge, + the RCCL exchange when sharded) of window w on stream `ss`
+                auto select = [&](uint32_t w, hipStream_t ss) {
+                    const int b = overlap ? (int)(w & 1) : 0;
+                    kt.begin(2, ss);
+                    HIPCHK(launch_la_window(c->dt, dp, w * geo.K, P, c->dc, geo, L0 + b * lwords,
+                                            C0 + b * cwords, on, ok, st, diag, nullptr, nullptr, ss, 1));
+                    kt.end(2, ss);
+                    if (c->comm) exchange_lists(c, L0 + b * lwords, rank_entries, ss);
+                };
+                auto resolve = [&](uint32_t w) {
+                    const int b = overlap ? (int)(w & 1) : 0;
+                    kt.begin(3, c->stream);
+                    HIPCHK(launch_la_window(c->dt, dp, w * geo.K, P, c->dc, geo, L0 + b * lwords,
+                                            C0 + b * cwords, on, ok, st, diag,
+                                            overlap ? dio + ((w + 1) & 1) * kDioWords : nullptr,
+                                            overlap ? dio + (w & 1) * kDioWords : nullptr,
+                                            c->stream, 2));
+                    kt.end(3, c->stream);
+                };
+                if (!overlap) {
+                    for (uint32_t w = 0; w < nwin; ++w) {
+                        select(w, c->stream);
+                        resolve(w);
+                    }
+                } else {
+                    // select(w+1) on the second stream runs beside resolve(w): it reads the table
+                    // after resolve(w-1), so the resolver treats the nodes of window w as dirty too
+                    // (lists of L = 2K keys).  Event rings order the two chains.
+                    constexpr int R = 4;
+                    hipEvent_t esel[R], eres[R], est;
+                    for (int r = 0; r < R; ++r) {
+                        HIPCHK(hipEventCreateWithFlags(&esel[r], hipEventDisableTiming));
+                        HIPCHK(hipEventCreateWithFlags(&eres[r], hipEventDisableTiming));
+                    }
+                    HIPCHK(hipEventCreateWithFlags(&est, hipEventDisableTiming));
+                    HIPCHK(hipEventRecord(est, c->stream));
+                    HIPCHK(hipStreamWaitEvent(c->stream2, est, 0));
+                    select(0, c->stream2);
+                    HIPCHK(hipEventRecord(esel[0], c->stream2));
+                    for (uint32_t w = 0; w < nwin; ++w) {
+                        if (w + 1 < nwin) {
+                            if (w >= 1) HIPCHK(hipStreamWaitEvent(c->stream2, eres[(w - 1) % R], 0));
+                            select(w + 1, c->stream2);
+                            HIPCHK(hipEventRecord(esel[(w + 1) % R], c->stream2));
+                        }
+                        HIPCHK(hipStreamWaitEvent(c->stream, esel[w % R], 0));
+                        resolve(w);
+                        HIPCHK(hipEventRecord(eres[w % R], c->stream));
+                    }
+                    for (int r = 0; r < R; ++r) {
+                        (void)hipEventDestroy(esel[r]);
+                        (void)hipEventDestroy(eres[r]);
+                    }
+                    (void)hipEventDestroy(est);
                 }
+                };
+                // Replay the whole window sequence as one HIP graph (built on the first run of this
+                // prepared stream): ~3 launches + 4 event operations per window would otherwise
+                // be issued one host call at a time.  Not used for diagnostic runs.
+                static const char *genv = getenv("QS_GRAPH");
+                const bool use_graph = !kt.on && !diag_on && !(genv && genv[0] == '0');
+                if (use_graph) {
+                    std::vector<uint8_t> key;
+                    auto put = [&](const void *p, size_t nb) {
+                        key.insert(key.end(), (const uint8_t *)p, (const uint8_t *)p + nb);
+                    };
+                    const void *ptrs[] = {c->dt.rows, c->dt.masks, L0, C0, dio, st, (void *)c->comm, dp};
+                    put(ptrs, sizeof ptrs);
+                    put(&c->dt.n, sizeof c->dt.n);
+                    put(&c->dc, sizeof c->dc);
+                    put(&geo, sizeof geo);
+                    put(&overlap, sizeof overlap);
+                    if (!s->gexec || s->gkey != key) {
+                        if (s->gexec) (void)hipGraphExecDestroy(s->gexec);
+                        s->gexec = nullptr;
+                        HIPCHK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+                        try {
+                            enqueue();
+                        } catch (...) {
+                            hipGraph_t g = nullptr;
+                            (void)hipStreamEndCapture(c->stream, &g);
+                            if (g) (void)hipGraphDestroy(g);
+                            throw;
+                        }
+                        hipGraph_t g = nullptr;
+                        HIPCHK(hipStreamEndCapture(c->stream, &g));
+                        const hipError_t ie = hipGraphInstantiate(&s->gexec, g, nullptr, nullptr, 0);
+                        (void)hipGraphDestroy(g);
+                        HIPCHK(ie);
+                        s->gkey = key;
+                    }
+                    HIPCHK(hipGraphLaunch(s->gexec, c->stream));
+                } else {
+                    enqueue();
+                }
+                batches = nwin;
+                if (getenv("QS_HOSTTIME"))
+                    fprintf(stderr, "QS_HOSTTIME enqueue %.3f ms for %u windows (overlap %d)\n",
+                            std::chrono::duration<double>(std::chrono::steady_clock::now() - th0).count() * 1e3,
+                            nwin, (int)overlap);
                 if (diag_on) {
                     uint64_t h[8] = {0};
                     HIPCHK(hipMemcpyAsync(h, diag, 48, hipMemcpyDeviceToHost, c->stream));

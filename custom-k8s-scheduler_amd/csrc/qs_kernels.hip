@@ -211,50 +211,25 @@ __device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t (*buf)[NW], i
     return s;
 }
 
-// Grid: K pods × G node-chunks.  Block (k, g) scores pod s0+k on chunk g and writes the top-L
-// keys of that chunk (lowest node index first among equal totals) to lists[(k*G+g)*L ...].
-// Wave w owns the contiguous sub-range [start + w*E*64, start + (w+1)*E*64), so node-index order
-// is (wave, j, lane) order and tie ranks come from ballots + one cross-wave prefix.
-template <int BS, int E, uint32_t F>
-__global__ __launch_bounds__(BS) void k_la_select(DevTable t, const DPod *__restrict__ pods,
-                                                  DevCfg c, uint32_t s0, uint32_t P, LaShard sh,
-                                                  uint32_t G, uint32_t L, uint32_t chunk,
-                                                  uint32_t GLp, uint64_t *__restrict__ lists) {
+// Block-wide top-L of per-position values tv (0 = empty).  Position order is (wave, j, lane):
+// wave w owns positions [w*E*64, (w+1)*E*64), so when positions follow node-index order, ranks
+// come from ballots and one cross-wave prefix.  Writes the keys of the L largest values to
+// out[0..L): every value > T (the L-th largest) in position order, then the ties at T lowest
+// position first; zero-fills the rest.  keyf(j) = key of this lane's j-th position.
+// Used twice: per node chunk in k_la_select (positions = node indices) and per pod in
+// k_la_merge (positions = chunk-major list slots, so equal totals stay in node-index order).
+template <int BS, int E, class KeyF>
+__device__ __forceinline__ void block_topl(const uint32_t (&tv)[E], uint32_t L,
+                                           uint64_t *__restrict__ out, KeyF keyf) {
     constexpr int NW = BS / kWave;
     __shared__ uint32_t cnt[2][NW];
-    __shared__ uint32_t slot_ctr;
-    // block -> (shard v, pod k, chunk g); shard v owns nodes [v*n/W, (v+1)*n/W)
-    const uint32_t per = sh.kw * G;
-    const uint32_t v = sh.v0 + blockIdx.x / per, rem = blockIdx.x % per;
-    const uint32_t k = rem / G, g = rem % G;
-    const uint32_t s = s0 + k;
-    if (s >= P) return;
+    __shared__ uint32_t cnt2[NW];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const DPod p = pods[s];
-    const DPodX px{};
-    const uint32_t lo = (uint32_t)((uint64_t)v * t.n / sh.W);
-    const uint32_t hi = (uint32_t)((uint64_t)(v + 1) * t.n / sh.W);
-    const uint32_t start = lo + g * chunk;
-    const uint32_t end = min(hi, start + chunk);
-    const uint32_t base = start + (uint32_t)w * E * kWave + lane;
-    uint32_t tv[E];
     uint32_t lmax = 0;
 #pragma unroll
-    for (int j = 0; j < E; ++j) {
-        const uint32_t idx = base + j * kWave;
-        tv[j] = 0;
-        if (idx < end) {
-            const Row r = load_row(t, idx);
-            const RowX x = load_rowx<F>(t, idx);
-            const bool f = feasible<F>(r, x, p, px);
-            const uint32_t tot = node_total<F>(r, x, p, px, c, 0, 0.0, 0, 0.0, nullptr);
-            tv[j] = f ? tot + 1 : 0;
-        }
-        lmax = tv[j] > lmax ? tv[j] : lmax;
-    }
+    for (int j = 0; j < E; ++j) lmax = tv[j] > lmax ? tv[j] : lmax;
     int par = 0;
-    if (tid == 0) slot_ctr = 0;
-    // block max of tv (reuse the sum buffer: a max of wave maxima)
+    // block max of tv (a max of wave maxima through the sum buffer)
     const uint32_t wmax = wave_max_u32(lmax);
     if (lane == 0) cnt[par][w] = wmax;
     __syncthreads();
@@ -268,7 +243,7 @@ __global__ __launch_bounds__(BS) void k_la_select(DevTable t, const DPod *__rest
         for (int j = 0; j < E; ++j) cw += (uint32_t)__popcll(__ballot(tv[j] >= thr));
         return block_sum<NW>(cw, cnt, par, lane, w);
     };
-    // T = largest threshold with count(tv >= T) >= L, or 1 if fewer than L feasible nodes.
+    // T = largest threshold with count(tv >= T) >= L, or 1 if fewer than L non-empty positions.
     uint32_t T = 1;
     if (maxtv > 0) {
         const uint32_t call = count_ge(1);
@@ -285,41 +260,107 @@ __global__ __launch_bounds__(BS) void k_la_select(DevTable t, const DPod *__rest
             }
         }
     }
-    const uint32_t c_gt = count_ge(T + 1);  // < L (or all feasible when fewer than L)
-    const uint32_t need = L > c_gt ? L - c_gt : 0;
-    // ties at T, lowest index first: rank = (ties in earlier waves) + (earlier j) + mbcnt
-    uint64_t tb[E];
-    uint32_t tie_w = 0;
+    // ballots of "> T" and "== T" per j; one barrier publishes both per-wave counts
+    uint64_t gb[E], tb[E];
+    uint32_t gt_w = 0, tie_w = 0;
 #pragma unroll
     for (int j = 0; j < E; ++j) {
+        gb[j] = __ballot(tv[j] > T);
         tb[j] = __ballot(tv[j] == T && maxtv > 0);
+        gt_w += (uint32_t)__popcll(gb[j]);
         tie_w += (uint32_t)__popcll(tb[j]);
     }
-    if (lane == 0) cnt[par][w] = tie_w;
+    if (lane == 0) { cnt[par][w] = gt_w; cnt2[w] = tie_w; }
     __syncthreads();
-    uint32_t rank = 0, ties_total = 0;
+    uint32_t rg = 0, rt = 0, c_gt = 0, ties_total = 0;
 #pragma unroll
     for (int i = 0; i < NW; ++i) {
-        const uint32_t v = cnt[par][i];
-        rank += i < w ? v : 0u;
-        ties_total += v;
+        const uint32_t a = cnt[par][i], b = cnt2[i];
+        rg += i < w ? a : 0u;
+        rt += i < w ? b : 0u;
+        c_gt += a;
+        ties_total += b;
     }
-    uint64_t *out = lists + (size_t)v * sh.RS + (size_t)k * GLp + (size_t)g * L;
+    const uint32_t need = L > c_gt ? L - c_gt : 0;  // c_gt < L unless fewer than L positions
     const uint64_t lane_mask_lt = (1ull << lane) - 1ull;
 #pragma unroll
     for (int j = 0; j < E; ++j) {
-        const uint32_t idx = base + j * kWave;
-        if (tv[j] > T) {
-            const uint32_t sl = atomicAdd(&slot_ctr, 1u);
-            out[sl] = pack_key(tv[j], idx);
+        if ((gb[j] >> lane) & 1ull) {
+            out[rg + (uint32_t)__popcll(gb[j] & lane_mask_lt)] = keyf(j);
         } else if ((tb[j] >> lane) & 1ull) {
-            const uint32_t rk = rank + (uint32_t)__popcll(tb[j] & lane_mask_lt);
-            if (rk < need) out[c_gt + rk] = pack_key(tv[j], idx);
+            const uint32_t rk = rt + (uint32_t)__popcll(tb[j] & lane_mask_lt);
+            if (rk < need) out[c_gt + rk] = keyf(j);
         }
-        rank += (uint32_t)__popcll(tb[j]);
+        rg += (uint32_t)__popcll(gb[j]);
+        rt += (uint32_t)__popcll(tb[j]);
     }
     const uint32_t written = c_gt + (ties_total < need ? ties_total : need);
     for (uint32_t i = written + tid; i < L; i += BS) out[i] = 0;
+}
+
+// Grid: shards × pods × G node-chunks.  Block (v, k, g) scores pod s0+k on chunk g of shard v
+// (Filter + Score in registers, against the window-start table) and writes the chunk's top-L
+// keys to out: straight into the final lists when G == 1, else into the chunk-list scratch
+// [nv][kw][G][L] that k_la_merge reduces to one top-L per pod and shard.
+template <int BS, int E, uint32_t F>
+__global__ __launch_bounds__(BS) void k_la_select(DevTable t, const DPod *__restrict__ pods,
+                                                  DevCfg c, uint32_t s0, uint32_t P, LaShard sh,
+                                                  uint32_t G, uint32_t L, uint32_t chunk,
+                                                  uint32_t GLp, uint64_t *__restrict__ lists,
+                                                  uint64_t *__restrict__ clists) {
+    // block -> (shard v, pod k, chunk g); shard v owns nodes [v*n/W, (v+1)*n/W)
+    const uint32_t per = sh.kw * G;
+    const uint32_t vs = blockIdx.x / per, rem = blockIdx.x % per;
+    const uint32_t v = sh.v0 + vs;
+    const uint32_t k = rem / G, g = rem % G;
+    const uint32_t s = s0 + k;
+    if (s >= P) return;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const DPod p = pods[s];
+    const DPodX px{};
+    const uint32_t lo = (uint32_t)((uint64_t)v * t.n / sh.W);
+    const uint32_t hi = (uint32_t)((uint64_t)(v + 1) * t.n / sh.W);
+    const uint32_t start = lo + g * chunk;
+    const uint32_t end = min(hi, start + chunk);
+    const uint32_t base = start + (uint32_t)w * E * kWave + lane;
+    uint32_t tv[E];
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+        const uint32_t idx = base + j * kWave;
+        tv[j] = 0;
+        if (idx < end) {
+            const Row r = load_row(t, idx);
+            const RowX x = load_rowx<F>(t, idx);
+            const bool f = feasible<F>(r, x, p, px);
+            const uint32_t tot = node_total<F>(r, x, p, px, c, 0, 0.0, 0, 0.0, nullptr);
+            tv[j] = f ? tot + 1 : 0;
+        }
+    }
+    uint64_t *out = G == 1 ? lists + (size_t)v * sh.RS + (size_t)k * GLp
+                           : clists + (((size_t)vs * sh.kw + k) * G + g) * L;
+    block_topl<BS, E>(tv, L, out, [&](int j) { return pack_key(tv[j], base + j * kWave); });
+}
+
+// Grid: shards × pods.  Reduces a pod's G chunk lists (M = G*L keys, chunk-major: equal totals
+// sit in node-index order) to its top-L in the final [W][K][GLp] lists the resolver reads, so the
+// resolver scans L keys per pod instead of G*L.
+template <int E2>
+__global__ __launch_bounds__(256) void k_la_merge(const uint64_t *__restrict__ clists, uint32_t M,
+                                                  uint32_t L, LaShard sh, uint32_t GLp,
+                                                  uint64_t *__restrict__ lists) {
+    const uint32_t vs = blockIdx.x / sh.kw, k = blockIdx.x % sh.kw;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint64_t *in = clists + ((size_t)vs * sh.kw + k) * M;
+    uint64_t e[E2];
+    uint32_t tv[E2];
+#pragma unroll
+    for (int j = 0; j < E2; ++j) {
+        const uint32_t pos = (uint32_t)w * E2 * kWave + (uint32_t)j * kWave + lane;
+        e[j] = pos < M ? in[pos] : 0ull;
+        tv[j] = (uint32_t)(e[j] >> 32);
+    }
+    block_topl<256, E2>(tv, L, lists + (size_t)(sh.v0 + vs) * sh.RS + (size_t)k * GLp,
+                        [&](int j) { return e[j]; });
 }
 
 // Entry m (0 <= m < EPL) of resolver lane `lane` for window pod `pod`.  Lists are laid out
@@ -531,7 +572,9 @@ __global__ __launch_bounds__(256) void k_la_resolve4(DevTable t, const DPod *__r
                                                      int32_t *__restrict__ out_node,
                                                      uint64_t *__restrict__ out_key,
                                                      uint64_t *__restrict__ stamps,
-                                                     uint64_t *__restrict__ diag) {
+                                                     uint64_t *__restrict__ diag,
+                                                     const uint32_t *__restrict__ dprev,
+                                                     uint32_t *__restrict__ dcur) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -554,6 +597,15 @@ __global__ __launch_bounds__(256) void k_la_resolve4(DevTable t, const DPod *__r
     const uint32_t kend = min(K, P - s0);
     if (threadIdx.x < kend) wpods[threadIdx.x] = pods[s0 + threadIdx.x];
     const DPodX px{};
+    // Overlapped windows (dprev != nullptr): this window's lists were selected against the table
+    // as it stood BEFORE the previous window, so the nodes that window dirtied (dprev[1..nd0])
+    // start as dirty slots: their list entries are stale and their rows are re-read here.
+    const uint32_t nd0 = dprev ? dprev[0] : 0u;
+    __syncthreads();
+    if (threadIdx.x < nd0) {
+        const uint32_t nn = dprev[1 + threadIdx.x];
+        atomicOr(&dirty[nn >> 5], 1u << (nn & 31));
+    }
     __syncthreads();
     if (kend == 0) return;
     uint64_t dsum = 0, tprev = 0;
@@ -564,7 +616,8 @@ __global__ __launch_bounds__(256) void k_la_resolve4(DevTable t, const DPod *__r
     // the barriers pair up.  Roles never share registers, which keeps waitcnt placement local.
     if (wv == 0) {
         // ---- D: pod i's winner from the precomputed keys ---------------------------------------
-        uint32_t nd = 0, didx = 0xFFFFFFFFu;
+        uint32_t nd = nd0, didx = (uint32_t)lane < nd0 ? dprev[1 + lane] : 0xFFFFFFFFu;
+        bool won = false;  // slot won a pod of THIS window (it belongs to the next window's dprev)
         uint64_t res_key = 0, res_stamp = 0;
         ResPub pv{0, 0xFFFFFFFFu, -1, -1, 0, {0, 0}};  // D produced it: kept in registers
         __syncthreads();  // prologue barrier (wave C publishes pod 0's candidates)
@@ -573,7 +626,7 @@ __global__ __launch_bounds__(256) void k_la_resolve4(DevTable t, const DPod *__r
             const int par = i & 1, pp = par ^ 1;
             // every LDS read of the step is independent of this step: one batch, one wait
             const uint64_t a = keyA[pp][lane], b = keyB[pp][lane], cl = keyC[pp][lane];
-            const uint64_t e1 = C1[pp][lane], e2 = C2[pp][lane];
+            const uint64_t e1 = C1[pp][lane], e2 = EPL > 1 ? C2[pp][lane] : 0ull;
             const bool pnew = pv.ks != 0 && pv.slot < 0;
             const uint64_t sc = (lane == pv.slot) ? b : a;
             uint64_t fk = ((uint32_t)lane < nd && sc) ? (sc | (uint64_t)(0xFFFFFFFFu - didx)) : 0ull;
@@ -598,9 +651,10 @@ __global__ __launch_bounds__(256) void k_la_resolve4(DevTable t, const DPod *__r
                 const uint64_t own = __ballot((uint32_t)lane < nd && didx == np.w);
                 if (own) {
                     np.slot = (int32_t)__builtin_ctzll(own);
+                    won |= lane == np.slot;
                 } else {
                     np.src = (int32_t)__builtin_ctzll(__ballot(cand == ks));
-                    if ((uint32_t)lane == nd) didx = np.w;
+                    if ((uint32_t)lane == nd) { didx = np.w; won = true; }
                     ++nd;
                 }
             }
@@ -620,11 +674,26 @@ __global__ __launch_bounds__(256) void k_la_resolve4(DevTable t, const DPod *__r
             if (stamps) stamps[s] = res_stamp;
         }
         if ((uint32_t)lane < nd) slotnode[lane] = didx;
+        if (dcur) {  // nodes dirtied in this window, for the next (overlapped) window
+            const uint64_t wm = __ballot(won && (uint32_t)lane < nd);
+            if (won && (uint32_t)lane < nd) dcur[1 + __popcll(wm & ((1ull << lane) - 1ull))] = didx;
+            if (lane == 0) dcur[0] = (uint32_t)__popcll(wm);
+        }
     } else if (wv <= 2) {
         // ---- A / B: apply pod i-1 to the slot copy, then the next pod's keys --------------------
         Row S = empty_row();
         RowX SX{};
-        uint32_t nd = 0;
+        uint32_t nd = nd0;
+        if ((uint32_t)lane < nd0) {
+            const uint32_t nn = dprev[1 + lane];
+            S = load_row(t, nn);
+            SX = load_rowx<F>(t, nn);
+        }
+        if (wv == 1 && nd0 > 0) {  // pod 0's keys of the inherited slots ("not the winner" case)
+            const bool f = feasible<F>(S, SX, wpods[0], px);
+            const uint32_t tot = node_total<F>(S, SX, wpods[0], px, c, 0, 0.0, 0, 0.0, nullptr);
+            keyA[1][lane] = ((uint32_t)lane < nd && f) ? ((uint64_t)(tot + 1) << 32) : 0ull;
+        }
         auto apply = [&](const ResPub &pv, int pp, const DPod &pprev) {
             if (pv.ks == 0) return;
             if (pv.slot >= 0) {
@@ -700,16 +769,20 @@ __global__ __launch_bounds__(256) void k_la_resolve4(DevTable t, const DPod *__r
         }
         load_ent(eX, 1);
         load_ent(eY, 2);
+        // EPL == 1 (merged lists): a lane holds one entry, so its second candidate is always empty
+        constexpr bool TWO = EPL > 1;
         C1[1][lane] = c1;
-        C2[1][lane] = c2;
-        Row r1 = load_row(t, c1 ? key_node(c1) : 0u), r2 = load_row(t, c2 ? key_node(c2) : 0u);
-        RowX x1 = load_rowx<F>(t, c1 ? key_node(c1) : 0u), x2 = load_rowx<F>(t, c2 ? key_node(c2) : 0u);
+        if (TWO) C2[1][lane] = c2;
+        Row r1 = load_row(t, c1 ? key_node(c1) : 0u), r2 = TWO ? load_row(t, c2 ? key_node(c2) : 0u) : empty_row();
+        RowX x1 = load_rowx<F>(t, c1 ? key_node(c1) : 0u), x2 = TWO ? load_rowx<F>(t, c2 ? key_node(c2) : 0u) : RowX{};
         __syncthreads();
         auto step = [&](uint32_t i, uint64_t(&en)[EPL]) {
             QS_DIAG_BEGIN()
             const int par = i & 1, pp = par ^ 1;
             const ResPub pv = read_pub(&pub[pp]);
-            if (lane == 0 && pv.ks != 0 && pv.slot < 0) dirty[pv.w >> 5] |= 1u << (pv.w & 31);
+            if (lane == 0 && pv.ks != 0 && pv.slot < 0)
+                __hip_atomic_fetch_or(&dirty[pv.w >> 5], 1u << (pv.w & 31), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_WORKGROUP);  // ds_or: no round trip
             const bool use2 = pv.ks != 0 && c1 != 0 && key_node(c1) == pv.w;
             const uint64_t cc = use2 ? c2 : c1;
             const Row crow = sel_row(use2, r2, r1);
@@ -720,11 +793,13 @@ __global__ __launch_bounds__(256) void k_la_resolve4(DevTable t, const DPod *__r
                 const DPod p = wpods[i], pn1 = wpods[i + 1];
                 top2(en, c1, c2);  // pod i+1 against the dirty set through pod i-1
                 C1[par][lane] = c1;
-                C2[par][lane] = c2;
+                if (TWO) C2[par][lane] = c2;
                 r1 = load_row(t, c1 ? key_node(c1) : 0u);
-                r2 = load_row(t, c2 ? key_node(c2) : 0u);
                 x1 = load_rowx<F>(t, c1 ? key_node(c1) : 0u);
-                x2 = load_rowx<F>(t, c2 ? key_node(c2) : 0u);
+                if (TWO) {
+                    r2 = load_row(t, c2 ? key_node(c2) : 0u);
+                    x2 = load_rowx<F>(t, c2 ? key_node(c2) : 0u);
+                }
                 load_ent(en, i + 3);
                 Row cr = crow;
                 RowX crx = cx;
@@ -867,21 +942,33 @@ size_t scan_scratch_bytes() { return sizeof(ScanScratch); }
 
 template <uint32_t F>
 static hipError_t la_window_f(const DevTable &t, const DPod *pods, uint32_t s0, uint32_t P,
-                              const DevCfg &c, const LaGeom &geo, uint64_t *lists, int32_t *on,
-                              uint64_t *ok, uint64_t *st, uint64_t *diag, hipStream_t stream,
-                              int part) {
+                              const DevCfg &c, const LaGeom &geo, uint64_t *lists,
+                              uint64_t *clists, int32_t *on, uint64_t *ok, uint64_t *st,
+                              uint64_t *diag, const uint32_t *dprev, uint32_t *dcur,
+                              hipStream_t stream, int part) {
     const uint32_t K = geo.K, G = geo.G, L = geo.L, GLp = geo.eplr * 64;
     const uint32_t kw = min(K, P - s0);
     LaShard sh{geo.W, geo.v0, kw, 0u, (uint64_t)K * GLp};
     if (part & 1) {
         const dim3 grid(geo.nv * kw * G);
         switch (geo.E) {
-#define QS_SEL(EE) case EE: hipLaunchKernelGGL((k_la_select<256, EE, F>), grid, dim3(256), 0, stream, t, pods, c, s0, P, sh, G, L, geo.chunk, GLp, lists); break;
+#define QS_SEL(EE) case EE: hipLaunchKernelGGL((k_la_select<256, EE, F>), grid, dim3(256), 0, stream, t, pods, c, s0, P, sh, G, L, geo.chunk, GLp, lists, clists); break;
             QS_SEL(1) QS_SEL(2) QS_SEL(3) QS_SEL(4) QS_SEL(5) QS_SEL(6) QS_SEL(8) QS_SEL(10) QS_SEL(12) QS_SEL(16)
 #undef QS_SEL
             default: return hipErrorInvalidValue;
         }
         QS_RET(hipGetLastError());
+        if (G > 1) {
+            const uint32_t M = G * L, e2 = (M + 255) / 256;
+            const dim3 mgrid(geo.nv * kw);
+            switch (e2) {
+#define QS_MRG(EE) case EE: hipLaunchKernelGGL((k_la_merge<EE>), mgrid, dim3(256), 0, stream, clists, M, L, sh, GLp, lists); break;
+                QS_MRG(1) QS_MRG(2) QS_MRG(3) QS_MRG(4) QS_MRG(5) QS_MRG(6) QS_MRG(7) QS_MRG(8)
+#undef QS_MRG
+                default: return hipErrorInvalidValue;
+            }
+            QS_RET(hipGetLastError());
+        }
     }
     if (part & 2) {
         const size_t bm = (((t.n + 31) / 32 + 3) & ~3u) * 4;
@@ -893,9 +980,9 @@ static hipError_t la_window_f(const DevTable &t, const DPod *pods, uint32_t s0, 
                 if (diag) hipLaunchKernelGGL((k_la_resolve<F, EP, true>), dim3(1), dim3(64), lds, stream, t, pods, c, s0, P, K, GLp, geo.lr, sh, lists, on, ok, st, diag); \
                 else hipLaunchKernelGGL((k_la_resolve<F, EP, false>), dim3(1), dim3(64), lds, stream, t, pods, c, s0, P, K, GLp, geo.lr, sh, lists, on, ok, st, diag); \
             } else { \
-                if (diag) hipLaunchKernelGGL((k_la_resolve4<F, EP, true, false>), dim3(1), dim3(256), lds4, stream, t, pods, c, s0, P, K, GLp, geo.lr, sh, lists, on, ok, st, diag); \
-                else if (geo.k32) hipLaunchKernelGGL((k_la_resolve4<F, EP, false, true>), dim3(1), dim3(256), lds4, stream, t, pods, c, s0, P, K, GLp, geo.lr, sh, lists, on, ok, st, diag); \
-                else hipLaunchKernelGGL((k_la_resolve4<F, EP, false, false>), dim3(1), dim3(256), lds4, stream, t, pods, c, s0, P, K, GLp, geo.lr, sh, lists, on, ok, st, diag); \
+                if (diag) hipLaunchKernelGGL((k_la_resolve4<F, EP, true, false>), dim3(1), dim3(256), lds4, stream, t, pods, c, s0, P, K, GLp, geo.lr, sh, lists, on, ok, st, diag, dprev, dcur); \
+                else if (geo.k32) hipLaunchKernelGGL((k_la_resolve4<F, EP, false, true>), dim3(1), dim3(256), lds4, stream, t, pods, c, s0, P, K, GLp, geo.lr, sh, lists, on, ok, st, diag, dprev, dcur); \
+                else hipLaunchKernelGGL((k_la_resolve4<F, EP, false, false>), dim3(1), dim3(256), lds4, stream, t, pods, c, s0, P, K, GLp, geo.lr, sh, lists, on, ok, st, diag, dprev, dcur); \
             } break;
             QS_RES(1) QS_RES(2) QS_RES(4) QS_RES(8) QS_RES(16)
 #undef QS_RES
@@ -906,48 +993,48 @@ static hipError_t la_window_f(const DevTable &t, const DPod *pods, uint32_t s0, 
 }
 
 hipError_t launch_la_window(const DevTable &t, const DPod *pods, uint32_t s0, uint32_t P,
-                            const DevCfg &c, const LaGeom &geo, uint64_t *lists, int32_t *on,
-                            uint64_t *ok, uint64_t *st, uint64_t *diag, hipStream_t stream,
-                            int part) {
+                            const DevCfg &c, const LaGeom &geo, uint64_t *lists, uint64_t *clists,
+                            int32_t *on, uint64_t *ok, uint64_t *st, uint64_t *diag,
+                            const uint32_t *dprev, uint32_t *dcur, hipStream_t stream, int part) {
     if (c.feat & kFeatNorm) return hipErrorInvalidValue;
-    if (c.feat & kFeatExt) return la_window_f<kFeatExt>(t, pods, s0, P, c, geo, lists, on, ok, st, diag, stream, part);
-    return la_window_f<0>(t, pods, s0, P, c, geo, lists, on, ok, st, diag, stream, part);
+    if (dprev && geo.waves == 1) return hipErrorInvalidValue;  // overlap needs the 4-wave resolver
+    if (c.feat & kFeatExt) return la_window_f<kFeatExt>(t, pods, s0, P, c, geo, lists, clists, on, ok, st, diag, dprev, dcur, stream, part);
+    return la_window_f<0>(t, pods, s0, P, c, geo, lists, clists, on, ok, st, diag, dprev, dcur, stream, part);
 }
 
-LaGeom la_geometry(uint32_t n, uint32_t K, uint32_t W) {
-    // Per shard (W shards of <= ceil(n/W) nodes; W = 1 unsharded): G node chunks per pod of about
-    // 1,280 nodes (E = 5 per lane of a 256-thread block), capped so the resolver sees at most
-    // 1,024 list entries per pod in total (16 per lane) over all shards.
+LaGeom la_geometry(uint32_t n, uint32_t K, uint32_t W, uint32_t L) {
+    // Per shard (W shards of <= ceil(n/W) nodes; W = 1 unsharded): G node chunks of `chunk` nodes
+    // per pod (E nodes per lane of a 256-thread select block; about 1,280 nodes by default, env
+    // QS_LA_E overrides E), each keeping its top-L; k_la_merge reduces the G*L <= 2,048 keys to one
+    // top-L per pod and shard, so a shard contributes L <= 64 keys (one 64-entry block, eplr = 1)
+    // and the resolver reads epl = pow2 >= W entries per lane.
     static const uint32_t Es[] = {1, 2, 3, 4, 5, 6, 8, 10, 12, 16};
+    static const char *env_e = getenv("QS_LA_E");
+    const uint32_t e_target = env_e ? (uint32_t)std::max(1, atoi(env_e)) : 5u;
     LaGeom g{};
     g.K = K;
-    g.L = K;
+    g.L = std::max(K, L);
     g.W = std::max(1u, W);
     g.v0 = 0;
     g.nv = g.W;
-    if (g.W > 16) return g;  // G = 0: no geometry
-    uint32_t eplr_max = 1;   // largest power of two with W * eplr <= 16
-    while (g.W * eplr_max * 2 <= 16) eplr_max *= 2;
+    if (g.W > 16 || g.L > 64) return g;  // G = 0: no geometry
     const uint32_t ns = (n + g.W - 1) / g.W;
-    const uint32_t gmax = (eplr_max * 64) / g.L;
-    if (gmax == 0) return g;
-    uint32_t G = std::max(1u, std::min(gmax, (ns + 1279) / 1280));
+    const uint32_t gmax = 2048u / g.L;
+    const uint32_t target = e_target * 256u;
+    uint32_t G = std::max(1u, std::min(gmax, (ns + target - 1) / target));
     const uint32_t per = (ns + G - 1) / G;
     const uint32_t e_need = std::max(1u, (per + 255) / 256);
     uint32_t E = 0;
     for (uint32_t e : Es)
         if (e >= e_need) { E = e; break; }
-    if (E == 0) return g;  // shard too large for one-level lists
+    if (E == 0) return g;  // shard too large for one level of chunk lists
     g.E = E;
     g.chunk = E * 256;
     G = std::max(1u, (ns + g.chunk - 1) / g.chunk);
-    const uint32_t need = (G * g.L + 63) / 64;  // list entries per resolver lane, per shard
     g.eplr = 1;
     g.lr = 0;
-    while (g.eplr < need) { g.eplr *= 2; ++g.lr; }
-    if (g.eplr > eplr_max) return g;
     g.epl = 1;
-    while (g.epl < g.W * g.eplr) g.epl *= 2;
+    while (g.epl < g.W) g.epl *= 2;
     g.G = G;
     return g;
 }

@@ -20,7 +20,7 @@ struct HostRow {
 };
 
 // Lookahead geometry: window K pods, list length L (= K), G node chunks of `chunk` nodes per pod,
-// E nodes per lane in the select kernel (256-thread blocks).
+// E nodes per lane in the select kernel (256-thread blocks); G > 1 adds the k_la_merge pass.
 // epl = list entries per resolver lane (power of two); a pod's lists occupy 64*epl entries.
 // waves = resolver geometry: 1 (single-wave) or 4 (pipelined four-wave resolver).
 // k32 = keys fit 32 bits ((max total + 1) < 2^10, n <= 2^22): one 32-bit wave reduction per pod.
@@ -49,11 +49,17 @@ hipError_t launch_scan_pod(const DevTable &t, const DPod *pods, const DPodX *pod
                            bool commit, hipStream_t stream);
 size_t scan_scratch_bytes();
 
-LaGeom la_geometry(uint32_t n, uint32_t K, uint32_t W = 1);
+// L = list length per pod and shard (>= K; 2K for overlapped windows).
+LaGeom la_geometry(uint32_t n, uint32_t K, uint32_t W = 1, uint32_t L = 0);
+// lists: final [W][K][64*eplr] keys the resolver reads; clists: chunk-list scratch of
+// nv*K*G*L keys (select -> merge; unused when G == 1).
 hipError_t launch_la_window(const DevTable &t, const DPod *pods, uint32_t s0, uint32_t P,
-                            const DevCfg &c, const LaGeom &geo, uint64_t *lists, int32_t *out_node,
-                            uint64_t *out_key, uint64_t *stamps, uint64_t *diag,
-                            hipStream_t stream, int part = 3);  // part: 1 select, 2 resolve
+                            const DevCfg &c, const LaGeom &geo, uint64_t *lists, uint64_t *clists,
+                            int32_t *out_node, uint64_t *out_key, uint64_t *stamps, uint64_t *diag,
+                            const uint32_t *dprev, uint32_t *dcur, hipStream_t stream,
+                            int part = 3);  // part: 1 select(+merge), 2 resolve
+// dprev/dcur (overlapped windows, 4-wave resolver only): {count, nodes[64]} dirtied by the
+// previous window (read) and by this window (written); nullptr = windows run back to back.
 
 __global__ void k_set_row(DevTable t, uint32_t i, HostRow v, uint32_t feat);
 

@@ -85,7 +85,9 @@ typedef struct qs_config {
     int32_t virtual_shards;      /* >1: run the sharded LOOKAHEAD protocol with this many node shards
                                     inside one process (no collective; parity testing of the
                                     multi-GPU layout on one device).  Ignored by qs_open_shard. */
-    int32_t reserved[6];
+    int32_t lookahead_serial;    /* 1 = LOOKAHEAD windows back to back; 0 (default) = the select of
+                                    window w+1 overlaps the resolve of window w (needs lookahead <= 32) */
+    int32_t reserved[5];
 } qs_config;
 
 /* Canonical node table, structure of arrays, n entries each.  alloc_ext/req_ext are [n][QS_MAX_EXT],
