@@ -96,6 +96,80 @@ def test_short_lists_would_break_exactness():
     assert not np.array_equal(placement, ref)
 
 
+# ------------------------------------------------- merged lists + overlapped windows ----
+def merged_select(nodes, pods, order, s0, K, L, shards):
+    """k_la_select + k_la_merge: per pod, the top-L keys of each node shard (chunk lists merged)."""
+    lists = []
+    for i in range(K):
+        if s0 + i >= len(order):
+            break
+        keys, _ = O.score_pod(nodes, pods, int(order[s0 + i]))
+        lst = []
+        for lo, hi in shards:
+            lst += topl_keys(keys, lo, hi, L)
+        lists.append(lst)
+    return lists
+
+
+def resolve_window_inherit(nodes, pods, order, s0, lists, placement, inherited):
+    """k_la_resolve4 with dprev: nodes dirtied by the previous window start dirty.  Returns the
+    nodes this window dirtied (its dcur)."""
+    dirty, won = set(inherited), set()
+    for i, lst in enumerate(lists):
+        j = int(order[s0 + i])
+        cand = max([e for e in lst if (0xFFFFFFFF - (e & 0xFFFFFFFF)) not in dirty], default=0)
+        fresh, _ = O.score_pod(nodes, pods, j)
+        best = max([cand] + [int(fresh[d]) for d in dirty])
+        if best == 0:
+            placement[j] = -1
+            continue
+        w = 0xFFFFFFFF - (best & 0xFFFFFFFF)
+        placement[j] = w
+        O.lib().or_reserve(O.ctypes.byref(O._mk_nodes(nodes)), O.ctypes.byref(O._mk_pods(pods)), j, w, 1)
+        dirty.add(w)
+        won.add(w)
+    return won
+
+
+def model_schedule_overlap(nodes, pods, K, L, shards):
+    """The overlapped engine: window w+1's lists are selected against the table as it stood
+    before window w (they run beside window w's resolve), so window w's dirtied nodes are
+    inherited as dirty; lists must hold L >= 2K keys per shard."""
+    order = O.py_order(pods, O.DEFAULT_CONFIG)
+    placement = np.full(len(order), -2, np.int32)
+    starts = list(range(0, len(order), K))
+    pending = merged_select(nodes, pods, order, starts[0], K, L, shards)  # select(0)
+    inherited = set()
+    for w, s0 in enumerate(starts):
+        lists = pending
+        # select(w+1) reads the table before resolve(w) runs (the stalest view it can get)
+        if w + 1 < len(starts):
+            pending = merged_select(nodes, pods, order, starts[w + 1], K, L, shards)
+        inherited = resolve_window_inherit(nodes, pods, order, s0, lists, placement, inherited)
+    return placement
+
+
+@pytest.mark.parametrize("K,W", [(1, 1), (4, 1), (8, 3), (16, 2), (32, 1)])
+def test_overlapped_merged_model_is_exact(K, W):
+    nodes, pods = O.generate(2, 150, 1200)
+    ref_nodes, _ = O.copy_cluster(nodes, pods)
+    ref, _, _ = O.schedule(ref_nodes, pods)
+    got = model_schedule_overlap(nodes, pods, K, 2 * K, chunks_of(150, W))
+    assert np.array_equal(got, ref)
+    for k in ("req_cpu", "req_mem", "nz_cpu", "nz_mem", "pods"):
+        assert np.array_equal(nodes[k], ref_nodes[k])
+
+
+def test_overlap_needs_two_windows_of_list():
+    """With overlapped windows, L = K is too short (up to 2K-1 nodes are dirty): the model
+    diverges from the oracle on a spreading stream, so the engine uses L = 2K."""
+    nodes, pods = O.generate(2, 60, 600)
+    ref_nodes, _ = O.copy_cluster(nodes, pods)
+    ref, _, _ = O.schedule(ref_nodes, pods)
+    got = model_schedule_overlap(nodes, pods, 16, 16, [(0, 60)])
+    assert not np.array_equal(got, ref)
+
+
 # ---------------------------------------------------------------- sharded protocol (gloo) ----
 def _shard_worker(rank, world, port, K, n, p, q):
     import torch
