@@ -52,6 +52,7 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=20000, help="pods in the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-config3", action="store_true", help="skip the N=1 config-3 reference point")
+    ap.add_argument("--no-scan", action="store_true", help="skip the HBM-resident scan roofline leg")
     return ap.parse_args()
 
 
@@ -205,14 +206,54 @@ def measure(cx, a, workload, steps, warmup, with_diag=True):
     return out
 
 
+def scan_roofline(cx, a, n_nodes=1 << 24, n_pods=32):
+    """The scoring scan at an HBM-resident table (north_star's >= 50 % target):
+    the SCAN engine's exact stream over 2^24 nodes (512 MiB of SoA columns, beyond the 256 MiB
+    Infinity Cache), one full Filter+Score scan + argmax per pod, then Reserve.  Achieved =
+    n_nodes x B_node / mean k_scan_soa launch time (HIP events on the library stream)."""
+    nodes, pods = qsched.synth_generate(2, n_nodes, n_pods)
+    cfg = {"engine": "scan"}
+    s = qsched.Scheduler(cfg, device=cx.local)
+    s.load_nodes(nodes)
+    s.save_table()
+    st = s.prepare(pods)
+    st.run()  # warm-up
+    walls = []
+    for _ in range(3):
+        s.restore_table()
+        walls.append(st.run()["wall_s"])
+    st.free()
+    s.close()
+    sp = qsched.Scheduler(dict(cfg, profile_kernels=1), device=cx.local)
+    sp.load_nodes(nodes)
+    stp = sp.prepare(pods)
+    stp.run()
+    kp = stp.run()["kernels"]["scan"]  # second run: table already advanced, same work per scan
+    stp.free()
+    sp.close()
+    avg = kp["s"] / kp["launches"]
+    achieved = n_nodes * B_NODE / avg / 1e9
+    wall = min(walls)
+    return {"workload": f"SCAN engine, {n_nodes:,} nodes (config-2 distribution, SoA columns) x "
+                        f"{n_pods} pods: one full scoring scan + argmax + Reserve per pod",
+            "pods_per_s": round(n_pods / wall, 1), "evals_per_s": round(n_pods * n_nodes / wall, 1),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": None, "kernel": "k_scan_soa",
+                         "avg_launch_us": round(avg * 1e6, 2),
+                         "bytes_per_launch": n_nodes * B_NODE}}
+
+
 def main():
     a = parse()
     cx = Ctx()
     workload = a.workload if a.workload != "auto" else ("config2" if cx.world == 1 else "config3")
     m = measure(cx, a, workload, a.steps, a.warmup)
-    c3 = None
+    c3 = scan = None
     if cx.world == 1 and workload == "config2" and not a.no_config3:
         c3 = measure(cx, a, "config3", 1, 1, with_diag=False)
+    if cx.world == 1 and not a.no_scan:
+        scan = scan_roofline(cx, a)
     if cx.rank == 0:
         rl = roofline(m["kp"], m["n_nodes"], m["n_pods"], m["wall_fallback"])
         if m["sharded"]:
@@ -242,6 +283,8 @@ def main():
                               "evals_per_s": round(c3["value"] * c3["n_nodes"], 1),
                               "ms_per_step": round(c3["ms_per_step"], 3), "steps": 1,
                               "engine": c3["engine"]}
+        if scan is not None:
+            out["scan"] = scan
         if cx.world == 1 and not a.no_cpu:
             out["cpu_baseline"] = cpu_baseline(m["nodes"], m["pods"], m["n_nodes"], m["n_pods"],
                                                a.cpu_sample)

@@ -15,6 +15,8 @@
 namespace qs_host {
 
 constexpr int64_t kLimit = (1LL << 24) - 1;  // 24-bit multiplier range of the kernels (spec S10)
+// Tables at least this large also keep the SoA copy the SCAN engine streams (L2-resident below).
+constexpr uint32_t kSoaMinNodes = 1u << 16;
 
 struct QsError {
     qs_status st;
@@ -100,6 +102,8 @@ struct qs_ctx {
     qs::DevTable dt{};
     qs::DevCfg dc{};
     qs_host::DevBuf tbl;  // all columns in one allocation
+    qs_host::DevBuf soa;  // SoA int32 copy (kSCols x cap) when n >= soa_min_nodes
+    bool soa_valid = false;  // SoA copy matches the rows (engines that update rows only clear it)
     qs_host::DevBuf tbl_saved;  // qs_table_save snapshot (whole allocation)
     bool saved = false;
     bool mirror_stale = false;  // device ran a stream since the last mirror sync

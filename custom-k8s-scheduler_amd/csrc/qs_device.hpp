@@ -30,10 +30,19 @@ struct alignas(16) DMask {
     uint64_t th, ts;         // taint_hard, taint_soft
     uint64_t lb0, lb1;       // label requirement bits
 };
+// Column-major (SoA) copy of the int32 fields for HBM-resident tables (n >= kSoaMinNodes): the
+// SCAN engine and qs_score_pod stream 4 nodes per lane with one 16-byte load per column, so a
+// scan moves exactly the 32 algorithmic bytes per node.  Reciprocals are
+// recomputed in registers.  c[0] == nullptr: no SoA copy.
+enum : int { kSAc, kSAm, kSRc, kSRm, kSZc, kSZm, kSNp, kSMp, kSAe0, kSRe0, kSAe1, kSRe1, kSCols };
+struct DevSoa {
+    int32_t *c[kSCols];
+};
 struct DevTable {
     DRow *rows;
     DMask *masks;
     uint32_t n;
+    DevSoa soa;
 };
 
 enum : uint32_t { kFeatTaint = 1u, kFeatAffinity = 2u, kFeatExt = 4u };

@@ -141,6 +141,11 @@ DRow to_drow(const HostRow &r) {
     return d;
 }
 
+uint32_t soa_min_nodes(const qs_ctx *c) {
+    const int32_t v = c->cfg.scan_soa_min_nodes;
+    return v == 0 ? kSoaMinNodes : (v < 0 ? 0xFFFFFFFFu : (uint32_t)v);
+}
+
 // Upload the whole mirror (compacted) to the device.
 void upload_table(qs_ctx *c) {
     const uint32_t n = c->m.n;
@@ -151,19 +156,39 @@ void upload_table(qs_ctx *c) {
     }
     carve(c->dt, c->cap, c->tbl.as<char>());
     c->dt.n = n;
+    const bool soa = n > 0 && n >= soa_min_nodes(c);
+    std::memset(&c->dt.soa, 0, sizeof c->dt.soa);
     std::vector<DRow> rows(n);
     std::vector<DMask> masks(n);
+    std::vector<int32_t> cols(soa ? (size_t)kSCols * c->cap : 0, 0);  // zero padding: infeasible
     for (uint32_t i = 0; i < n; i++) {
         const HostRow r = compact_row(c->m, i, c->shift);
         rows[i] = to_drow(r);
         masks[i] = DMask{r.th, r.ts, r.lb0, r.lb1};
+        if (soa) {
+            const int32_t f[kSCols] = {r.ac, r.am, r.rc, r.rm, r.zc, r.zm, r.np, r.mp, r.ae0, r.re0, r.ae1, r.re1};
+            for (int k = 0; k < kSCols; k++) cols[(size_t)k * c->cap + i] = f[k];
+        }
     }
     if (n) {
         HIPCHK(hipMemcpyAsync(c->dt.rows, rows.data(), n * sizeof(DRow), hipMemcpyHostToDevice, c->stream));
         HIPCHK(hipMemcpyAsync(c->dt.masks, masks.data(), n * sizeof(DMask), hipMemcpyHostToDevice, c->stream));
     }
+    if (soa) {
+        c->soa.ensure(cols.size() * 4);
+        for (int k = 0; k < kSCols; k++) c->dt.soa.c[k] = c->soa.as<int32_t>() + (size_t)k * c->cap;
+        HIPCHK(hipMemcpyAsync(c->soa.p, cols.data(), cols.size() * 4, hipMemcpyHostToDevice, c->stream));
+    }
     HIPCHK(hipStreamSynchronize(c->stream));
     c->dev_valid = true;
+    c->soa_valid = soa;
+}
+
+// The SCAN engine reads the SoA copy: rebuild it after engines that only update the rows.
+void ensure_soa(qs_ctx *c) {
+    if (!c->dt.soa.c[0] || c->soa_valid) return;
+    HIPCHK(launch_rows_to_soa(c->dt, c->stream));
+    c->soa_valid = true;
 }
 
 void push_row(qs_ctx *c, uint32_t i) {
@@ -586,10 +611,11 @@ qs_status qs_score_pod(qs_ctx *c, const qs_pod *pod, uint8_t *feas, int32_t *sco
         HIPCHK(hipMemcpyAsync(c->one_podx.p, &dx, sizeof dx, hipMemcpyHostToDevice, c->stream));
         HIPCHK(hipMemsetAsync(c->scratch.p, 0, scan_scratch_bytes(), c->stream));
         if (n) {
+            ensure_soa(c);
             HIPCHK(launch_scan_pod(c->dt, c->one_pod.as<DPod>(), c->one_podx.as<DPodX>(), 0, c->dc,
                                    c->scratch.p, nullptr, nullptr, nullptr, c->out_feas.as<uint8_t>(),
-                                   c->out_score.as<int32_t>(), c->out_total.as<int32_t>(), false,
-                                   c->stream));
+                                   c->out_score.as<int32_t>(), c->out_total.as<int32_t>(), 3,
+                                   c->stream));  // scan + reduce (no Reserve: out_node == nullptr)
         }
         unsigned long long kbest = 0;
         HIPCHK(hipMemcpyAsync(&kbest, c->scratch.p, 8, hipMemcpyDeviceToHost, c->stream));
@@ -680,11 +706,14 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                 batches = 1;
             } else if (eng == QS_ENGINE_SCAN) {
                 HIPCHK(hipMemsetAsync(c->scratch.p, 0, scan_scratch_bytes(), c->stream));
+                ensure_soa(c);
                 for (uint32_t k = 0; k < P; k++) {
-                    kt.begin(1, c->stream);
+                    kt.begin(1, c->stream);  // the key scan alone (+ normalize pre-pass)
                     HIPCHK(launch_scan_pod(c->dt, dp, dx, k, c->dc, c->scratch.p, on, ok, st,
-                                           nullptr, nullptr, nullptr, true, c->stream));
+                                           nullptr, nullptr, nullptr, 1, c->stream));
                     kt.end(1, c->stream);
+                    HIPCHK(launch_scan_pod(c->dt, dp, dx, k, c->dc, c->scratch.p, on, ok, st,
+                                           nullptr, nullptr, nullptr, 2, c->stream));
                 }
                 batches = P;
             } else {
@@ -838,6 +867,7 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
         (void)hipEventDestroy(e1);
         s->ran = true;
         c->mirror_stale = true;
+        if (eng != QS_ENGINE_SCAN) c->soa_valid = false;  // those engines update the rows only
         kt.finish();
         if (stats) {
             std::memset(stats, 0, sizeof(*stats));
@@ -898,6 +928,7 @@ qs_status qs_table_restore(qs_ctx *c) {
         HIPCHK(hipSetDevice(c->device));
         HIPCHK(hipMemcpyAsync(c->tbl.p, c->tbl_saved.p, c->tbl.bytes, hipMemcpyDeviceToDevice, c->stream));
         c->mirror_stale = true;  // mirror re-reads the restored rows on demand
+        c->soa_valid = false;    // the SoA copy is rebuilt from the restored rows on demand
     });
 }
 

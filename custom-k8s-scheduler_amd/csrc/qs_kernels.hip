@@ -113,10 +113,29 @@ __global__ __launch_bounds__(BS) void k_persistent(DevTable t, const DPod *__res
 // =============================================================================================
 // SCAN engine (and qs_score_pod)
 // =============================================================================================
+// Per-pod scratch: normalize maxima (taint / affinity) and one partial argmax key per block of the
+// key scan; the commit kernel reduces the partials (no single-address atomics on the hot path:
+// thousands of blocks hitting one u64 serialise at the memory-side atomic unit).
+constexpr uint32_t kScanBlocksMax = 2048;
 struct ScanScratch {
-    unsigned long long best;
-    uint32_t mt, ma;
+    unsigned long long best;  // reduced key of the last commit (qs_score_pod reads it)
+    uint32_t mt, ma;          // normalize maxima (k_scan_norm)
+    uint32_t nblk, pad;       // partials written by the last key scan
+    uint64_t partial[kScanBlocksMax];
 };
+
+// Block-wide max of a u64 key: wave DPP max, then one LDS exchange.
+template <int BS>
+__device__ __forceinline__ uint64_t block_max_u64(uint64_t v) {
+    __shared__ uint64_t red[BS / kWave];
+    v = wave_max_u64(v);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    uint64_t m = 0;
+#pragma unroll
+    for (int i = 0; i < BS / kWave; ++i) m = red[i] > m ? red[i] : m;
+    return m;
+}
 
 template <uint32_t F>
 __global__ __launch_bounds__(256) void k_scan_norm(DevTable t, const DPod *__restrict__ pods,
@@ -134,6 +153,7 @@ __global__ __launch_bounds__(256) void k_scan_norm(DevTable t, const DPod *__res
             la = b > la ? b : la;
         }
     }
+    // (normalizing profiles run this scan on row tables of a few thousand nodes: few blocks)
     lt = wave_max_u32(lt);
     la = wave_max_u32(la);
     if ((threadIdx.x & 63) == 0) {
@@ -142,7 +162,7 @@ __global__ __launch_bounds__(256) void k_scan_norm(DevTable t, const DPod *__res
     }
 }
 
-// Keys for every node; optionally per-node outputs for qs_score_pod.
+// Keys for every node from the row table; optionally per-node outputs for qs_score_pod.
 template <uint32_t F>
 __global__ __launch_bounds__(256) void k_scan_key(DevTable t, const DPod *__restrict__ pods,
                                                   const DPodX *__restrict__ podx, uint32_t s,
@@ -169,15 +189,86 @@ __global__ __launch_bounds__(256) void k_scan_key(DevTable t, const DPod *__rest
             for (int q = 0; q < 4; ++q) score_out[4 * (size_t)i + q] = f ? (int32_t)sco[q] : 0;
         }
     }
-    best = wave_max_u64(best);
-    if ((threadIdx.x & 63) == 0 && best) atomicMax(&sc->best, (unsigned long long)best);
+    best = block_max_u64<256>(best);
+    if (threadIdx.x == 0) sc->partial[blockIdx.x] = best;
 }
 
-// Decode the winner, apply Reserve to the HBM row, emit outputs, reset the scratch.
+// Keys over the SoA copy (HBM-resident tables; F = 0 or kFeatExt): lane q covers nodes
+// 4q..4q+3 with one 16-byte load per column; RN(1/alloc) is recomputed with an IEEE division
+// (the same value the host stores in the row copy, so keys are bit-identical to k_scan_key).
 template <uint32_t F>
-__global__ void k_scan_commit(DevTable t, const DPod *__restrict__ pods, uint32_t s, ScanScratch *sc,
-                              int32_t *out_node, uint64_t *out_key, uint64_t *stamps) {
-    const uint64_t ks = sc->best;
+__global__ __launch_bounds__(256) void k_scan_soa(DevTable t, const DPod *__restrict__ pods,
+                                                  uint32_t s, DevCfg c, ScanScratch *sc,
+                                                  uint8_t *feas_out, int32_t *score_out,
+                                                  int32_t *total_out) {
+    const DPod p = pods[s];
+    const DPodX px{};
+    const uint32_t nq = (t.n + 3) / 4;  // columns are zero-padded to a multiple of 64 nodes
+    uint64_t best = 0;
+    for (uint32_t q = blockIdx.x * 256 + threadIdx.x; q < nq; q += gridDim.x * 256) {
+        int4 col[kSCols];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) col[k] = reinterpret_cast<const int4 *>(t.soa.c[k])[q];
+        if (F & kFeatExt) {
+#pragma unroll
+            for (int k = 8; k < kSCols; ++k) col[k] = reinterpret_cast<const int4 *>(t.soa.c[k])[q];
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            auto el = [&](int k) { return e == 0 ? col[k].x : e == 1 ? col[k].y : e == 2 ? col[k].z : col[k].w; };
+            Row r;
+            r.ac = el(kSAc); r.am = el(kSAm); r.rc = el(kSRc); r.rm = el(kSRm);
+            r.zc = el(kSZc); r.zm = el(kSZm); r.np = el(kSNp); r.mp = el(kSMp);
+            r.yc = r.ac ? 1.0 / (double)r.ac : 0.0;
+            r.ym = r.am ? 1.0 / (double)r.am : 0.0;
+            RowX x{};
+            if (F & kFeatExt) { x.ae0 = el(kSAe0); x.re0 = el(kSRe0); x.ae1 = el(kSAe1); x.re1 = el(kSRe1); }
+            const uint32_t idx = 4 * q + e;
+            const bool f = feasible<F>(r, x, p, px);  // padding rows: max_pods 0 -> infeasible
+            uint32_t sco[4];
+            const uint32_t tot = node_total<F>(r, x, p, px, c, 0, 0.0, 0, 0.0, score_out ? sco : nullptr);
+            const uint64_t key = f ? pack_key(tot + 1, idx) : 0ull;
+            best = key > best ? key : best;
+            if (idx < t.n) {
+                if (feas_out) feas_out[idx] = f;
+                if (total_out) total_out[idx] = f ? (int32_t)tot : -1;
+                if (score_out) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) score_out[4 * (size_t)idx + k] = f ? (int32_t)sco[k] : 0;
+                }
+            }
+        }
+    }
+    best = block_max_u64<256>(best);
+    if (threadIdx.x == 0) sc->partial[blockIdx.x] = best;
+}
+
+// Rebuild the SoA copy from the row table (after engines that update rows only).
+__global__ __launch_bounds__(256) void k_rows_to_soa(DevTable t) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= t.n) return;
+    const DRow r = t.rows[i];
+    t.soa.c[kSAc][i] = r.ac; t.soa.c[kSAm][i] = r.am; t.soa.c[kSRc][i] = r.rc; t.soa.c[kSRm][i] = r.rm;
+    t.soa.c[kSZc][i] = r.zc; t.soa.c[kSZm][i] = r.zm; t.soa.c[kSNp][i] = r.np; t.soa.c[kSMp][i] = r.mp;
+    t.soa.c[kSAe0][i] = r.ae0; t.soa.c[kSRe0][i] = r.re0; t.soa.c[kSAe1][i] = r.ae1; t.soa.c[kSRe1][i] = r.re1;
+}
+
+// One 256-thread block: reduce the key scan's partials to the pod's winner, then (stream mode,
+// out_node != nullptr) apply Reserve to the row (and SoA) copy and emit the outputs.  Resets the
+// normalize maxima for the next pod.
+template <uint32_t F>
+__global__ __launch_bounds__(256) void k_scan_commit(DevTable t, const DPod *__restrict__ pods,
+                                                     uint32_t s, uint32_t nblk, ScanScratch *sc,
+                                                     int32_t *out_node, uint64_t *out_key,
+                                                     uint64_t *stamps) {
+    uint64_t v = 0;
+    for (uint32_t i = threadIdx.x; i < nblk; i += 256) v = sc->partial[i] > v ? sc->partial[i] : v;
+    const uint64_t ks = block_max_u64<256>(v);
+    if (threadIdx.x != 0) return;
+    sc->best = ks;
+    sc->mt = 0;
+    sc->ma = 0;
+    if (!out_node) return;
     const DPod p = pods[s];
     if (ks) {
         const uint32_t w = key_node(ks);
@@ -186,13 +277,16 @@ __global__ void k_scan_commit(DevTable t, const DPod *__restrict__ pods, uint32_
         reserve(r, x, p, +1);
         store_dyn(t, w, r);
         store_dynx<F>(t, w, x);
+        if (t.soa.c[0]) {
+            t.soa.c[kSRc][w] = r.rc; t.soa.c[kSRm][w] = r.rm;
+            t.soa.c[kSZc][w] = r.zc; t.soa.c[kSZm][w] = r.zm;
+            t.soa.c[kSNp][w] = r.np;
+            if (F & kFeatExt) { t.soa.c[kSRe0][w] = x.re0; t.soa.c[kSRe1][w] = x.re1; }
+        }
     }
     out_node[s] = ks ? (int32_t)key_node(ks) : -1;
     if (out_key) out_key[s] = ks;
     if (stamps) stamps[s] = __builtin_amdgcn_s_memrealtime();
-    sc->best = 0;
-    sc->mt = 0;
-    sc->ma = 0;
 }
 
 // =============================================================================================
@@ -839,6 +933,11 @@ __global__ void k_set_row(DevTable t, uint32_t i, HostRow v, uint32_t feat) {
     r.ae0 = v.ae0; r.re0 = v.re0; r.ae1 = v.ae1; r.re1 = v.re1;
     t.rows[i] = r;
     t.masks[i] = DMask{v.th, v.ts, v.lb0, v.lb1};
+    if (t.soa.c[0]) {
+        const int32_t f[kSCols] = {v.ac, v.am, v.rc, v.rm, v.zc, v.zm, v.np, v.mp, v.ae0, v.re0, v.ae1, v.re1};
+#pragma unroll
+        for (int k = 0; k < kSCols; ++k) t.soa.c[k][i] = f[k];
+    }
 }
 
 // =============================================================================================
@@ -914,27 +1013,44 @@ template <uint32_t F>
 static hipError_t scan_pod_f(const DevTable &t, const DPod *pods, const DPodX *podx, uint32_t s,
                              const DevCfg &c, void *scratch, int32_t *on, uint64_t *ok,
                              uint64_t *st, uint8_t *feas, int32_t *score, int32_t *total,
-                             bool commit, hipStream_t stream) {
+                             int part, hipStream_t stream) {
     ScanScratch *sc = (ScanScratch *)scratch;
-    const uint32_t blocks = min(2048u, max(1u, (t.n + 255) / 256));
-    if (F & kFeatNorm)
-        hipLaunchKernelGGL((k_scan_norm<F>), dim3(blocks), dim3(256), 0, stream, t, pods, podx, s, sc);
-    hipLaunchKernelGGL((k_scan_key<F>), dim3(blocks), dim3(256), 0, stream, t, pods, podx, s, c, sc,
-                       feas, score, total);
-    if (commit)
-        hipLaunchKernelGGL((k_scan_commit<F>), dim3(1), dim3(1), 0, stream, t, pods, s, sc, on, ok, st);
+    const bool soa = !(F & kFeatNorm) && t.soa.c[0];
+    // one partial key per block; a grid of <= 2048 blocks (8 four-wave blocks per CU) strides
+    const uint32_t units = soa ? (t.n + 3) / 4 : t.n;
+    const uint32_t blocks = min(kScanBlocksMax, max(1u, (units + 255) / 256));
+    if (part & 1) {
+        if (soa) {
+            hipLaunchKernelGGL((k_scan_soa<F>), dim3(blocks), dim3(256), 0, stream, t, pods, s, c, sc,
+                               feas, score, total);
+        } else {
+            if (F & kFeatNorm)
+                hipLaunchKernelGGL((k_scan_norm<F>), dim3(blocks), dim3(256), 0, stream, t, pods, podx, s, sc);
+            hipLaunchKernelGGL((k_scan_key<F>), dim3(blocks), dim3(256), 0, stream, t, pods, podx, s, c, sc,
+                               feas, score, total);
+        }
+    }
+    if (part & 2)
+        hipLaunchKernelGGL((k_scan_commit<F>), dim3(1), dim3(256), 0, stream, t, pods, s, blocks, sc,
+                           on, ok, st);
+    return hipGetLastError();
+}
+
+hipError_t launch_rows_to_soa(const DevTable &t, hipStream_t stream) {
+    if (!t.soa.c[0] || t.n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_rows_to_soa, dim3((t.n + 255) / 256), dim3(256), 0, stream, t);
     return hipGetLastError();
 }
 
 hipError_t launch_scan_pod(const DevTable &t, const DPod *pods, const DPodX *podx, uint32_t s,
                            const DevCfg &c, void *scratch, int32_t *on, uint64_t *ok, uint64_t *st,
-                           uint8_t *feas, int32_t *score, int32_t *total, bool commit,
+                           uint8_t *feas, int32_t *score, int32_t *total, int part,
                            hipStream_t stream) {
     switch (feat_class(c.feat)) {
-        case 0: return scan_pod_f<0>(t, pods, podx, s, c, scratch, on, ok, st, feas, score, total, commit, stream);
-        case kFeatExt: return scan_pod_f<kFeatExt>(t, pods, podx, s, c, scratch, on, ok, st, feas, score, total, commit, stream);
+        case 0: return scan_pod_f<0>(t, pods, podx, s, c, scratch, on, ok, st, feas, score, total, part, stream);
+        case kFeatExt: return scan_pod_f<kFeatExt>(t, pods, podx, s, c, scratch, on, ok, st, feas, score, total, part, stream);
         default:
-            return scan_pod_f<kFeatExt | kFeatTaint | kFeatAffinity>(t, pods, podx, s, c, scratch, on, ok, st, feas, score, total, commit, stream);
+            return scan_pod_f<kFeatExt | kFeatTaint | kFeatAffinity>(t, pods, podx, s, c, scratch, on, ok, st, feas, score, total, part, stream);
     }
 }
 

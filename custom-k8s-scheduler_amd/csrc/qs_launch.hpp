@@ -46,7 +46,8 @@ uint32_t persistent_max_nodes(uint32_t feat);
 hipError_t launch_scan_pod(const DevTable &t, const DPod *pods, const DPodX *podx, uint32_t s,
                            const DevCfg &c, void *scratch, int32_t *out_node, uint64_t *out_key,
                            uint64_t *stamps, uint8_t *feas, int32_t *score, int32_t *total,
-                           bool commit, hipStream_t stream);
+                           int part, hipStream_t stream);  // part: 1 keys (+norm), 2 commit
+hipError_t launch_rows_to_soa(const DevTable &t, hipStream_t stream);
 size_t scan_scratch_bytes();
 
 // L = list length per pod and shard (>= K; 2K for overlapped windows).

@@ -47,7 +47,8 @@ class QsConfig(ctypes.Structure):
                 ("balanced_skip_besteffort", ctypes.c_int32), ("qos_sort", ctypes.c_int32),
                 ("lookahead", ctypes.c_int32), ("record_timestamps", ctypes.c_int32),
                 ("profile_kernels", ctypes.c_int32), ("virtual_shards", ctypes.c_int32),
-                ("lookahead_serial", ctypes.c_int32), ("reserved", ctypes.c_int32 * 5)]
+                ("lookahead_serial", ctypes.c_int32),
+                ("scan_soa_min_nodes", ctypes.c_int32), ("reserved", ctypes.c_int32 * 4)]
 
 
 _NODE_COLS = ["alloc_cpu", "alloc_mem", "alloc_ext", "max_pods", "req_cpu", "req_mem", "req_ext",

@@ -87,7 +87,9 @@ typedef struct qs_config {
                                     multi-GPU layout on one device).  Ignored by qs_open_shard. */
     int32_t lookahead_serial;    /* 1 = LOOKAHEAD windows back to back; 0 (default) = the select of
                                     window w+1 overlaps the resolve of window w (needs lookahead <= 32) */
-    int32_t reserved[5];
+    int32_t scan_soa_min_nodes;  /* tables with at least this many nodes also keep the column-major
+                                    copy the SCAN engine / qs_score_pod stream (0 = 65,536; -1 never) */
+    int32_t reserved[4];
 } qs_config;
 
 /* Canonical node table, structure of arrays, n entries each.  alloc_ext/req_ext are [n][QS_MAX_EXT],
