@@ -239,7 +239,7 @@ def scan_roofline(cx, a, n_nodes=1 << 24, n_pods=32):
             "pods_per_s": round(n_pods / wall, 1), "evals_per_s": round(n_pods * n_nodes / wall, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": None, "kernel": "k_scan_soa",
+                         "traffic": pmc_traffic("k_scan_soa"), "kernel": "k_scan_soa",
                          "avg_launch_us": round(avg * 1e6, 2),
                          "bytes_per_launch": n_nodes * B_NODE}}
 

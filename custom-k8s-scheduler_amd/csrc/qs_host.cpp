@@ -744,6 +744,11 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                 uint32_t *dio = c->dio.as<uint32_t>();
                 const uint32_t nwin = (P + geo.K - 1) / geo.K;
                 const auto th0 = std::chrono::steady_clock::now();
+                // QS_SYNC_EVERY=n (profiling aid): bound the launches in flight under counter
+                // collection by a host sync every n windows (individual launches only)
+                static const char *se = getenv("QS_SYNC_EVERY");
+                const uint32_t sync_every = se ? (uint32_t)std::max(0, atoi(se)) : 0u;
+                bool capturing = false;
                 auto enqueue = [&]() {
                 HIPCHK(hipMemsetAsync(c->lists.p, 0, 8 * lwords * nbuf, c->stream));  // padding stays 0
                 HIPCHK(hipMemsetAsync(c->dio.p, 0, 2 * kDioWords * 4, c->stream));
@@ -770,6 +775,8 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                     for (uint32_t w = 0; w < nwin; ++w) {
                         select(w, c->stream);
                         resolve(w);
+                        if (sync_every && !capturing && (w + 1) % sync_every == 0)
+                            HIPCHK(hipStreamSynchronize(c->stream));
                     }
                 } else {
                     // select(w+1) on the second stream runs beside resolve(w): it reads the table
@@ -795,6 +802,10 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                         HIPCHK(hipStreamWaitEvent(c->stream, esel[w % R], 0));
                         resolve(w);
                         HIPCHK(hipEventRecord(eres[w % R], c->stream));
+                        if (sync_every && !capturing && (w + 1) % sync_every == 0) {
+                            HIPCHK(hipStreamSynchronize(c->stream2));
+                            HIPCHK(hipStreamSynchronize(c->stream));
+                        }
                     }
                     for (int r = 0; r < R; ++r) {
                         (void)hipEventDestroy(esel[r]);
@@ -823,6 +834,7 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                         if (s->gexec) (void)hipGraphExecDestroy(s->gexec);
                         s->gexec = nullptr;
                         HIPCHK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+                        capturing = true;
                         try {
                             enqueue();
                         } catch (...) {
