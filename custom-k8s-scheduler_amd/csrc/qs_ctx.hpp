@@ -108,7 +108,7 @@ struct qs_ctx {
     bool saved = false;
     bool mirror_stale = false;  // device ran a stream since the last mirror sync
     qs_host::DevBuf diag;
-    qs_host::DevBuf scratch, lists, clists, dio, one_pod, one_podx, out_feas, out_score, out_total;
+    qs_host::DevBuf scratch, lists, clists, dio, npart, normi, nfall, one_pod, one_podx, out_feas, out_score, out_total;
     uint32_t cap = 0;
     // sharding (qs_open_shard): RCCL communicator of this rank, nullptr when unsharded
     int rank = 0, world = 1;
@@ -129,6 +129,8 @@ inline ShardPlan shard_plan(const qs_ctx *c) {
 // The per-window exchange of the sharded engine (qs_dist.cpp): all-gather of each rank's
 // [K][GLp] list block into [world][K][GLp] (in place), on the context's stream.
 void exchange_lists(qs_ctx *c, uint64_t *lists, size_t per_rank_entries, hipStream_t stream);
+// The same in-place all-gather for 32-bit words (normalizing profiles' partial maxima).
+void exchange_u32(qs_ctx *c, uint32_t *buf, size_t per_rank_words, hipStream_t stream);
 // {count, nodes[64]} dirty-set hand-off between overlapped lookahead windows (+ pad)
 constexpr size_t kDioWords = 68;
 }  // namespace qs_host

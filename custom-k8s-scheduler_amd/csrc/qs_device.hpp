@@ -71,6 +71,22 @@ struct alignas(16) DPodX {
     int32_t pw[4];
 };
 
+// Load a wave-uniform record through the vector path (VGPRs).  The pod extension record is 44
+// dwords; read with scalar loads it pushed the normalizing kernels into SGPR spills.  The zero
+// offset comes from an opaque VGPR so the compiler cannot prove uniformity.
+template <class T>
+__device__ __forceinline__ T load_vgpr(const T *p) {
+    static_assert(sizeof(T) % 16 == 0, "16-byte granules");
+    int z;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+    const int4 *q = reinterpret_cast<const int4 *>(p) + z;
+    T out;
+    int4 *o = reinterpret_cast<int4 *>(&out);
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 16); ++i) o[i] = q[i];
+    return out;
+}
+
 // One node row in registers.
 struct Row {
     int32_t ac, am, rc, rm, zc, zm, np, mp;
@@ -262,6 +278,13 @@ __device__ __forceinline__ uint32_t node_total(const Row &r, const RowX &x, cons
     if (sc) { sc[0] = la; sc[1] = ba; sc[2] = tt; sc[3] = na; }
     return total;
 }
+
+// Normalization facts of one pod at selection time (LOOKAHEAD with TaintToleration /
+// NodeAffinity): the maxima of the raw scores over the nodes feasible then, and how many nodes
+// attain each maximum (the resolver's proof that a maximum still holds).
+struct alignas(16) NormInfo {
+    uint32_t mt, ct, ma, ca;
+};
 
 // spec S7 packed key: ((total + 1) << 32) | (0xFFFFFFFF - idx); 0 = infeasible
 __device__ __forceinline__ uint64_t pack_key(uint32_t tv, uint32_t idx) {

@@ -33,6 +33,11 @@ void exchange_lists(qs_ctx *c, uint64_t *lists, size_t per_rank_entries, hipStre
                           ncclUint64, c->comm, stream));
 }
 
+void exchange_u32(qs_ctx *c, uint32_t *buf, size_t per_rank_words, hipStream_t stream) {
+    NCCLCHK(ncclAllGather(buf + (size_t)c->rank * per_rank_words, buf, per_rank_words, ncclUint32,
+                          c->comm, stream));
+}
+
 }  // namespace qs_host
 
 extern "C" {

@@ -370,8 +370,7 @@ int pick_engine(const qs_ctx *c, uint32_t n) {
     int e = c->cfg.engine;
     const uint32_t feat = c->dc.feat;
     if (e == QS_ENGINE_AUTO) {
-        if (!(feat & (kFeatTaint | kFeatAffinity)) && n > 0 &&
-            la_geometry(n, la_window(c), shard_plan(c).W, 2 * la_window(c)).G > 0)
+        if (n > 0 && la_geometry(n, la_window(c), shard_plan(c).W, 2 * la_window(c)).G > 0)
             e = QS_ENGINE_LOOKAHEAD;
         else if (n <= persistent_max_nodes(feat)) e = QS_ENGINE_PERSISTENT;
         else e = QS_ENGINE_SCAN;
@@ -379,8 +378,6 @@ int pick_engine(const qs_ctx *c, uint32_t n) {
     if (e == QS_ENGINE_PERSISTENT && n > persistent_max_nodes(feat))
         fail(QS_EINVAL, "PERSISTENT engine supports at most " +
                             std::to_string(persistent_max_nodes(feat)) + " nodes for this profile");
-    if (e == QS_ENGINE_LOOKAHEAD && (feat & (kFeatTaint | kFeatAffinity)))
-        fail(QS_EINVAL, "LOOKAHEAD engine does not support TaintToleration/NodeAffinity yet");
     return e;
 }
 
@@ -720,7 +717,9 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                 const bool overlap = la_overlap(c);
                 LaGeom geo = lookahead_geometry(c, n, overlap);
                 static const char *rw = getenv("QS_RESOLVER_WAVES");  // 1 = single-wave resolver
-                geo.waves = (rw && rw[0] == '1' && !overlap) ? 1u : 4u;
+                const bool norm = (c->dc.feat & (kFeatTaint | kFeatAffinity)) != 0;
+                // normalizing profiles: k_la_norm pre-pass + the single-wave k_la_resolve_norm
+                geo.waves = norm || (rw && rw[0] == '1' && !overlap) ? 1u : 4u;
                 int64_t wmax = 0;
                 for (int q = 0; q < 3; q++) wmax = std::max<int64_t>(wmax, (int64_t)c->cfg.w_fit[q] + c->cfg.w_bal[q]);
                 geo.k32 = (100 * wmax + 1 < 1024 && n <= (1u << 22)) ? 1u : 0u;
@@ -732,6 +731,10 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                 c->lists.ensure(8 * lwords * nbuf);
                 c->clists.ensure(8 * cwords * nbuf);
                 c->dio.ensure(2 * kDioWords * 4);
+                const size_t nparts = norm ? (size_t)geo.W * geo.K * geo.G : 1;  // uint4 per window
+                c->npart.ensure(16 * nparts * nbuf);
+                c->normi.ensure(16 * (size_t)geo.K * nbuf);
+                c->nfall.ensure(8);
                 // QS_DIAG=1: diagnostic resolver with per-segment shader-clock stamps (stderr)
                 static const bool diag_on = getenv("QS_DIAG") && getenv("QS_DIAG")[0] == '1';
                 uint64_t *diag = nullptr;
@@ -752,23 +755,35 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                 auto enqueue = [&]() {
                 HIPCHK(hipMemsetAsync(c->lists.p, 0, 8 * lwords * nbuf, c->stream));  // padding stays 0
                 HIPCHK(hipMemsetAsync(c->dio.p, 0, 2 * kDioWords * 4, c->stream));
-                // select (+ merge, + the RCCL exchange when sharded) of window w on stream `ss`
-                auto select = [&](uint32_t w, hipStream_t ss) {
+                HIPCHK(hipMemsetAsync(c->nfall.p, 0, 8, c->stream));
+                auto bufs = [&](uint32_t w) {
                     const int b = overlap ? (int)(w & 1) : 0;
+                    LaBufs bf{L0 + b * lwords, C0 + b * cwords, c->npart.as<uint4>() + b * nparts,
+                              c->normi.as<NormInfo>() + (size_t)b * geo.K, nullptr, nullptr,
+                              c->nfall.as<unsigned long long>()};
+                    if (overlap) {
+                        bf.dprev = dio + ((w + 1) & 1) * kDioWords;
+                        bf.dcur = dio + (w & 1) * kDioWords;
+                    }
+                    return bf;
+                };
+                // select (+ norm pre-pass, + merge, + the RCCL exchanges when sharded) of window w
+                // on stream `ss`
+                auto select = [&](uint32_t w, hipStream_t ss) {
+                    const LaBufs bf = bufs(w);
                     kt.begin(2, ss);
-                    HIPCHK(launch_la_window(c->dt, dp, w * geo.K, P, c->dc, geo, L0 + b * lwords,
-                                            C0 + b * cwords, on, ok, st, diag, nullptr, nullptr, ss, 1));
+                    if (norm) {
+                        HIPCHK(launch_la_window(c->dt, dp, dx, w * geo.K, P, c->dc, geo, bf, on, ok, st, diag, ss, 4));
+                        if (c->comm) exchange_u32(c, (uint32_t *)bf.npart, 4 * (size_t)geo.K * geo.G, ss);
+                    }
+                    HIPCHK(launch_la_window(c->dt, dp, dx, w * geo.K, P, c->dc, geo, bf, on, ok, st, diag, ss, 1));
                     kt.end(2, ss);
-                    if (c->comm) exchange_lists(c, L0 + b * lwords, rank_entries, ss);
+                    if (c->comm) exchange_lists(c, bf.lists, rank_entries, ss);
                 };
                 auto resolve = [&](uint32_t w) {
-                    const int b = overlap ? (int)(w & 1) : 0;
                     kt.begin(3, c->stream);
-                    HIPCHK(launch_la_window(c->dt, dp, w * geo.K, P, c->dc, geo, L0 + b * lwords,
-                                            C0 + b * cwords, on, ok, st, diag,
-                                            overlap ? dio + ((w + 1) & 1) * kDioWords : nullptr,
-                                            overlap ? dio + (w & 1) * kDioWords : nullptr,
-                                            c->stream, 2));
+                    HIPCHK(launch_la_window(c->dt, dp, dx, w * geo.K, P, c->dc, geo, bufs(w), on, ok, st,
+                                            diag, c->stream, 2));
                     kt.end(3, c->stream);
                 };
                 if (!overlap) {
@@ -824,7 +839,8 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                     auto put = [&](const void *p, size_t nb) {
                         key.insert(key.end(), (const uint8_t *)p, (const uint8_t *)p + nb);
                     };
-                    const void *ptrs[] = {c->dt.rows, c->dt.masks, L0, C0, dio, st, (void *)c->comm, dp};
+                    const void *ptrs[] = {c->dt.rows, c->dt.masks, L0, C0, dio, st, (void *)c->comm, dp, dx,
+                                          c->npart.p, c->normi.p, c->nfall.p};
                     put(ptrs, sizeof ptrs);
                     put(&c->dt.n, sizeof c->dt.n);
                     put(&c->dc, sizeof c->dc);
@@ -877,6 +893,9 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
         HIPCHK(hipEventElapsedTime(&ms, e0, e1));
         (void)hipEventDestroy(e0);
         (void)hipEventDestroy(e1);
+        uint64_t rescans = 0;
+        if (eng == QS_ENGINE_LOOKAHEAD && c->nfall.p)
+            HIPCHK(hipMemcpy(&rescans, c->nfall.p, 8, hipMemcpyDeviceToHost));
         s->ran = true;
         c->mirror_stale = true;
         if (eng != QS_ENGINE_SCAN) c->soa_valid = false;  // those engines update the rows only
@@ -891,6 +910,7 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
             stats->evals = (uint64_t)P * n;
             stats->wall_s = ms * 1e-3;
             stats->batches = batches;
+            stats->truncations = rescans;
             stats->engine_used = eng;
         }
     });

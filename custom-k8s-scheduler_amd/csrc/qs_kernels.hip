@@ -392,46 +392,141 @@ __device__ __forceinline__ void block_topl(const uint32_t (&tv)[E], uint32_t L,
     for (uint32_t i = written + tid; i < L; i += BS) out[i] = 0;
 }
 
-// Grid: shards × pods × G node-chunks.  Block (v, k, g) scores pod s0+k on chunk g of shard v
-// (Filter + Score in registers, against the window-start table) and writes the chunk's top-L
-// keys to out: straight into the final lists when G == 1, else into the chunk-list scratch
-// [nv][kw][G][L] that k_la_merge reduces to one top-L per pod and shard.
-template <int BS, int E, uint32_t F>
-__global__ __launch_bounds__(BS) void k_la_select(DevTable t, const DPod *__restrict__ pods,
-                                                  DevCfg c, uint32_t s0, uint32_t P, LaShard sh,
-                                                  uint32_t G, uint32_t L, uint32_t chunk,
-                                                  uint32_t GLp, uint64_t *__restrict__ lists,
-                                                  uint64_t *__restrict__ clists) {
-    // block -> (shard v, pod k, chunk g); shard v owns nodes [v*n/W, (v+1)*n/W)
+// Block (v, k, g) of the select grid: shard v owns nodes [v*n/W, (v+1)*n/W).
+struct SelBlock {
+    uint32_t vs, v, k, g, start, end;
+};
+__device__ __forceinline__ SelBlock sel_block(const DevTable &t, const LaShard &sh, uint32_t G,
+                                              uint32_t chunk) {
+    SelBlock b;
     const uint32_t per = sh.kw * G;
-    const uint32_t vs = blockIdx.x / per, rem = blockIdx.x % per;
-    const uint32_t v = sh.v0 + vs;
-    const uint32_t k = rem / G, g = rem % G;
-    const uint32_t s = s0 + k;
+    b.vs = blockIdx.x / per;
+    const uint32_t rem = blockIdx.x % per;
+    b.v = sh.v0 + b.vs;
+    b.k = rem / G;
+    b.g = rem % G;
+    const uint32_t lo = (uint32_t)((uint64_t)b.v * t.n / sh.W);
+    const uint32_t hi = (uint32_t)((uint64_t)(b.v + 1) * t.n / sh.W);
+    b.start = lo + b.g * chunk;
+    b.end = min(hi, b.start + chunk);
+    return b;
+}
+
+// Normalizing profiles, pass 1 (same grid as k_la_select): per (shard, pod, chunk) the maxima of
+// the raw TaintToleration / NodeAffinity scores over the chunk's feasible nodes and their counts,
+// into npart[(v*K + k)*G + g] (the [W][K][G] layout the RCCL all-gather completes).
+template <int BS, int E, uint32_t F>
+__global__ __launch_bounds__(BS) void k_la_norm(DevTable t, const DPod *__restrict__ pods,
+                                                const DPodX *__restrict__ podx, uint32_t s0,
+                                                uint32_t P, LaShard sh, uint32_t G, uint32_t K,
+                                                uint32_t chunk, uint4 *__restrict__ npart) {
+    constexpr int NW = BS / kWave;
+    __shared__ uint32_t red[4][NW];
+    const SelBlock b = sel_block(t, sh, G, chunk);
+    const uint32_t s = s0 + b.k;
     if (s >= P) return;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const DPod p = pods[s];
-    const DPodX px{};
-    const uint32_t lo = (uint32_t)((uint64_t)v * t.n / sh.W);
-    const uint32_t hi = (uint32_t)((uint64_t)(v + 1) * t.n / sh.W);
-    const uint32_t start = lo + g * chunk;
-    const uint32_t end = min(hi, start + chunk);
-    const uint32_t base = start + (uint32_t)w * E * kWave + lane;
+    const DPodX px = load_vgpr(podx + s);
+    const uint32_t base = b.start + (uint32_t)w * E * kWave + lane;
+    uint32_t rt[E], ra[E], mt = 0, ma = 0;
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+        const uint32_t idx = base + j * kWave;
+        rt[j] = ra[j] = 0xFFFFFFFFu;  // not feasible / not in the chunk
+        if (idx < b.end) {
+            const Row r = load_row(t, idx);
+            const RowX x = load_rowx<F>(t, idx);
+            if (feasible<F>(r, x, p, px)) {
+                rt[j] = taint_raw(x, px);
+                ra[j] = affinity_raw(x, p, px);
+                mt = rt[j] > mt ? rt[j] : mt;
+                ma = ra[j] > ma ? ra[j] : ma;
+            }
+        }
+    }
+    mt = wave_max_u32(mt);
+    ma = wave_max_u32(ma);
+    if (lane == 0) { red[0][w] = mt; red[1][w] = ma; }
+    __syncthreads();
+    mt = ma = 0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) { mt = red[0][i] > mt ? red[0][i] : mt; ma = red[1][i] > ma ? red[1][i] : ma; }
+    uint32_t ct = 0, ca = 0;
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+        ct += (uint32_t)__popcll(__ballot(rt[j] == mt));
+        ca += (uint32_t)__popcll(__ballot(ra[j] == ma));
+    }
+    if (lane == 0) { red[2][w] = ct; red[3][w] = ca; }
+    __syncthreads();
+    if (tid == 0) {
+        uint4 o = make_uint4(mt, 0, ma, 0);
+#pragma unroll
+        for (int i = 0; i < NW; ++i) { o.y += red[2][i]; o.w += red[3][i]; }
+        npart[((size_t)b.v * K + b.k) * G + b.g] = o;
+    }
+}
+
+// Combine a pod's [W][G] partials into its NormInfo (max, and the count of nodes attaining it).
+__device__ __forceinline__ NormInfo norm_reduce(const uint4 *__restrict__ npart, uint32_t W,
+                                                uint32_t K, uint32_t G, uint32_t k) {
+    NormInfo r{0, 0, 0, 0};
+    for (uint32_t v = 0; v < W; ++v)
+        for (uint32_t g = 0; g < G; ++g) {
+            const uint4 q = npart[((size_t)v * K + k) * G + g];
+            if (q.x > r.mt) { r.mt = q.x; r.ct = 0; }
+            if (q.x == r.mt) r.ct += q.y;
+            if (q.z > r.ma) { r.ma = q.z; r.ca = 0; }
+            if (q.z == r.ma) r.ca += q.w;
+        }
+    return r;
+}
+
+// Grid: shards × pods × G node-chunks.  Block (v, k, g) scores pod s0+k on chunk g of shard v
+// (Filter + Score in registers, against the window-start table) and writes the chunk's top-L
+// keys to out: straight into the final lists when G == 1, else into the chunk-list scratch
+// [nv][kw][G][L] that k_la_merge reduces to one top-L per pod and shard.  Normalizing profiles
+// first combine the k_la_norm partials (uniform per pod: scalar loads) and block (0, k, 0) of
+// this process publishes the pod's NormInfo for the resolver.
+template <int BS, int E, uint32_t F>
+__global__ __launch_bounds__(BS) void k_la_select(DevTable t, const DPod *__restrict__ pods,
+                                                  const DPodX *__restrict__ podx, DevCfg c,
+                                                  uint32_t s0, uint32_t P, LaShard sh,
+                                                  uint32_t G, uint32_t L, uint32_t chunk,
+                                                  uint32_t GLp, uint64_t *__restrict__ lists,
+                                                  uint64_t *__restrict__ clists,
+                                                  const uint4 *__restrict__ npart, uint32_t K,
+                                                  NormInfo *__restrict__ norm_out) {
+    const SelBlock b = sel_block(t, sh, G, chunk);
+    const uint32_t s = s0 + b.k;
+    if (s >= P) return;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const DPod p = pods[s];
+    DPodX px{};
+    NormInfo nf{0, 0, 0, 0};
+    if (F & kFeatNorm) {
+        px = load_vgpr(podx + s);
+        nf = norm_reduce(npart, sh.W, K, G, b.k);
+        if (tid == 0 && b.vs == 0 && b.g == 0) norm_out[b.k] = nf;
+    }
+    const double ymt = rcp_exact(nf.mt), yma = rcp_exact(nf.ma);
+    const uint32_t base = b.start + (uint32_t)w * E * kWave + lane;
     uint32_t tv[E];
 #pragma unroll
     for (int j = 0; j < E; ++j) {
         const uint32_t idx = base + j * kWave;
         tv[j] = 0;
-        if (idx < end) {
+        if (idx < b.end) {
             const Row r = load_row(t, idx);
             const RowX x = load_rowx<F>(t, idx);
             const bool f = feasible<F>(r, x, p, px);
-            const uint32_t tot = node_total<F>(r, x, p, px, c, 0, 0.0, 0, 0.0, nullptr);
+            const uint32_t tot = node_total<F>(r, x, p, px, c, nf.mt, ymt, nf.ma, yma, nullptr);
             tv[j] = f ? tot + 1 : 0;
         }
     }
-    uint64_t *out = G == 1 ? lists + (size_t)v * sh.RS + (size_t)k * GLp
-                           : clists + (((size_t)vs * sh.kw + k) * G + g) * L;
+    uint64_t *out = G == 1 ? lists + (size_t)b.v * sh.RS + (size_t)b.k * GLp
+                           : clists + (((size_t)b.vs * sh.kw + b.k) * G + b.g) * L;
     block_topl<BS, E>(tv, L, out, [&](int j) { return pack_key(tv[j], base + j * kWave); });
 }
 
@@ -622,6 +717,195 @@ __global__ __launch_bounds__(64) void k_la_resolve(DevTable t, const DPod *__res
         if (stamps) stamps[s] = res_stamp;
     }
     if ((uint32_t)lane < nd) { store_dyn(t, didx, dr); store_dynx<F>(t, didx, dx); }
+}
+
+// Single-wave resolver for normalizing profiles (TaintToleration / NodeAffinity on).  Keys carry
+// per-pod normalized scores, so a list is only valid while the pod's selection-time maxima (nf)
+// still hold.  The feasible set only shrinks during a stream, and only dirty nodes changed, so a
+// maximum still holds whenever fewer of its holders than nf.ct / nf.ca are dirty AND infeasible
+// now; otherwise (rare: few holders left) the wave rescans every node at the current state for
+// the exact maxima and keys (`nfall` counts those pods).  Supports overlapped windows (dprev/dcur)
+// like k_la_resolve4.
+template <uint32_t F, int EPL>
+__global__ __launch_bounds__(64) void k_la_resolve_norm(
+    DevTable t, const DPod *__restrict__ pods, const DPodX *__restrict__ podx, DevCfg c,
+    uint32_t s0, uint32_t P, uint32_t K, uint32_t GLp, uint32_t lr, LaShard sh,
+    const uint64_t *__restrict__ lists, const NormInfo *__restrict__ norm,
+    int32_t *__restrict__ out_node, uint64_t *__restrict__ out_key, uint64_t *__restrict__ stamps,
+    const uint32_t *__restrict__ dprev, uint32_t *__restrict__ dcur, unsigned long long *nfall) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const int lane = threadIdx.x;
+    const uint32_t n = t.n, nwords = (n + 31) / 32;
+    uint32_t *dirty = lds;
+    Row *srow = (Row *)(lds + ((nwords + 3) & ~3u));  // [64] slot rows, staged for a rescan
+    RowX *sx = (RowX *)(srow + 64);                    // [64]
+    Row *stage = (Row *)(sx + 64);                     // newly dirtied row hand-off
+    RowX *stagex = (RowX *)(stage + 1);
+    uint32_t *sidx = (uint32_t *)(stagex + 1);         // [64] slot -> node, staged for a rescan
+    for (uint32_t i = lane; i < nwords; i += 64) dirty[i] = 0;
+    const uint32_t kend = min(K, P - s0);
+    const uint32_t nd0 = dprev ? dprev[0] : 0u;
+    __syncthreads();
+    Row dr = empty_row();
+    RowX dx{};
+    uint32_t didx = 0xFFFFFFFFu;
+    if ((uint32_t)lane < nd0) {
+        didx = dprev[1 + lane];
+        dr = load_row(t, didx);
+        dx = load_rowx<F>(t, didx);
+        atomicOr(&dirty[didx >> 5], 1u << (didx & 31));
+    }
+    uint32_t nd = nd0;
+    bool won = false;
+    uint64_t res_key = 0, res_stamp = 0;
+    __syncthreads();
+    auto top2 = [&](const uint64_t(&e)[EPL], uint64_t &c1, uint64_t &c2) {
+        uint32_t word[EPL];
+#pragma unroll
+        for (int m = 0; m < EPL; ++m) {
+            const uint32_t nidx = e[m] ? key_node(e[m]) : 0u;
+            word[m] = dirty[nidx >> 5] >> (nidx & 31);
+        }
+        c1 = c2 = 0;
+#pragma unroll
+        for (int m = 0; m < EPL; ++m) {
+            const uint64_t x = (word[m] & 1u) ? 0ull : e[m];
+            const bool gt1 = x > c1;
+            c2 = gt1 ? c1 : (x > c2 ? x : c2);
+            c1 = gt1 ? x : c1;
+        }
+    };
+    uint64_t ent1[EPL], ent2[EPL];
+#pragma unroll
+    for (int m = 0; m < EPL; ++m) ent1[m] = list_ent(lists, 0, GLp, lr, sh, m, lane);
+#pragma unroll
+    for (int m = 0; m < EPL; ++m) ent2[m] = kend > 1 ? list_ent(lists, 1, GLp, lr, sh, m, lane) : 0ull;
+    uint64_t c1, c2;
+    top2(ent1, c1, c2);
+    Row r1 = load_row(t, c1 ? key_node(c1) : 0u), r2 = load_row(t, c2 ? key_node(c2) : 0u);
+    RowX x1 = load_rowx<F>(t, c1 ? key_node(c1) : 0u), x2 = load_rowx<F>(t, c2 ? key_node(c2) : 0u);
+    uint32_t wprev = 0xFFFFFFFFu;
+    for (uint32_t i = 0; i < kend; ++i) {
+        const DPod p = load_vgpr(pods + s0 + i);  // vector path: keeps the SGPRs from spilling
+        const DPodX px = load_vgpr(podx + s0 + i);
+        const NormInfo nf = load_vgpr(norm + i);
+        const bool use2 = c1 && key_node(c1) == wprev;
+        const uint64_t cand = use2 ? c2 : c1;
+        const Row crow = sel_row(use2, r2, r1);
+        const RowX cx = sel_rowx(use2, x2, x1);
+        if (i + 1 < kend) {  // next pod's candidates and rows; the pod after: its list entries
+            top2(ent2, c1, c2);
+            r1 = load_row(t, c1 ? key_node(c1) : 0u);
+            r2 = load_row(t, c2 ? key_node(c2) : 0u);
+            x1 = load_rowx<F>(t, c1 ? key_node(c1) : 0u);
+            x2 = load_rowx<F>(t, c2 ? key_node(c2) : 0u);
+        }
+        if (i + 2 < kend) {
+#pragma unroll
+            for (int m = 0; m < EPL; ++m) ent2[m] = list_ent(lists, i + 2, GLp, lr, sh, m, lane);
+        }
+        const double ymt = rcp_exact(nf.mt), yma = rcp_exact(nf.ma);
+        const bool act = (uint32_t)lane < nd;
+        const bool f = feasible<F>(dr, dx, p, px);
+        const uint32_t tot = node_total<F>(dr, dx, p, px, c, nf.mt, ymt, nf.ma, yma, nullptr);
+        const uint64_t fk = (act && f) ? pack_key(tot + 1, didx) : 0ull;
+        // do the selection-time maxima still hold?  (holders lost = dirty, infeasible now)
+        bool unsafe = false;
+        if (F & kFeatTaint) {
+            const uint32_t lost = (uint32_t)__popcll(__ballot(act && !f && taint_raw(dx, px) == nf.mt));
+            unsafe |= nf.mt > 0 && lost >= nf.ct;
+        }
+        if (F & kFeatAffinity) {
+            const uint32_t lost = (uint32_t)__popcll(__ballot(act && !f && affinity_raw(dx, p, px) == nf.ma));
+            unsafe |= nf.ma > 0 && lost >= nf.ca;
+        }
+        uint64_t ks;
+        if (!unsafe) {
+            ks = wave_max_u64(fk > cand ? fk : cand);
+        } else {
+            // exact rescan at the current state: slot rows from LDS, every other row from HBM
+            if (act) { srow[lane] = dr; sx[lane] = dx; sidx[lane] = didx; }
+            auto row_at = [&](uint32_t idx, Row &r, RowX &x) {
+                if ((dirty[idx >> 5] >> (idx & 31)) & 1u) {
+                    uint32_t j = 0;
+                    while (j < nd && sidx[j] != idx) ++j;  // dirty => held by a slot
+                    r = srow[j];
+                    x = sx[j];
+                } else {
+                    r = load_row(t, idx);
+                    x = load_rowx<F>(t, idx);
+                }
+            };
+            uint32_t mt = 0, ma = 0;
+            for (uint32_t idx = lane; idx < n; idx += 64) {
+                Row r; RowX x;
+                row_at(idx, r, x);
+                if (feasible<F>(r, x, p, px)) {
+                    const uint32_t a = taint_raw(x, px), b2 = affinity_raw(x, p, px);
+                    mt = a > mt ? a : mt;
+                    ma = b2 > ma ? b2 : ma;
+                }
+            }
+            mt = (F & kFeatTaint) ? wave_max_u32(mt) : 0u;
+            ma = (F & kFeatAffinity) ? wave_max_u32(ma) : 0u;
+            const double ymt2 = rcp_exact(mt), yma2 = rcp_exact(ma);
+            uint64_t best = 0;
+            for (uint32_t idx = lane; idx < n; idx += 64) {
+                Row r; RowX x;
+                row_at(idx, r, x);
+                const uint32_t tv = node_total<F>(r, x, p, px, c, mt, ymt2, ma, yma2, nullptr);
+                const uint64_t key = feasible<F>(r, x, p, px) ? pack_key(tv + 1, idx) : 0ull;
+                best = key > best ? key : best;
+            }
+            ks = wave_max_u64(best);
+            if (lane == 0 && nfall) atomicAdd(nfall, 1ull);
+        }
+        if (ks) {
+            const uint32_t win = key_node(ks);
+            const uint64_t own = __ballot(act && didx == win);
+            if (own) {
+                if (lane == __builtin_ctzll(own)) { reserve(dr, dx, p, +1); won = true; }
+            } else {
+                // clean winner: its row was prefetched by a lane whose candidate it is (after a
+                // rescan it may be nobody's candidate: then lane 0 loads it)
+                const uint64_t srcm = __ballot(cand == ks);
+                if (srcm) {
+                    if (lane == __builtin_ctzll(srcm)) { *stage = crow; *stagex = cx; }
+                } else if (lane == 0) {
+                    *stage = load_row(t, win);
+                    *stagex = load_rowx<F>(t, win);
+                }
+                const Row nr = *stage;
+                const RowX nx = *stagex;
+                if ((uint32_t)lane == nd) {
+                    dr = nr;
+                    dx = nx;
+                    reserve(dr, dx, p, +1);
+                    didx = win;
+                    won = true;
+                    dirty[win >> 5] |= 1u << (win & 31);
+                }
+                ++nd;
+            }
+        }
+        wprev = ks ? key_node(ks) : 0xFFFFFFFFu;
+        if ((uint32_t)lane == i) {
+            res_key = ks;
+            if (stamps) res_stamp = __builtin_amdgcn_s_memrealtime();
+        }
+    }
+    if ((uint32_t)lane < kend) {
+        const uint32_t s = s0 + lane;
+        out_node[s] = res_key ? (int32_t)key_node(res_key) : -1;
+        if (out_key) out_key[s] = res_key;
+        if (stamps) stamps[s] = res_stamp;
+    }
+    if ((uint32_t)lane < nd) { store_dyn(t, didx, dr); store_dynx<F>(t, didx, dx); }
+    if (dcur) {
+        const uint64_t wm = __ballot(won && (uint32_t)lane < nd);
+        if (won && (uint32_t)lane < nd) dcur[1 + __popcll(wm & ((1ull << lane) - 1ull))] = didx;
+        if (lane == 0) dcur[0] = (uint32_t)__popcll(wm);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1057,18 +1341,26 @@ hipError_t launch_scan_pod(const DevTable &t, const DPod *pods, const DPodX *pod
 size_t scan_scratch_bytes() { return sizeof(ScanScratch); }
 
 template <uint32_t F>
-static hipError_t la_window_f(const DevTable &t, const DPod *pods, uint32_t s0, uint32_t P,
-                              const DevCfg &c, const LaGeom &geo, uint64_t *lists,
-                              uint64_t *clists, int32_t *on, uint64_t *ok, uint64_t *st,
-                              uint64_t *diag, const uint32_t *dprev, uint32_t *dcur,
+static hipError_t la_window_f(const DevTable &t, const DPod *pods, const DPodX *podx, uint32_t s0,
+                              uint32_t P, const DevCfg &c, const LaGeom &geo, const LaBufs &bf,
+                              int32_t *on, uint64_t *ok, uint64_t *st, uint64_t *diag,
                               hipStream_t stream, int part) {
     const uint32_t K = geo.K, G = geo.G, L = geo.L, GLp = geo.eplr * 64;
     const uint32_t kw = min(K, P - s0);
     LaShard sh{geo.W, geo.v0, kw, 0u, (uint64_t)K * GLp};
-    if (part & 1) {
-        const dim3 grid(geo.nv * kw * G);
+    const dim3 grid(geo.nv * kw * G);
+    if ((part & 4) && (F & kFeatNorm)) {
         switch (geo.E) {
-#define QS_SEL(EE) case EE: hipLaunchKernelGGL((k_la_select<256, EE, F>), grid, dim3(256), 0, stream, t, pods, c, s0, P, sh, G, L, geo.chunk, GLp, lists, clists); break;
+#define QS_NRM(EE) case EE: hipLaunchKernelGGL((k_la_norm<256, EE, F>), grid, dim3(256), 0, stream, t, pods, podx, s0, P, sh, G, K, geo.chunk, bf.npart); break;
+            QS_NRM(1) QS_NRM(2) QS_NRM(3) QS_NRM(4) QS_NRM(5) QS_NRM(6) QS_NRM(8) QS_NRM(10) QS_NRM(12) QS_NRM(16)
+#undef QS_NRM
+            default: return hipErrorInvalidValue;
+        }
+        QS_RET(hipGetLastError());
+    }
+    if (part & 1) {
+        switch (geo.E) {
+#define QS_SEL(EE) case EE: hipLaunchKernelGGL((k_la_select<256, EE, F>), grid, dim3(256), 0, stream, t, pods, podx, c, s0, P, sh, G, L, geo.chunk, GLp, bf.lists, bf.clists, bf.npart, K, bf.norm); break;
             QS_SEL(1) QS_SEL(2) QS_SEL(3) QS_SEL(4) QS_SEL(5) QS_SEL(6) QS_SEL(8) QS_SEL(10) QS_SEL(12) QS_SEL(16)
 #undef QS_SEL
             default: return hipErrorInvalidValue;
@@ -1078,7 +1370,7 @@ static hipError_t la_window_f(const DevTable &t, const DPod *pods, uint32_t s0, 
             const uint32_t M = G * L, e2 = (M + 255) / 256;
             const dim3 mgrid(geo.nv * kw);
             switch (e2) {
-#define QS_MRG(EE) case EE: hipLaunchKernelGGL((k_la_merge<EE>), mgrid, dim3(256), 0, stream, clists, M, L, sh, GLp, lists); break;
+#define QS_MRG(EE) case EE: hipLaunchKernelGGL((k_la_merge<EE>), mgrid, dim3(256), 0, stream, bf.clists, M, L, sh, GLp, bf.lists); break;
                 QS_MRG(1) QS_MRG(2) QS_MRG(3) QS_MRG(4) QS_MRG(5) QS_MRG(6) QS_MRG(7) QS_MRG(8)
 #undef QS_MRG
                 default: return hipErrorInvalidValue;
@@ -1088,6 +1380,19 @@ static hipError_t la_window_f(const DevTable &t, const DPod *pods, uint32_t s0, 
     }
     if (part & 2) {
         const size_t bm = (((t.n + 31) / 32 + 3) & ~3u) * 4;
+        if constexpr ((F & kFeatNorm) != 0) {
+            const size_t ldsn = bm + 64 * (sizeof(Row) + sizeof(RowX)) + sizeof(Row) + sizeof(RowX) + 64 * 4;
+            switch (geo.epl) {
+#define QS_RESN(EP) case EP: hipLaunchKernelGGL((k_la_resolve_norm<F, EP>), dim3(1), dim3(64), ldsn, stream, t, pods, podx, c, s0, P, K, GLp, geo.lr, sh, bf.lists, bf.norm, on, ok, st, bf.dprev, bf.dcur, bf.nfall); break;
+                QS_RESN(1) QS_RESN(2) QS_RESN(4) QS_RESN(8) QS_RESN(16)
+#undef QS_RESN
+                default: return hipErrorInvalidValue;
+            }
+            return hipGetLastError();
+        }
+        const uint64_t *lists = bf.lists;
+        const uint32_t *dprev = bf.dprev;
+        uint32_t *dcur = bf.dcur;
         const size_t lds = bm + sizeof(Row) + sizeof(RowX);
         const size_t lds4 = bm + 5 * 2 * 64 * 8 + 2 * 64 * (sizeof(Row) + sizeof(int4)) + 2 * sizeof(ResPub) + 64 * 4 + 64 * sizeof(DPod);
         switch (geo.epl) {
@@ -1108,14 +1413,17 @@ static hipError_t la_window_f(const DevTable &t, const DPod *pods, uint32_t s0, 
     return hipGetLastError();
 }
 
-hipError_t launch_la_window(const DevTable &t, const DPod *pods, uint32_t s0, uint32_t P,
-                            const DevCfg &c, const LaGeom &geo, uint64_t *lists, uint64_t *clists,
+hipError_t launch_la_window(const DevTable &t, const DPod *pods, const DPodX *podx, uint32_t s0,
+                            uint32_t P, const DevCfg &c, const LaGeom &geo, const LaBufs &bf,
                             int32_t *on, uint64_t *ok, uint64_t *st, uint64_t *diag,
-                            const uint32_t *dprev, uint32_t *dcur, hipStream_t stream, int part) {
-    if (c.feat & kFeatNorm) return hipErrorInvalidValue;
-    if (dprev && geo.waves == 1) return hipErrorInvalidValue;  // overlap needs the 4-wave resolver
-    if (c.feat & kFeatExt) return la_window_f<kFeatExt>(t, pods, s0, P, c, geo, lists, clists, on, ok, st, diag, dprev, dcur, stream, part);
-    return la_window_f<0>(t, pods, s0, P, c, geo, lists, clists, on, ok, st, diag, dprev, dcur, stream, part);
+                            hipStream_t stream, int part) {
+    if (bf.dprev && geo.waves == 1 && !(c.feat & kFeatNorm)) return hipErrorInvalidValue;
+    if (c.feat & kFeatNorm) {
+        if (diag) return hipErrorInvalidValue;
+        return la_window_f<kFeatExt | kFeatTaint | kFeatAffinity>(t, pods, podx, s0, P, c, geo, bf, on, ok, st, diag, stream, part);
+    }
+    if (c.feat & kFeatExt) return la_window_f<kFeatExt>(t, pods, podx, s0, P, c, geo, bf, on, ok, st, diag, stream, part);
+    return la_window_f<0>(t, pods, podx, s0, P, c, geo, bf, on, ok, st, diag, stream, part);
 }
 
 LaGeom la_geometry(uint32_t n, uint32_t K, uint32_t W, uint32_t L) {

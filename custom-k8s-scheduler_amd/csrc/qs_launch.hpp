@@ -52,15 +52,24 @@ size_t scan_scratch_bytes();
 
 // L = list length per pod and shard (>= K; 2K for overlapped windows).
 LaGeom la_geometry(uint32_t n, uint32_t K, uint32_t W = 1, uint32_t L = 0);
-// lists: final [W][K][64*eplr] keys the resolver reads; clists: chunk-list scratch of
-// nv*K*G*L keys (select -> merge; unused when G == 1).
-hipError_t launch_la_window(const DevTable &t, const DPod *pods, uint32_t s0, uint32_t P,
-                            const DevCfg &c, const LaGeom &geo, uint64_t *lists, uint64_t *clists,
+// Device buffers of one lookahead window.  lists: final [W][K][64*eplr] keys the resolver reads;
+// clists: chunk-list scratch of nv*K*G*L keys (select -> merge; unused when G == 1); npart / norm:
+// normalizing profiles' [W][K][G] partial maxima and per-pod NormInfo; dprev/dcur (overlapped
+// windows): {count, nodes[64]} dirtied by the previous window (read) and by this window
+// (written), nullptr = windows back to back; nfall: count of exact-rescan pods (normalizing).
+struct NormInfo;
+struct LaBufs {
+    uint64_t *lists, *clists;
+    uint4 *npart;
+    NormInfo *norm;
+    const uint32_t *dprev;
+    uint32_t *dcur;
+    unsigned long long *nfall;
+};
+hipError_t launch_la_window(const DevTable &t, const DPod *pods, const DPodX *podx, uint32_t s0,
+                            uint32_t P, const DevCfg &c, const LaGeom &geo, const LaBufs &bufs,
                             int32_t *out_node, uint64_t *out_key, uint64_t *stamps, uint64_t *diag,
-                            const uint32_t *dprev, uint32_t *dcur, hipStream_t stream,
-                            int part = 3);  // part: 1 select(+merge), 2 resolve
-// dprev/dcur (overlapped windows, 4-wave resolver only): {count, nodes[64]} dirtied by the
-// previous window (read) and by this window (written); nullptr = windows run back to back.
+                            hipStream_t stream, int part);  // part: 4 norm, 1 select(+merge), 2 resolve
 
 __global__ void k_set_row(DevTable t, uint32_t i, HostRow v, uint32_t feat);
 

@@ -138,7 +138,8 @@ typedef struct qs_container {
 
 typedef struct qs_stats {
     uint64_t pods, placed, unschedulable, evals;
-    uint64_t batches, truncations;  /* lookahead windows run / windows cut early */
+    uint64_t batches, truncations;  /* lookahead windows run / pods resolved by an exact full
+                                       rescan (normalizing profiles: a normalize maximum lost) */
     double wall_s;                  /* qs_stream_run wall, device-resident inputs */
     double h2d_s, d2h_s;            /* host<->device copies around it (qs_schedule_stream) */
     double p50_cycle_us, p99_cycle_us, max_cycle_us; /* per-pod decision interval (record_timestamps) */

@@ -58,10 +58,31 @@ def test_lookahead_windows(oracle, K):
     assert_same(g[:2], o[:2], g[2], o[2])
 
 
-@pytest.mark.parametrize("engine", ["persistent", "scan"])
+@pytest.mark.parametrize("engine", ["persistent", "scan", "lookahead"])
 def test_config4_parity(oracle, engine):
     nodes, pods = synth_generate(4, 2000, 6000)
     g = run_gpu(nodes, pods, CFG4, engine)
+    o = run_oracle(oracle, nodes, pods, CFG4)
+    assert_same(g[:2], o[:2], g[2], o[2])
+
+
+@pytest.mark.parametrize("serial", [0, 1])
+def test_config4_full_lookahead(oracle, serial):
+    """BASELINE.json configs[3]: 5,000 nodes x 150,000 pods, Fit + Balanced + TaintToleration +
+    NodeAffinity + amd.com/gpu, on the normalizing LOOKAHEAD engine (overlapped and serial)."""
+    nodes, pods = synth_generate(4, 5000, 150000)
+    g = run_gpu(nodes, pods, dict(CFG4, lookahead_serial=serial), "lookahead")
+    o = run_oracle(oracle, nodes, pods, CFG4)
+    assert_same(g[:2], o[:2], g[2], o[2])
+    assert g[3]["engine_used"] == "lookahead"
+
+
+@pytest.mark.parametrize("K", [1, 5, 32, 64])
+def test_config4_lookahead_windows(oracle, K):
+    """Tight cluster (many nodes fill up): exercises the normalize-maximum safety test and the
+    exact rescan fallback."""
+    nodes, pods = synth_generate(4, 400, 14000)
+    g = run_gpu(nodes, pods, CFG4, "lookahead", lookahead=K)
     o = run_oracle(oracle, nodes, pods, CFG4)
     assert_same(g[:2], o[:2], g[2], o[2])
 

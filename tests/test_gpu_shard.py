@@ -62,3 +62,22 @@ def test_rccl_one_rank_communicator(oracle):
     g = run_sharded(nodes, pods, {}, shard=(0, 1, dist_unique_id()))
     o = run_oracle(oracle, nodes, pods, {})
     assert_same(g[:2], o[:2], g[2], o[2])
+
+
+@pytest.mark.parametrize("W", [2, 4])
+def test_config4_virtual_shards(oracle, W):
+    """Normalizing profile, sharded: partial maxima of every shard combine into each pod's
+    NormInfo before the shard selects (the RCCL path all-gathers them first)."""
+    from test_gpu_parity import CFG4
+    nodes, pods = synth_generate(4, 3000, 9000)
+    g = run_sharded(nodes, pods, dict(CFG4, virtual_shards=W))
+    o = run_oracle(oracle, nodes, pods, CFG4)
+    assert_same(g[:2], o[:2], g[2], o[2])
+
+
+def test_config4_rccl_one_rank(oracle):
+    from test_gpu_parity import CFG4
+    nodes, pods = synth_generate(4, 2000, 5000)
+    g = run_sharded(nodes, pods, CFG4, shard=(0, 1, dist_unique_id()))
+    o = run_oracle(oracle, nodes, pods, CFG4)
+    assert_same(g[:2], o[:2], g[2], o[2])
