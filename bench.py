@@ -34,7 +34,10 @@ WORKLOADS = {
                                  "Fit+Balanced+QoS weights, percentageOfNodesToScore=100"),
     "config3": (3, 50000, 1000000, "config3: 50,000 nodes x 1,000,000 pods, exact sequential, "
                                    "node table sharded across ranks (RCCL all-gather per window)"),
+    "config4": (4, 5000, 150000, "config4: 5,000 nodes x 150,000 pods, exact sequential, Fit + "
+                                 "Balanced + TaintToleration + NodeAffinity + amd.com/gpu"),
 }
+PROFILE = {"config4": {"enable_taint": 1, "enable_affinity": 1}}  # plugin switches per workload
 B_NODE = 32  # algorithmic bytes per pod×node evaluation (8 int32 columns)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md:36 (spec); 6,290 GB/s measured
 KERNEL_NAMES = {"resolve": "k_la_resolve4", "select": "k_la_select", "persistent": "k_persistent",
@@ -172,7 +175,7 @@ def measure(cx, a, workload, steps, warmup, with_diag=True):
     sharded = workload == "config3" and cx.world > 1
     seed = 0x5EED0000 + gen + (cx.rank if (cx.world > 1 and not sharded) else 0)
     nodes, pods = qsched.synth_generate(gen, n_nodes, n_pods, seed=seed)
-    cfg = {"engine": a.engine, "lookahead": a.lookahead}
+    cfg = dict({"engine": a.engine, "lookahead": a.lookahead}, **PROFILE.get(workload, {}))
     s = open_sched(cx, cfg, sharded)
     s.load_nodes(nodes)
     s.save_table()
@@ -249,9 +252,10 @@ def main():
     cx = Ctx()
     workload = a.workload if a.workload != "auto" else ("config2" if cx.world == 1 else "config3")
     m = measure(cx, a, workload, a.steps, a.warmup)
-    c3 = scan = None
+    c3 = c4 = scan = None
     if cx.world == 1 and workload == "config2" and not a.no_config3:
         c3 = measure(cx, a, "config3", 1, 1, with_diag=False)
+        c4 = measure(cx, a, "config4", 3, 1, with_diag=False)
     if cx.world == 1 and not a.no_scan:
         scan = scan_roofline(cx, a)
     if cx.rank == 0:
@@ -283,6 +287,12 @@ def main():
                               "evals_per_s": round(c3["value"] * c3["n_nodes"], 1),
                               "ms_per_step": round(c3["ms_per_step"], 3), "steps": 1,
                               "engine": c3["engine"]}
+        if c4 is not None:
+            out["config4"] = {"workload": c4["desc"], "value": round(c4["value"], 1), "unit": "pods/s",
+                              "evals_per_s": round(c4["value"] * c4["n_nodes"], 1),
+                              "ms_per_step": round(c4["ms_per_step"], 3), "steps": 3,
+                              "engine": c4["engine"],
+                              "unschedulable_frac": round(c4["unschedulable_frac"], 5)}
         if scan is not None:
             out["scan"] = scan
         if cx.world == 1 and not a.no_cpu:

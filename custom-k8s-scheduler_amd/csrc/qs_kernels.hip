@@ -785,10 +785,20 @@ __global__ __launch_bounds__(64) void k_la_resolve_norm(
     Row r1 = load_row(t, c1 ? key_node(c1) : 0u), r2 = load_row(t, c2 ? key_node(c2) : 0u);
     RowX x1 = load_rowx<F>(t, c1 ? key_node(c1) : 0u), x2 = load_rowx<F>(t, c2 ? key_node(c2) : 0u);
     uint32_t wprev = 0xFFFFFFFFu;
+    // pod records + normalization facts, one pod ahead, through the vector path (scalar copies
+    // of the 44-dword extension record spilled the SGPRs)
+    DPod pn = load_vgpr(pods + s0);
+    DPodX pxn = load_vgpr(podx + s0);
+    NormInfo nfn = load_vgpr(norm);
     for (uint32_t i = 0; i < kend; ++i) {
-        const DPod p = load_vgpr(pods + s0 + i);  // vector path: keeps the SGPRs from spilling
-        const DPodX px = load_vgpr(podx + s0 + i);
-        const NormInfo nf = load_vgpr(norm + i);
+        const DPod p = pn;
+        const DPodX px = pxn;
+        const NormInfo nf = nfn;
+        if (i + 1 < kend) {
+            pn = load_vgpr(pods + s0 + i + 1);
+            pxn = load_vgpr(podx + s0 + i + 1);
+            nfn = load_vgpr(norm + i + 1);
+        }
         const bool use2 = c1 && key_node(c1) == wprev;
         const uint64_t cand = use2 ? c2 : c1;
         const Row crow = sel_row(use2, r2, r1);
