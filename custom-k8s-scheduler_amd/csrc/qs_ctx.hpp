@@ -17,6 +17,9 @@ namespace qs_host {
 constexpr int64_t kLimit = (1LL << 24) - 1;  // 24-bit multiplier range of the kernels (spec S10)
 // Tables at least this large also keep the SoA copy the SCAN engine streams (L2-resident below).
 constexpr uint32_t kSoaMinNodes = 1u << 16;
+// Tables up to this size also keep the batched-mode anti-affinity state (128 B of app bits per
+// node + the (app, zone) counts) inside the table allocation, so save/restore covers it.
+constexpr uint32_t kAaMaxNodes = 1u << 20;
 
 struct QsError {
     qs_status st;
@@ -56,9 +59,11 @@ struct Mirror {
     std::vector<int64_t> ac, am, mp, rc, rm, zc, zm, np;
     std::vector<int64_t> ae, re;  // [n][QS_MAX_EXT]
     std::vector<uint64_t> th, ts, lb;  // lb [n][2]
+    std::vector<int32_t> zone;
     std::vector<uint64_t> gen;
     void resize(uint32_t nn) {
         n = nn;
+        zone.assign(nn, 0);
         for (auto *v : {&ac, &am, &mp, &rc, &rm, &zc, &zm, &np}) v->assign(nn, 0);
         ae.assign((size_t)nn * QS_MAX_EXT, 0);
         re.assign((size_t)nn * QS_MAX_EXT, 0);
@@ -108,7 +113,7 @@ struct qs_ctx {
     bool saved = false;
     bool mirror_stale = false;  // device ran a stream since the last mirror sync
     qs_host::DevBuf diag;
-    qs_host::DevBuf scratch, lists, clists, dio, npart, normi, nfall, one_pod, one_podx, out_feas, out_score, out_total;
+    qs_host::DevBuf scratch, lists, clists, dio, npart, normi, nfall, bctrl, one_pod, one_podx, out_feas, out_score, out_total;
     uint32_t cap = 0;
     // sharding (qs_open_shard): RCCL communicator of this rank, nullptr when unsharded
     int rank = 0, world = 1;

@@ -38,14 +38,34 @@ enum : int { kSAc, kSAm, kSRc, kSRm, kSZc, kSZm, kSNp, kSMp, kSAe0, kSRe0, kSAe1
 struct DevSoa {
     int32_t *c[kSCols];
 };
+// Anti-affinity state of batched mode (spec S11): per node its topology zone, per (app, node) a
+// presence bit (word-major: word w of node i at apps[w * cap + i], so a wave over consecutive
+// nodes reads consecutive words), per (app, zone) a pod count.  apps == nullptr: not kept.
+constexpr uint32_t kMaxApps = 1024, kMaxZones = 64, kAppWords = kMaxApps / 32;
 struct DevTable {
     DRow *rows;
     DMask *masks;
     uint32_t n;
     DevSoa soa;
+    int32_t *zone;
+    uint32_t *apps;
+    int32_t *zcount;  // [kMaxApps][kMaxZones]
+    uint32_t cap;     // row capacity (stride of the app words)
 };
 
 enum : uint32_t { kFeatTaint = 1u, kFeatAffinity = 2u, kFeatExt = 4u };
+
+// pod flags: bits 0-1 QoS, 4-6 required terms, 8-10 preferred terms, 12-13 anti-affinity kind,
+// 16-25 app group (spec S11)
+__device__ __forceinline__ uint32_t pod_aa(uint32_t flags) { return (flags >> 12) & 3u; }
+__device__ __forceinline__ uint32_t pod_app(uint32_t flags) { return (flags >> 16) & 1023u; }
+// Required anti-affinity of a batched-mode pod against node i (state at batch start).
+__device__ __forceinline__ bool aa_ok(const DevTable &t, uint32_t flags, uint32_t i) {
+    const uint32_t aa = pod_aa(flags), app = pod_app(flags);
+    if (aa == 1u) return !((t.apps[(size_t)(app >> 5) * t.cap + i] >> (app & 31u)) & 1u);
+    if (aa == 2u) return t.zcount[app * kMaxZones + (uint32_t)t.zone[i]] == 0;
+    return true;
+}
 
 // Profile constants resolved on the host.
 struct DevCfg {

@@ -120,7 +120,7 @@ qs_status qs_synth_generate(int config, uint64_t seed, uint32_t n, uint32_t p,
     static const int64_t kPodMemMi[7] = {128, 256, 512, 1024, 2048, 4096, 8192};
     static const int64_t kGpu[4] = {1, 2, 4, 8};
     const int64_t GiB = 1LL << 30, MiB = 1LL << 20;
-    const bool c4 = config == 4;
+    const bool c4 = config == 4, c5 = config == 5;
     if (n && (!nd || !nd->alloc_cpu || !nd->alloc_mem)) return QS_EINVAL;
     if (p && !pods) return QS_EINVAL;
     for (uint32_t i = 0; i < n; i++) {
@@ -155,6 +155,7 @@ qs_status qs_synth_generate(int config, uint64_t seed, uint32_t n, uint32_t p,
                 for (int b = a + 1; b < 10; b++)
                     if (a == zone || b == zone) set_bit128(lb, zone_pair_bit(a, b));
         }
+        if (nd->zone) nd->zone[i] = (c4 || c5) ? (int32_t)pick(seed, c + 4, 10) : 0;  // zone z0..z9
         if (nd->taint_hard) nd->taint_hard[i] = th;
         if (nd->taint_soft) nd->taint_soft[i] = ts;
         if (nd->label_bits) { nd->label_bits[2 * (size_t)i] = lb[0]; nd->label_bits[2 * (size_t)i + 1] = lb[1]; }
@@ -206,6 +207,11 @@ qs_status qs_synth_generate(int config, uint64_t seed, uint32_t n, uint32_t p,
             if (pick(seed, c + 12, 10) == 0) tol_soft |= 2ULL;
         }
         qs_pod_from_containers(&ct, 1, nullptr, &pd);
+        if (c5) {  // spec/synth.md G5: app group and its required anti-affinity kind
+            pd.app = (int32_t)pick(seed, c + 13, 1000);
+            const uint32_t kind = pick(seed, 8ULL * n + 16ULL * p + (uint64_t)pd.app, 10);
+            pd.anti_affinity = kind < 5 ? QS_AA_HOSTNAME : (kind == 5 ? QS_AA_ZONE : QS_AA_NONE);
+        }
         pd.tol_hard = tol_hard;
         pd.tol_soft = tol_soft;
         pd.sel[0] = sel[0];

@@ -100,6 +100,9 @@ HostRow compact_row(const Mirror &m, uint32_t i, int shift) {
     check_range(m.zm[i] >> shift, "nz_mem", i);
     check_range(m.np[i], "pods", i);
     check_range(m.mp[i], "max_pods", i);
+    if (m.zone[i] < 0 || m.zone[i] >= (int32_t)kMaxZones)
+        fail(QS_EINVAL, "node " + std::to_string(i) + ": zone outside [0, 64)");
+    r.zone = m.zone[i];
     r.ac = (int32_t)m.ac[i];
     r.am = (int32_t)(m.am[i] >> shift);
     r.rc = (int32_t)m.rc[i];
@@ -127,10 +130,28 @@ HostRow compact_row(const Mirror &m, uint32_t i, int shift) {
 
 // Table layout inside ctx->tbl: cap rows of 64 B, then cap mask rows of 32 B.  Returns the size;
 // assigns the pointers when base != nullptr.
+// Table layout inside ctx->tbl: cap rows of 64 B, cap mask rows of 32 B, cap zone ids, then (tables
+// up to kAaMaxNodes) the anti-affinity state: kAppWords x cap app words and the (app, zone)
+// counts.  Returns the size; assigns the pointers when base != nullptr.
 size_t carve(DevTable &t, uint32_t cap, char *base) {
-    t.rows = base ? (DRow *)base : nullptr;
-    t.masks = base ? (DMask *)(base + (size_t)cap * sizeof(DRow)) : nullptr;
-    return (size_t)cap * (sizeof(DRow) + sizeof(DMask));
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        char *p = base ? base + off : nullptr;
+        off += (bytes + 255) & ~(size_t)255;
+        return p;
+    };
+    t.rows = (DRow *)take((size_t)cap * sizeof(DRow));
+    t.masks = (DMask *)take((size_t)cap * sizeof(DMask));
+    t.zone = (int32_t *)take((size_t)cap * 4);
+    t.cap = cap;
+    if (cap <= kAaMaxNodes) {
+        t.apps = (uint32_t *)take((size_t)kAppWords * cap * 4);
+        t.zcount = (int32_t *)take((size_t)kMaxApps * kMaxZones * 4);
+    } else {
+        t.apps = nullptr;
+        t.zcount = nullptr;
+    }
+    return off;
 }
 
 DRow to_drow(const HostRow &r) {
@@ -173,6 +194,11 @@ void upload_table(qs_ctx *c) {
     if (n) {
         HIPCHK(hipMemcpyAsync(c->dt.rows, rows.data(), n * sizeof(DRow), hipMemcpyHostToDevice, c->stream));
         HIPCHK(hipMemcpyAsync(c->dt.masks, masks.data(), n * sizeof(DMask), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(c->dt.zone, c->m.zone.data(), n * 4, hipMemcpyHostToDevice, c->stream));
+    }
+    if (c->dt.apps) {  // a (re)loaded table starts with no batched-mode pods placed
+        HIPCHK(hipMemsetAsync(c->dt.apps, 0, (size_t)kAppWords * c->cap * 4, c->stream));
+        HIPCHK(hipMemsetAsync(c->dt.zcount, 0, (size_t)kMaxApps * kMaxZones * 4, c->stream));
     }
     if (soa) {
         c->soa.ensure(cols.size() * 4);
@@ -237,6 +263,8 @@ void check_pod(const qs_pod &p, uint32_t j) {
         bad("term count out of range");
     for (int t = 0; t < p.n_pref_terms; t++)
         if (p.pref_weight[t] < 0 || p.pref_weight[t] > 100) bad("preferred term weight must be 0..100");
+    if (p.app < 0 || p.app >= QS_MAX_APPS) bad("app outside [0, QS_MAX_APPS)");
+    if (p.anti_affinity < QS_AA_NONE || p.anti_affinity > QS_AA_ZONE) bad("anti_affinity must be 0..2");
 }
 
 DPod compact_pod(const qs_ctx *c, const qs_pod &p, uint32_t j, int shift) {
@@ -252,7 +280,8 @@ DPod compact_pod(const qs_ctx *c, const qs_pod &p, uint32_t j, int shift) {
     d.re1 = (int32_t)p.req_ext[1];
     d.wfit = (uint16_t)c->cfg.w_fit[p.qos];
     d.wbal = (uint16_t)c->cfg.w_bal[p.qos];
-    d.flags = (uint32_t)p.qos | ((uint32_t)p.n_req_terms << 4) | ((uint32_t)p.n_pref_terms << 8);
+    d.flags = (uint32_t)p.qos | ((uint32_t)p.n_req_terms << 4) | ((uint32_t)p.n_pref_terms << 8) |
+              ((uint32_t)p.anti_affinity << 12) | ((uint32_t)p.app << 16);
     return d;
 }
 
@@ -375,6 +404,7 @@ int pick_engine(const qs_ctx *c, uint32_t n) {
         else if (n <= persistent_max_nodes(feat)) e = QS_ENGINE_PERSISTENT;
         else e = QS_ENGINE_SCAN;
     }
+    if (e == QS_ENGINE_BATCHED) fail(QS_EINVAL, "the batched engine runs through QS_MODE_BATCHED");
     if (e == QS_ENGINE_PERSISTENT && n > persistent_max_nodes(feat))
         fail(QS_EINVAL, "PERSISTENT engine supports at most " +
                             std::to_string(persistent_max_nodes(feat)) + " nodes for this profile");
@@ -415,6 +445,101 @@ void percentile_stats(const std::vector<uint64_t> &st, qs_stats *s) {
 }
 
 }  // namespace
+
+// QS_MODE_BATCHED (spec S11): batches of B <= 64 pods; per batch one select + merge (each pod's
+// 64 best keys against the batch-start table, anti-affinity included) and one claim kernel that
+// resolves the batch, applies it and builds the next one on the device.  The ceil(P/B) batches of
+// a stream are captured once as a HIP graph; the few pods still carried at the end (all their
+// candidates claimed by earlier pods of their batch) run in extra batches.  Returns the batch count.
+uint64_t run_batched(qs_ctx *c, qs_stream *s, const DPod *dp, const DPodX *dx, int32_t *on, uint64_t *ok,
+                     KernelTimer &kt) {
+    const uint32_t n = c->m.n, P = s->p;
+    if (c->dc.feat & (kFeatTaint | kFeatAffinity))
+        fail(QS_EINVAL, "QS_MODE_BATCHED supports the Fit + Balanced (+ extended resources) profile");
+    if (!c->dt.apps) fail(QS_EINVAL, "QS_MODE_BATCHED keeps anti-affinity state for tables up to 2^20 nodes");
+    if (c->world > 1 || c->cfg.virtual_shards > 1) fail(QS_EINVAL, "QS_MODE_BATCHED runs unsharded");
+    if (batch_claim_lds(n) > 160 * 1024)
+        fail(QS_EINVAL, "QS_MODE_BATCHED claims batches in LDS: tables up to 845,824 nodes");
+    HIPCHK(batch_claim_prepare());
+    const uint32_t B = c->cfg.batch_pods > 0 ? (uint32_t)std::min(64, c->cfg.batch_pods) : 64u;
+    LaGeom geo = la_geometry(n, B, 1, 64);
+    if (geo.G == 0) fail(QS_EINVAL, "no batched geometry for this table size");
+    geo.waves = 4;
+    geo.k32 = 0;
+    const size_t lwords = (size_t)geo.K * 64 * geo.eplr;
+    const size_t cwords = std::max<size_t>(1, (size_t)geo.K * geo.G * geo.L);
+    c->lists.ensure(8 * lwords);
+    c->clists.ensure(8 * cwords);
+    c->bctrl.ensure(4 * 128);
+    uint32_t *ctrl = c->bctrl.as<uint32_t>(), *bidx = ctrl + 64;
+    LaBufs bf{c->lists.as<uint64_t>(), c->clists.as<uint64_t>(), nullptr, nullptr, nullptr, nullptr,
+              nullptr, bidx, ctrl};
+    auto batch = [&]() {
+        kt.begin(2, c->stream);
+        HIPCHK(launch_la_window(c->dt, dp, dx, 0, P, c->dc, geo, bf, on, ok, nullptr, nullptr, c->stream, 1));
+        kt.end(2, c->stream);
+        kt.begin(3, c->stream);
+        HIPCHK(launch_batch_claim(c->dt, dp, bf.lists, ctrl, bidx, P, B, on, ok, c->stream));
+        kt.end(3, c->stream);
+    };
+    const uint32_t nb0 = (P + B - 1) / B;
+    auto enqueue = [&]() {
+        HIPCHK(hipMemsetAsync(bf.lists, 0, 8 * lwords, c->stream));
+        HIPCHK(launch_batch_init(ctrl, bidx, P, B, c->stream));
+        static const char *se = getenv("QS_SYNC_EVERY");  // profiling aid (see the lookahead run)
+        const uint32_t every = se ? (uint32_t)atoi(se) : 0u;
+        for (uint32_t b = 0; b < nb0; ++b) {
+            batch();
+            if (every && (b + 1) % every == 0 && !kt.on) HIPCHK(hipStreamSynchronize(c->stream));
+        }
+    };
+    static const char *genv = getenv("QS_GRAPH");
+    if (!kt.on && !(genv && genv[0] == '0')) {
+        std::vector<uint8_t> key;
+        auto put = [&](const void *p, size_t nb) { key.insert(key.end(), (const uint8_t *)p, (const uint8_t *)p + nb); };
+        const void *ptrs[] = {c->dt.rows, c->dt.apps, bf.lists, bf.clists, ctrl, dp, on, ok};
+        put(ptrs, sizeof ptrs);
+        put(&c->dt.n, sizeof c->dt.n);
+        put(&c->dc, sizeof c->dc);
+        put(&geo, sizeof geo);
+        const int tag = 2;  // batched
+        put(&tag, sizeof tag);
+        if (!s->gexec || s->gkey != key) {
+            if (s->gexec) (void)hipGraphExecDestroy(s->gexec);
+            s->gexec = nullptr;
+            HIPCHK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+            try {
+                enqueue();
+            } catch (...) {
+                hipGraph_t g = nullptr;
+                (void)hipStreamEndCapture(c->stream, &g);
+                if (g) (void)hipGraphDestroy(g);
+                throw;
+            }
+            hipGraph_t g = nullptr;
+            HIPCHK(hipStreamEndCapture(c->stream, &g));
+            const hipError_t ie = hipGraphInstantiate(&s->gexec, g, nullptr, nullptr, 0);
+            (void)hipGraphDestroy(g);
+            HIPCHK(ie);
+            s->gkey = key;
+        }
+        HIPCHK(hipGraphLaunch(s->gexec, c->stream));
+    } else {
+        enqueue();
+    }
+    uint64_t batches = nb0;
+    for (;;) {  // carried pods left after the planned batches
+        uint32_t h[2] = {0, 0};
+        HIPCHK(hipMemcpyAsync(h, ctrl, 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (h[0] == 0) break;
+        if (batches > 2ull * P + 64) fail(QS_EDEVICE, "batched mode made no progress");  // cannot happen
+        batch();
+        ++batches;
+    }
+    c->soa_valid = false;
+    return batches;
+}
 
 // =============================================================================================
 // C ABI
@@ -505,6 +630,7 @@ qs_status qs_nodes_load(qs_ctx *c, const qs_node_soa *nd, uint32_t n) {
                 m.ae[(size_t)i * QS_MAX_EXT + k] = get(nd->alloc_ext, (size_t)i * QS_MAX_EXT + k, 0);
                 m.re[(size_t)i * QS_MAX_EXT + k] = get(nd->req_ext, (size_t)i * QS_MAX_EXT + k, 0);
             }
+            m.zone[i] = nd->zone ? nd->zone[i] : 0;
             m.th[i] = nd->taint_hard ? nd->taint_hard[i] : 0;
             m.ts[i] = nd->taint_soft ? nd->taint_soft[i] : 0;
             m.lb[2 * (size_t)i] = nd->label_bits ? nd->label_bits[2 * (size_t)i] : 0;
@@ -533,6 +659,7 @@ qs_status qs_nodes_read(qs_ctx *c, const qs_node_soa_out *o, uint32_t n) {
         if (o->taint_hard) std::memcpy(o->taint_hard, m.th.data(), 8 * (size_t)n);
         if (o->taint_soft) std::memcpy(o->taint_soft, m.ts.data(), 8 * (size_t)n);
         if (o->label_bits) std::memcpy(o->label_bits, m.lb.data(), 16 * (size_t)n);
+        if (o->zone) std::memcpy(o->zone, m.zone.data(), 4 * (size_t)n);
     });
 }
 
@@ -553,6 +680,7 @@ qs_status qs_node_upsert(qs_ctx *c, uint32_t idx, const qs_node_row *r, uint64_t
             std::copy(old.ts.begin(), old.ts.end(), m.ts.begin());
             std::copy(old.lb.begin(), old.lb.end(), m.lb.begin());
             std::copy(old.gen.begin(), old.gen.end(), m.gen.begin());
+            std::copy(old.zone.begin(), old.zone.end(), m.zone.begin());
             c->dev_valid = false;
         } else if (generation != 0 && generation <= m.gen[idx]) {
             return;  // already applied (UP NodeInfo.Generation diff)
@@ -566,6 +694,7 @@ qs_status qs_node_upsert(qs_ctx *c, uint32_t idx, const qs_node_row *r, uint64_t
         }
         m.th[idx] = r->taint_hard; m.ts[idx] = r->taint_soft;
         m.lb[2 * (size_t)idx] = r->label_bits[0]; m.lb[2 * (size_t)idx + 1] = r->label_bits[1];
+        m.zone[idx] = r->zone;
         m.gen[idx] = generation;
         const int want = std::min({ctz64(r->alloc_mem), ctz64(r->req_mem), ctz64(r->nz_mem)});
         if (want < c->shift) { c->shift = want; c->dev_valid = false; }
@@ -674,12 +803,12 @@ qs_status qs_stream_prepare(qs_ctx *c, const qs_pod *pods, uint32_t p, qs_stream
 qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) {
     return guarded(c, [&] {
         if (!s) fail(QS_EINVAL, "null stream");
-        if (mode != QS_MODE_EXACT) fail(QS_EINVAL, "only QS_MODE_EXACT is implemented");
+        if (mode != QS_MODE_EXACT && mode != QS_MODE_BATCHED) fail(QS_EINVAL, "unknown qs_mode");
         if (s->shift != c->shift || !c->dev_valid) fail(QS_ESTATE, "node table recompacted after prepare");
         HIPCHK(hipSetDevice(c->device));
         const uint32_t n = c->m.n, P = s->p;
         c->dc.feat = s->feat;
-        const int eng = pick_engine(c, n);
+        const int eng = mode == QS_MODE_BATCHED ? QS_ENGINE_BATCHED : pick_engine(c, n);
         int32_t *on = s->d_node.as<int32_t>();
         uint64_t *ok = s->d_key.as<uint64_t>();
         uint64_t *st = c->cfg.record_timestamps ? s->d_stamp.as<uint64_t>() : nullptr;
@@ -696,7 +825,9 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
         } else if (P > 0) {
             const DPod *dp = s->d_pods.as<DPod>();
             const DPodX *dx = s->d_podx.as<DPodX>();
-            if (eng == QS_ENGINE_PERSISTENT) {
+            if (eng == QS_ENGINE_BATCHED) {
+                batches = run_batched(c, s, dp, dx, on, ok, kt);
+            } else if (eng == QS_ENGINE_PERSISTENT) {
                 kt.begin(0, c->stream);
                 HIPCHK(launch_persistent(c->dt, dp, dx, P, c->dc, on, ok, st, c->stream));
                 kt.end(0, c->stream);

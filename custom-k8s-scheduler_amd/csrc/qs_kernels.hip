@@ -497,12 +497,21 @@ __global__ __launch_bounds__(BS) void k_la_select(DevTable t, const DPod *__rest
                                                   uint32_t GLp, uint64_t *__restrict__ lists,
                                                   uint64_t *__restrict__ clists,
                                                   const uint4 *__restrict__ npart, uint32_t K,
-                                                  NormInfo *__restrict__ norm_out) {
+                                                  NormInfo *__restrict__ norm_out,
+                                                  const uint32_t *__restrict__ pidx,
+                                                  const uint32_t *__restrict__ pcount) {
     const SelBlock b = sel_block(t, sh, G, chunk);
-    const uint32_t s = s0 + b.k;
-    if (s >= P) return;
+    uint32_t s;
+    if (pidx) {  // batched mode: the batch's stream positions and size live on the device
+        if (b.k >= *pcount) return;
+        s = pidx[b.k];
+    } else {
+        s = s0 + b.k;
+        if (s >= P) return;
+    }
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const DPod p = pods[s];
+    const bool aa = t.apps && pod_aa(p.flags) != 0;  // batched-mode anti-affinity (spec S11)
     DPodX px{};
     NormInfo nf{0, 0, 0, 0};
     if (F & kFeatNorm) {
@@ -520,7 +529,7 @@ __global__ __launch_bounds__(BS) void k_la_select(DevTable t, const DPod *__rest
         if (idx < b.end) {
             const Row r = load_row(t, idx);
             const RowX x = load_rowx<F>(t, idx);
-            const bool f = feasible<F>(r, x, p, px);
+            const bool f = feasible<F>(r, x, p, px) && (!aa || aa_ok(t, p.flags, idx));
             const uint32_t tot = node_total<F>(r, x, p, px, c, nf.mt, ymt, nf.ma, yma, nullptr);
             tv[j] = f ? tot + 1 : 0;
         }
@@ -1217,6 +1226,238 @@ __global__ __launch_bounds__(256) void k_la_resolve4(DevTable t, const DPod *__r
 }
 
 // =============================================================================================
+// BATCHED mode (spec S11): per batch of B <= 64 pods, k_la_select + k_la_merge give each pod its
+// 64 best keys against the batch-start table; k_batch_claim walks the batch in queue order, each
+// pod claiming its best key whose node (and, for zone anti-affinity, whose (app, zone)) no earlier
+// pod of the batch claimed, then applies every claim (Reserve + anti-affinity state) and builds
+// the next batch: the pods that found no free candidate first, then fresh pods from the stream.
+// ctrl = {pods in the batch, stream cursor}.
+// =============================================================================================
+__global__ void k_batch_init(uint32_t *ctrl, uint32_t *bidx, uint32_t P, uint32_t B) {
+    const uint32_t nb = min(P, B);
+    if (threadIdx.x < nb) bidx[threadIdx.x] = threadIdx.x;
+    if (threadIdx.x == 0) { ctrl[0] = nb; ctrl[1] = nb; }
+}
+
+// Descending bitonic sort of one 64-bit key per lane across the wave (21 compare-exchange steps).
+__device__ __forceinline__ uint64_t wave_sort_desc(uint64_t v, int lane) {
+#pragma unroll
+    for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, j);
+            const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), j);
+            const uint64_t o = ((uint64_t)hi << 32) | lo;
+            const bool keep_max = ((lane & j) == 0) == ((lane & k) == 0);
+            v = keep_max ? (v > o ? v : o) : (v < o ? v : o);
+        }
+    }
+    return v;
+}
+
+#ifdef QS_CLAIM_DIAG
+__device__ uint64_t g_claim_diag[5];
+#define CLAIM_STAMP0() uint64_t cds[4] = {0, 0, 0, 0}; uint64_t ctp = diag_stamp();
+#define CLAIM_STAMP(q) { const uint64_t t_ = diag_stamp(); cds[q] += t_ - ctp; ctp = t_; }
+#else
+#define CLAIM_STAMP0()
+#define CLAIM_STAMP(q)
+#endif
+constexpr int kClaimWaves = 16;
+
+__global__ __launch_bounds__(64 * kClaimWaves) void k_batch_claim(
+    DevTable t, const DPod *__restrict__ pods, const uint64_t *__restrict__ lists, uint32_t GLp,
+    uint32_t *ctrl, uint32_t *bidx, uint32_t P, uint32_t B, int32_t *__restrict__ out_node,
+    uint64_t *__restrict__ out_key) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    CLAIM_STAMP0();
+    const uint32_t nwords = (t.n + 31) / 32;
+    uint32_t *claimed = lds;                                   // node bitmap
+    uint32_t *claimed_az = lds + ((nwords + 3) & ~3u);         // (app, zone) bitmap
+    uint32_t *pend = claimed_az + kMaxApps * kMaxZones / 32;   // carried pods (<= 64)
+    uint64_t *lkey = (uint64_t *)(pend + 64);                  // [64 pods][64] keys, best first
+    uint32_t *lzone = (uint32_t *)(lkey + 64 * 64);            // [64 pods][64] their zones
+    uint32_t *lpod = lzone + 64 * 64;                          // [64] stream positions, [64] flags
+    const uint32_t nb = ctrl[0], cursor = ctrl[1];
+    for (uint32_t i = tid; i < nwords; i += 64 * kClaimWaves) claimed[i] = 0;
+    for (uint32_t i = tid; i < kMaxApps * kMaxZones / 32; i += 64 * kClaimWaves) claimed_az[i] = 0;
+    // Staging, all waves: each pod's list sorted best-first (so that a pod's claim is the first
+    // still-available lane: one ballot instead of a 64-bit max reduction in the sequential loop)
+    // and, for zone-anti-affinity pods, the zones of its candidates.
+    // Wave wv takes pods wv + 16q (q < 4): all loads of a round are issued before any is used and
+    // the four sorts interleave.
+    {
+        constexpr int Q = 64 / kClaimWaves;
+        uint64_t ev[Q];
+        uint32_t fv[Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const uint32_t i = (uint32_t)wv + kClaimWaves * q;
+            ev[q] = i < nb ? lists[(size_t)i * GLp + lane] : 0ull;
+            fv[q] = i < nb ? bidx[i] : 0u;
+        }
+        uint32_t sv[Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            sv[q] = fv[q];
+            fv[q] = (uint32_t)wv + kClaimWaves * q < nb ? pods[sv[q]].flags : 0u;
+        }
+#pragma unroll
+        for (int q = 0; q < Q; ++q) ev[q] = wave_sort_desc(ev[q], lane);
+        uint32_t zv[Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q)
+            zv[q] = (ev[q] && pod_aa(fv[q]) == 2u) ? (uint32_t)t.zone[key_node(ev[q])] : 0u;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const uint32_t i = (uint32_t)wv + kClaimWaves * q;
+            if (i < nb) {
+                lkey[i * 64 + lane] = ev[q];
+                lzone[i * 64 + lane] = zv[q];
+                if (lane == 0) { lpod[i] = sv[q]; lpod[64 + i] = fv[q]; }
+            }
+        }
+    }
+    __syncthreads();
+    if (wv != 0) return;
+    CLAIM_STAMP(0);  // the claim walk and the apply step are one wave's work
+    int32_t my_node = -2;  // lane i: batch pod i's outcome (-2 carried, -1 unschedulable)
+    uint64_t my_key = 0;
+    uint32_t npend = 0;
+    // lane i holds batch pod i's stream position and flags (read with readlane in the walk)
+    const uint32_t my_s = (uint32_t)lane < nb ? lpod[lane] : 0u;
+    const uint32_t my_flags = (uint32_t)lane < nb ? lpod[64 + lane] : 0u;
+    CLAIM_STAMP(1);
+    // Software-pipelined walk.  Entering iteration i: pod i's entries (e, z) and its exact
+    // availability mask am (claims of pods < i), pod i+1's entries (e1, z1).  Pod i+1's bitmap
+    // words are read before pod i's claim is written (they see the claims of pods < i) and then
+    // patched with pod i's claim (node w; (app, zone) when both are zone-anti-affinity pods), so
+    // the LDS round trip overlaps pod i's scalar chain instead of following it.
+    auto lane_node = [](uint64_t v, bool ok) { return (ok && v) ? key_node(v) : 0u; };
+    uint64_t e = lkey[lane];
+    uint32_t z = lzone[lane] & (kMaxZones - 1);
+    uint32_t fl = (uint32_t)__builtin_amdgcn_readlane((int)my_flags, 0);
+    uint64_t am;
+    {
+        const uint32_t node = lane_node(e, true), azb = pod_app(fl) * kMaxZones + z;
+        const uint32_t taken = ((claimed[node >> 5] >> (node & 31)) |
+                                (pod_aa(fl) == 2u ? claimed_az[azb >> 5] >> (azb & 31) : 0u)) & 1u;
+        am = __ballot(e != 0ull && taken == 0u);
+    }
+    uint64_t e1 = lkey[min(1u, 63u) * 64 + lane];
+    uint32_t z1 = lzone[min(1u, 63u) * 64 + lane] & (kMaxZones - 1);
+    for (uint32_t i = 0; i < nb; ++i) {
+        const uint32_t aa = pod_aa(fl), app = pod_app(fl);
+        const bool has1 = i + 1 < nb;
+        const uint32_t fl1 = (uint32_t)__builtin_amdgcn_readlane((int)my_flags, (int)min(i + 1, 63u));
+        const uint32_t aa1 = pod_aa(fl1), app1 = pod_app(fl1);
+        // pod i+1: bitmap words (claims of pods < i) and pod i+2's entries, all in flight now
+        const uint32_t node1 = lane_node(e1, has1), azb1 = app1 * kMaxZones + z1;
+        const uint32_t cw1 = claimed[node1 >> 5], aw1 = claimed_az[azb1 >> 5];
+        const uint32_t j2 = min(i + 2, 63u);
+        const uint64_t e2 = lkey[j2 * 64 + lane];
+        const uint32_t z2 = lzone[j2 * 64 + lane] & (kMaxZones - 1);
+        // pod i
+        uint32_t w = 0xFFFFFFFFu, zw = 0xFFFFFFFFu;
+        if (am) {
+            const int src = __builtin_ctzll(am);
+            const uint64_t best = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(e >> 32), src) << 32) |
+                                  (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)e, src);
+            w = key_node(best);
+            zw = (uint32_t)__builtin_amdgcn_readlane((int)z, src);
+            const uint32_t b2 = app * kMaxZones + zw;
+            if (lane == 0) {
+                __hip_atomic_fetch_or(&claimed[w >> 5], 1u << (w & 31), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (aa == 2u)
+                    __hip_atomic_fetch_or(&claimed_az[b2 >> 5], 1u << (b2 & 31), __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            if ((uint32_t)lane == i) { my_node = (int32_t)w; my_key = best; }
+        } else if (__ballot(e != 0ull)) {
+            if (lane == 0) pend[npend] = (uint32_t)__builtin_amdgcn_readlane((int)my_s, (int)i);
+            ++npend;  // every candidate taken by an earlier pod: carried to the next batch
+        } else if ((uint32_t)lane == i) {
+            my_node = -1;  // no feasible node at all (spec S7: unschedulable)
+        }
+        // pod i+1's exact mask: bitmap words patched with pod i's claim
+        const bool az_hit = aa1 == 2u && aa == 2u && app1 == app && z1 == zw;
+        const uint32_t taken1 = ((cw1 >> (node1 & 31)) | (aa1 == 2u ? aw1 >> (azb1 & 31) : 0u)) & 1u;
+        am = __ballot(has1 && e1 != 0ull && taken1 == 0u && node1 != w && !az_hit);
+        e = e1;
+        z = z1;
+        fl = fl1;
+        e1 = e2;
+        z1 = z2;
+    }
+    CLAIM_STAMP(2);
+    // apply every claim (distinct nodes; counts of one (app, zone) may be shared: atomics)
+    if ((uint32_t)lane < nb && my_node != -2) {
+        const uint32_t s = my_s;
+        if (my_node >= 0) {
+            const DPod p = pods[s];
+            const uint32_t w = (uint32_t)my_node;
+            Row r = load_row(t, w);
+            RowX x = load_rowx<kFeatExt>(t, w);
+            reserve(r, x, p, +1);
+            store_dyn(t, w, r);
+            store_dynx<kFeatExt>(t, w, x);
+            if (t.apps) {
+                const uint32_t app = pod_app(p.flags);
+                atomicOr(&t.apps[(size_t)(app >> 5) * t.cap + w], 1u << (app & 31));
+                atomicAdd(&t.zcount[app * kMaxZones + (uint32_t)t.zone[w]], 1);
+            }
+        }
+        out_node[s] = my_node;
+        if (out_key) out_key[s] = my_key;
+    }
+    // next batch: carried pods first (queue order), then fresh pods from the stream.  bidx is
+    // rewritten only after every lane has read its entry above (single wave, program order).
+    const uint32_t take = min(B - npend, P - cursor);
+    if ((uint32_t)lane < npend) bidx[lane] = pend[lane];
+    else if ((uint32_t)lane < npend + take) bidx[lane] = cursor + (uint32_t)lane - npend;
+    if (lane == 0) { ctrl[0] = npend + take; ctrl[1] = cursor + take; }
+    CLAIM_STAMP(3);
+#ifdef QS_CLAIM_DIAG
+    if (lane == 0) {
+        for (int q = 0; q < 4; ++q) atomicAdd((unsigned long long *)&g_claim_diag[q], (unsigned long long)cds[q]);
+        const unsigned long long nbt = atomicAdd((unsigned long long *)&g_claim_diag[4], 1ull);
+        if (npend + take == 0)
+            printf("claim diag: batches %llu  stage %llu  setup %llu  walk %llu  apply %llu (clocks, totals)\n",
+                   nbt + 1, (unsigned long long)g_claim_diag[0], (unsigned long long)g_claim_diag[1],
+                   (unsigned long long)g_claim_diag[2], (unsigned long long)g_claim_diag[3]);
+    }
+#endif
+}
+
+hipError_t launch_batch_init(uint32_t *ctrl, uint32_t *bidx, uint32_t P, uint32_t B, hipStream_t stream) {
+    hipLaunchKernelGGL(k_batch_init, dim3(1), dim3(64), 0, stream, ctrl, bidx, P, B);
+    return hipGetLastError();
+}
+
+// Raises the claim kernel's dynamic-LDS limit to the CU's 160 KB; called once, outside capture.
+hipError_t batch_claim_prepare() {
+    static const hipError_t attr = hipFuncSetAttribute((const void *)k_batch_claim,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    return attr;
+}
+
+size_t batch_claim_lds(uint32_t n) {
+    return ((((size_t)n + 31) / 32 + 3) & ~(size_t)3) * 4 + kMaxApps * kMaxZones / 8 + 64 * 4 + 64 * 64 * (8 + 4) + 128 * 4;
+}
+
+hipError_t launch_batch_claim(const DevTable &t, const DPod *pods, const uint64_t *lists, uint32_t *ctrl,
+                              uint32_t *bidx, uint32_t P, uint32_t B, int32_t *on, uint64_t *ok,
+                              hipStream_t stream) {
+    const size_t lds = batch_claim_lds(t.n);
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_batch_claim, dim3(1), dim3(64 * kClaimWaves), lds, stream, t, pods, lists, 64u, ctrl, bidx, P, B,
+                       on, ok);
+    return hipGetLastError();
+}
+
+// =============================================================================================
 // small row kernels (qs_node_upsert / qs_reserve / qs_unreserve)
 // =============================================================================================
 __global__ void k_set_row(DevTable t, uint32_t i, HostRow v, uint32_t feat) {
@@ -1232,6 +1473,7 @@ __global__ void k_set_row(DevTable t, uint32_t i, HostRow v, uint32_t feat) {
 #pragma unroll
         for (int k = 0; k < kSCols; ++k) t.soa.c[k][i] = f[k];
     }
+    if (t.zone) t.zone[i] = v.zone;
 }
 
 // =============================================================================================
@@ -1370,7 +1612,7 @@ static hipError_t la_window_f(const DevTable &t, const DPod *pods, const DPodX *
     }
     if (part & 1) {
         switch (geo.E) {
-#define QS_SEL(EE) case EE: hipLaunchKernelGGL((k_la_select<256, EE, F>), grid, dim3(256), 0, stream, t, pods, podx, c, s0, P, sh, G, L, geo.chunk, GLp, bf.lists, bf.clists, bf.npart, K, bf.norm); break;
+#define QS_SEL(EE) case EE: hipLaunchKernelGGL((k_la_select<256, EE, F>), grid, dim3(256), 0, stream, t, pods, podx, c, s0, P, sh, G, L, geo.chunk, GLp, bf.lists, bf.clists, bf.npart, K, bf.norm, bf.pidx, bf.pcount); break;
             QS_SEL(1) QS_SEL(2) QS_SEL(3) QS_SEL(4) QS_SEL(5) QS_SEL(6) QS_SEL(8) QS_SEL(10) QS_SEL(12) QS_SEL(16)
 #undef QS_SEL
             default: return hipErrorInvalidValue;

@@ -17,6 +17,7 @@ struct HostRow {
     double yc, ym;
     int32_t ae0, re0, ae1, re1;
     uint64_t th, ts, lb0, lb1;
+    int32_t zone, pad;
 };
 
 // Lookahead geometry: window K pods, list length L (= K), G node chunks of `chunk` nodes per pod,
@@ -65,11 +66,23 @@ struct LaBufs {
     const uint32_t *dprev;
     uint32_t *dcur;
     unsigned long long *nfall;
+    // batched mode: the batch's stream positions and size on the device (nullptr: s0 + k, kw)
+    const uint32_t *pidx = nullptr, *pcount = nullptr;
 };
 hipError_t launch_la_window(const DevTable &t, const DPod *pods, const DPodX *podx, uint32_t s0,
                             uint32_t P, const DevCfg &c, const LaGeom &geo, const LaBufs &bufs,
                             int32_t *out_node, uint64_t *out_key, uint64_t *stamps, uint64_t *diag,
                             hipStream_t stream, int part);  // part: 4 norm, 1 select(+merge), 2 resolve
+
+// Batched mode (spec S11): ctrl = {pods in the current batch, stream cursor}, bidx = the batch's
+// stream positions.  init sets up the first batch; claim resolves one batch, applies its claims
+// and builds the next.
+hipError_t launch_batch_init(uint32_t *ctrl, uint32_t *bidx, uint32_t P, uint32_t B, hipStream_t stream);
+size_t batch_claim_lds(uint32_t n);
+hipError_t batch_claim_prepare();  // dynamic LDS of the claim kernel (<= 160 KB)
+hipError_t launch_batch_claim(const DevTable &t, const DPod *pods, const uint64_t *lists, uint32_t *ctrl,
+                              uint32_t *bidx, uint32_t P, uint32_t B, int32_t *out_node,
+                              uint64_t *out_key, hipStream_t stream);
 
 __global__ void k_set_row(DevTable t, uint32_t i, HostRow v, uint32_t feat);
 

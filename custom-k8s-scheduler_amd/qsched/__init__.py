@@ -18,7 +18,7 @@ import ctypes
 import numpy as np
 
 from ._abi import (ENGINES, ENGINE_NAMES, EXPORTED, LIB_PATH, POD_DTYPE, QS_ABI_VERSION,
-                   QS_MAX_EXT, QS_MAX_TERMS, QS_MODE_EXACT, QS_OK, QschedError,
+                   QS_MAX_EXT, QS_MAX_TERMS, QS_MODE_BATCHED, QS_MODE_EXACT, QS_OK, QschedError,
                    QschedLibraryMissing, QsConfig, QsContainer, QsNodeRow, QsNodeSoa, QsStats,
                    load)
 
@@ -26,6 +26,7 @@ __all__ = ["Scheduler", "Config", "POD_DTYPE", "pods_to_struct", "pods_from_stru
            "synth_generate", "dist_unique_id", "empty_nodes", "pod_from_containers", "compute_qos", "load",
            "QschedError", "QschedLibraryMissing", "ENGINES", "EXPORTED", "LIB_PATH"]
 
+MODES = {"exact": QS_MODE_EXACT, "batched": QS_MODE_BATCHED}
 NODE_I64 = ["alloc_cpu", "alloc_mem", "max_pods", "req_cpu", "req_mem", "nz_cpu", "nz_mem", "pods"]
 
 
@@ -49,6 +50,7 @@ def empty_nodes(n: int):
     d["taint_hard"] = np.zeros(n, np.uint64)
     d["taint_soft"] = np.zeros(n, np.uint64)
     d["label_bits"] = np.zeros((n, 2), np.uint64)
+    d["zone"] = np.zeros(n, np.int32)
     return d
 
 
@@ -57,7 +59,8 @@ def _soa(nodes, lib_out=False):
     for f, _ in QsNodeSoa._fields_:
         a = nodes.get(f)
         if a is not None:
-            want = np.uint64 if f in ("taint_hard", "taint_soft", "label_bits") else np.int64
+            want = (np.uint64 if f in ("taint_hard", "taint_soft", "label_bits") else
+                    np.int32 if f == "zone" else np.int64)
             if a.dtype != want or not a.flags["C_CONTIGUOUS"]:
                 if lib_out:
                     raise TypeError(f"output column {f} must be C-contiguous {want}")
@@ -197,11 +200,11 @@ class Scheduler:
         return dict(feasible=feas.astype(bool), scores=score, total=total, best=best.value)
 
     # ---- exact stream ----
-    def schedule(self, pods, with_stats=False):
+    def schedule(self, pods, with_stats=False, mode="exact"):
         arr = pods_to_struct(pods)
         placement = np.empty(len(arr), np.int32)
         stats = QsStats()
-        self._chk(self.lib.qs_schedule_stream(self.ctx, _ptr(arr), len(arr), QS_MODE_EXACT,
+        self._chk(self.lib.qs_schedule_stream(self.ctx, _ptr(arr), len(arr), MODES[mode],
                                               _ptr(placement), ctypes.byref(stats)))
         return (placement, stats.as_dict()) if with_stats else placement
 
@@ -219,9 +222,10 @@ class Stream:
         self.s, self.h, self.p = sched, handle, p
         self.stats = None
 
-    def run(self):
+    def run(self, mode="exact"):
+        """qs_stream_run: mode "exact" (spec S7/S8) or "batched" (spec S11)."""
         st = QsStats()
-        self.s._chk(self.s.lib.qs_stream_run(self.s.ctx, self.h, QS_MODE_EXACT, ctypes.byref(st)))
+        self.s._chk(self.s.lib.qs_stream_run(self.s.ctx, self.h, MODES[mode], ctypes.byref(st)))
         self.stats = st.as_dict()
         return self.stats
 

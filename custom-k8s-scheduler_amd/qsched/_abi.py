@@ -15,16 +15,19 @@ import numpy as np
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(PKG_ROOT, "libqsched.so")
 
-QS_ABI_VERSION = 1
+QS_ABI_VERSION = 2
 QS_MAX_EXT = 2
 QS_MAX_TERMS = 4
+QS_MAX_APPS = 1024
+QS_MAX_ZONES = 64
+QS_AA_NONE, QS_AA_HOSTNAME, QS_AA_ZONE = 0, 1, 2
 
 QS_OK, QS_EINVAL, QS_EDEVICE, QS_ETIMEOUT, QS_ENOMEM, QS_ESTATE = range(6)
 STATUS_NAMES = {0: "QS_OK", 1: "QS_EINVAL", 2: "QS_EDEVICE", 3: "QS_ETIMEOUT", 4: "QS_ENOMEM",
                 5: "QS_ESTATE"}
 QS_QOS_BESTEFFORT, QS_QOS_BURSTABLE, QS_QOS_GUARANTEED = 0, 1, 2
 QS_MODE_EXACT, QS_MODE_BATCHED = 0, 1
-ENGINES = {"auto": 0, "persistent": 1, "scan": 2, "lookahead": 3}
+ENGINES = {"auto": 0, "persistent": 1, "scan": 2, "lookahead": 3, "batched": 4}
 ENGINE_NAMES = {v: k for k, v in ENGINES.items()}
 
 
@@ -48,11 +51,12 @@ class QsConfig(ctypes.Structure):
                 ("lookahead", ctypes.c_int32), ("record_timestamps", ctypes.c_int32),
                 ("profile_kernels", ctypes.c_int32), ("virtual_shards", ctypes.c_int32),
                 ("lookahead_serial", ctypes.c_int32),
-                ("scan_soa_min_nodes", ctypes.c_int32), ("reserved", ctypes.c_int32 * 4)]
+                ("scan_soa_min_nodes", ctypes.c_int32), ("batch_pods", ctypes.c_int32),
+                ("reserved", ctypes.c_int32 * 3)]
 
 
 _NODE_COLS = ["alloc_cpu", "alloc_mem", "alloc_ext", "max_pods", "req_cpu", "req_mem", "req_ext",
-              "nz_cpu", "nz_mem", "pods", "taint_hard", "taint_soft", "label_bits"]
+              "nz_cpu", "nz_mem", "pods", "taint_hard", "taint_soft", "label_bits", "zone"]
 
 
 class QsNodeSoa(ctypes.Structure):
@@ -66,7 +70,8 @@ class QsNodeRow(ctypes.Structure):
                 ("req_ext", ctypes.c_int64 * QS_MAX_EXT), ("nz_cpu", ctypes.c_int64),
                 ("nz_mem", ctypes.c_int64), ("pods", ctypes.c_int64),
                 ("taint_hard", ctypes.c_uint64), ("taint_soft", ctypes.c_uint64),
-                ("label_bits", ctypes.c_uint64 * 2)]
+                ("label_bits", ctypes.c_uint64 * 2), ("zone", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
 
 
 class QsContainer(ctypes.Structure):
@@ -98,14 +103,14 @@ class QsStats(ctypes.Structure):
         return d
 
 
-# qs_pod as a numpy structured dtype (C layout, 240 bytes)
+# qs_pod as a numpy structured dtype (C layout, 248 bytes)
 POD_DTYPE = np.dtype([
     ("req_cpu", "<i8"), ("req_mem", "<i8"), ("req_ext", "<i8", (QS_MAX_EXT,)),
     ("nz_cpu", "<i8"), ("nz_mem", "<i8"), ("qos", "<i4"), ("priority", "<i4"),
     ("tol_hard", "<u8"), ("tol_soft", "<u8"), ("sel", "<u8", (2,)),
     ("n_req_terms", "<i4"), ("n_pref_terms", "<i4"),
     ("req_terms", "<u8", (QS_MAX_TERMS, 2)), ("pref_terms", "<u8", (QS_MAX_TERMS, 2)),
-    ("pref_weight", "<i4", (QS_MAX_TERMS,)),
+    ("pref_weight", "<i4", (QS_MAX_TERMS,)), ("app", "<i4"), ("anti_affinity", "<i4"),
 ], align=True)
 
 _P = ctypes.c_void_p

@@ -41,9 +41,11 @@ extern "C" {
 #define QS_API
 #endif
 
-#define QS_ABI_VERSION 1
+#define QS_ABI_VERSION 2
 #define QS_MAX_EXT 2   /* extended resources per node/pod (e.g. amd.com/gpu) */
 #define QS_MAX_TERMS 4 /* node-affinity terms per pod (required OR-terms, preferred terms) */
+#define QS_MAX_APPS 1024 /* anti-affinity groups (batched mode, spec S11) */
+#define QS_MAX_ZONES 64  /* topology zones (batched mode zone anti-affinity) */
 
 typedef enum qs_status {
     QS_OK = 0,
@@ -58,12 +60,17 @@ typedef enum qs_qos { QS_QOS_BESTEFFORT = 0, QS_QOS_BURSTABLE = 1, QS_QOS_GUARAN
 
 typedef enum qs_mode { QS_MODE_EXACT = 0, QS_MODE_BATCHED = 1 } qs_mode;
 
+/* Required pod anti-affinity to the pod's own app group (batched mode, spec S11; the subset of
+ * UP plugins/interpodaffinity that config 5 uses): none, per node (topologyKey hostname), per zone. */
+typedef enum qs_anti_affinity { QS_AA_NONE = 0, QS_AA_HOSTNAME = 1, QS_AA_ZONE = 2 } qs_anti_affinity;
+
 /* Which device engine runs the exact stream (all are bit-exact; AUTO picks the fastest). */
 typedef enum qs_engine {
     QS_ENGINE_AUTO = 0,
     QS_ENGINE_PERSISTENT = 1, /* one resident workgroup, node rows in registers (N <= 8192) */
     QS_ENGINE_SCAN = 2,       /* per-pod grid scan + finalize/reserve launch chain (any N) */
-    QS_ENGINE_LOOKAHEAD = 3   /* exact top-K lookahead: chip-wide stale scan + sequential resolve */
+    QS_ENGINE_LOOKAHEAD = 3,  /* exact top-K lookahead: chip-wide stale scan + sequential resolve */
+    QS_ENGINE_BATCHED = 4     /* reported by qs_stats.engine_used for QS_MODE_BATCHED streams */
 } qs_engine;
 
 typedef struct qs_config {
@@ -89,15 +96,18 @@ typedef struct qs_config {
                                     window w+1 overlaps the resolve of window w (needs lookahead <= 32) */
     int32_t scan_soa_min_nodes;  /* tables with at least this many nodes also keep the column-major
                                     copy the SCAN engine / qs_score_pod stream (0 = 65,536; -1 never) */
-    int32_t reserved[4];
+    int32_t batch_pods;          /* QS_MODE_BATCHED: pods per batch (0 = 64; at most 64) */
+    int32_t reserved[3];
 } qs_config;
 
 /* Canonical node table, structure of arrays, n entries each.  alloc_ext/req_ext are [n][QS_MAX_EXT],
- * label_bits is [n][2].  Optional columns may be NULL (read as 0). */
+ * label_bits is [n][2], zone is the node's topology zone id (< QS_MAX_ZONES; batched-mode zone
+ * anti-affinity).  Optional columns may be NULL (read as 0). */
 typedef struct qs_node_soa {
     const int64_t *alloc_cpu, *alloc_mem, *alloc_ext, *max_pods;
     const int64_t *req_cpu, *req_mem, *req_ext, *nz_cpu, *nz_mem, *pods;
     const uint64_t *taint_hard, *taint_soft, *label_bits;
+    const int32_t *zone;
 } qs_node_soa;
 
 /* Same layout, writable (qs_nodes_read, qs_synth_generate). */
@@ -105,12 +115,14 @@ typedef struct qs_node_soa_out {
     int64_t *alloc_cpu, *alloc_mem, *alloc_ext, *max_pods;
     int64_t *req_cpu, *req_mem, *req_ext, *nz_cpu, *nz_mem, *pods;
     uint64_t *taint_hard, *taint_soft, *label_bits;
+    int32_t *zone;
 } qs_node_soa_out;
 
 typedef struct qs_node_row {
     int64_t alloc_cpu, alloc_mem, alloc_ext[QS_MAX_EXT], max_pods;
     int64_t req_cpu, req_mem, req_ext[QS_MAX_EXT], nz_cpu, nz_mem, pods;
     uint64_t taint_hard, taint_soft, label_bits[2];
+    int32_t zone, reserved;
 } qs_node_row;
 
 /* One pod, precomputed on the host (spec S2/S3; qs_pod_from_containers helps). */
@@ -126,6 +138,8 @@ typedef struct qs_pod {
     uint64_t req_terms[QS_MAX_TERMS][2];  /* required node-affinity terms (OR of ANDs) */
     uint64_t pref_terms[QS_MAX_TERMS][2]; /* preferred terms */
     int32_t pref_weight[QS_MAX_TERMS];
+    int32_t app;           /* anti-affinity group (< QS_MAX_APPS) */
+    int32_t anti_affinity; /* qs_anti_affinity: required anti-affinity to the pod's own app */
 } qs_pod;
 
 /* One container of a pod spec for qs_pod_from_containers (spec S2/S3). has_* = 0 means missing. */

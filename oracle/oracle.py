@@ -50,6 +50,7 @@ def empty_cluster(n: int, p: int):
     nodes["taint_hard"] = np.zeros(n, np.uint64)
     nodes["taint_soft"] = np.zeros(n, np.uint64)
     nodes["label_bits"] = np.zeros((n, 2), np.uint64)
+    nodes["zone"] = np.zeros(n, np.int32)
     pods = {f: np.zeros(p, np.int64) for f in POD_FIELDS_I64}
     pods["req_ext"] = np.zeros((p, MAX_EXT), np.int64)
     pods["qos"] = np.zeros(p, np.int32)
@@ -62,6 +63,8 @@ def empty_cluster(n: int, p: int):
     pods["req_terms"] = np.zeros((p, MAX_TERMS, 2), np.uint64)
     pods["pref_terms"] = np.zeros((p, MAX_TERMS, 2), np.uint64)
     pods["pref_weight"] = np.zeros((p, MAX_TERMS), np.int32)
+    pods["app"] = np.zeros(p, np.int32)
+    pods["anti_affinity"] = np.zeros(p, np.int32)
     return nodes, pods
 
 
@@ -75,14 +78,14 @@ def copy_cluster(nodes, pods):
 class _Nodes(ctypes.Structure):
     _fields_ = [("n", ctypes.c_uint32)] + [(f, ctypes.c_void_p) for f in
                ["alloc_cpu", "alloc_mem", "alloc_ext", "max_pods", "req_cpu", "req_mem", "req_ext",
-                "nz_cpu", "nz_mem", "pods", "taint_hard", "taint_soft", "label_bits"]]
+                "nz_cpu", "nz_mem", "pods", "taint_hard", "taint_soft", "label_bits", "zone"]]
 
 
 class _Pods(ctypes.Structure):
     _fields_ = [("p", ctypes.c_uint32)] + [(f, ctypes.c_void_p) for f in
                ["req_cpu", "req_mem", "req_ext", "nz_cpu", "nz_mem", "qos", "priority", "tol_hard",
                 "tol_soft", "sel", "n_req_terms", "n_pref_terms", "req_terms", "pref_terms",
-                "pref_weight"]]
+                "pref_weight", "app", "anti_affinity"]]
 
 
 class _Config(ctypes.Structure):
@@ -118,6 +121,8 @@ def lib():
         L.or_score_pod.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint32] + [ctypes.c_void_p] * 2
         L.or_reserve.restype = None
         L.or_reserve.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_uint32] * 2 + [ctypes.c_int]
+        L.or_schedule_batched.restype = ctypes.c_uint32
+        L.or_schedule_batched.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint32] + [ctypes.c_void_p] * 2 + [ctypes.c_int]
         L.or_generate.restype = None
         L.or_generate.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
         _LIB = L
@@ -179,6 +184,18 @@ def schedule(nodes, pods, cfg=None, nthreads=1):
     lib().or_schedule(ctypes.byref(sc), ctypes.byref(sn), ctypes.byref(sp), _ptr(placement),
                       _ptr(best), _ptr(order), ctypes.c_int(nthreads))
     return placement, best, order
+
+
+def schedule_batched(nodes, pods, batch=64, cfg=None, nthreads=1):
+    """Batched mode (spec S11).  Mutates ``nodes``.  Returns (placement[p], key[p], batches)."""
+    p = len(pods["req_cpu"])
+    placement = np.full(p, -3, np.int32)
+    best = np.zeros(p, np.uint64)
+    sn, sp, sc = _mk_nodes(nodes), _mk_pods(pods), _mk_cfg(cfg)
+    nb = lib().or_schedule_batched(ctypes.byref(sc), ctypes.byref(sn), ctypes.byref(sp),
+                                   ctypes.c_uint32(batch), _ptr(placement), _ptr(best),
+                                   ctypes.c_int(nthreads))
+    return placement, best, int(nb)
 
 
 def score_pod(nodes, pods, j, cfg=None):
@@ -372,7 +389,9 @@ def py_generate(config: int, n: int, p: int, seed: int | None = None):
     nodes["alloc_cpu"][:] = cpu
     nodes["alloc_mem"][:] = (cpu // 1000) * mpc * GIB
     nodes["max_pods"][:] = 110
-    c4 = config == 4
+    c4, c5 = config == 4, config == 5
+    if c4 or c5:
+        nodes["zone"][:] = _pick(seed, i + np.uint64(4), 10).astype(np.int32)
     if c4:
         gpu = _pick(seed, i + np.uint64(2), 10) == 0
         maint = _pick(seed, i + np.uint64(3), 20) == 0
@@ -402,6 +421,11 @@ def py_generate(config: int, n: int, p: int, seed: int | None = None):
     has_mem = (q == 2) | ((q == 1) & (memmode != 0))
     pods["req_mem"][:] = np.where(has_mem, mem, 0)
     pods["nz_mem"][:] = np.where(has_mem, mem, DEF_MEM)
+    if c5:  # spec/synth.md G5
+        app = _pick(seed, j + np.uint64(13), 1000)
+        kind = _pick(seed, np.uint64(8 * n + 16 * p) + app.astype(np.uint64), 10)
+        pods["app"][:] = app.astype(np.int32)
+        pods["anti_affinity"][:] = np.where(kind < 5, 1, np.where(kind == 5, 2, 0)).astype(np.int32)
     if c4:
         pairs = [(a, b) for a in range(10) for b in range(a + 1, 10)]
         gpu = _pick(seed, j + np.uint64(5), 20) == 0

@@ -246,6 +246,124 @@ void or_schedule(const or_config *cfg, or_nodes *nd, const or_pods *pd, int32_t 
     free(order);
 }
 
+/* ---------------- spec S11: batched mode ---------------- */
+#define OR_LIST 64
+#define OR_APPS 1024
+#define OR_ZONES 64
+
+static int cmp_key_desc(const void *a, const void *b) {
+    uint64_t x = *(const uint64_t *)a, y = *(const uint64_t *)b;
+    return x < y ? 1 : (x > y ? -1 : 0);
+}
+
+/* required anti-affinity of pod j against node n (UP plugins/interpodaffinity, the config-5
+ * subset: a term selecting the pod's own app, topologyKey hostname or zone) */
+static int aa_ok(const or_pods *pd, uint32_t j, uint32_t n, const uint8_t *present,
+                 const int32_t *zcount, const or_nodes *nd) {
+    int32_t app = pd->app[j], aa = pd->anti_affinity[j];
+    if (aa == 1) return !present[(size_t)app * nd->n + n];
+    if (aa == 2) return zcount[app * OR_ZONES + nd->zone[n]] == 0;
+    return 1;
+}
+
+uint32_t or_schedule_batched(const or_config *cfg, or_nodes *nd, const or_pods *pd, uint32_t batch,
+                             int32_t *placement, uint64_t *best_key, int nthreads) {
+    uint32_t P = pd->p, N = nd->n;
+    if (batch == 0 || batch > OR_LIST) batch = OR_LIST;
+    if (nthreads < 1) nthreads = 1;
+    uint32_t *order = (uint32_t *)malloc(sizeof(uint32_t) * (P ? P : 1));
+    order_pods(cfg, pd, order);
+    uint8_t *present = (uint8_t *)calloc((size_t)OR_APPS * (N ? N : 1), 1);
+    int32_t *zcount = (int32_t *)calloc((size_t)OR_APPS * OR_ZONES, sizeof(int32_t));
+    uint8_t *claimed = (uint8_t *)calloc(N ? N : 1, 1);
+    uint8_t *claimed_az = (uint8_t *)calloc((size_t)OR_APPS * OR_ZONES, 1);
+    uint64_t *keys = (uint64_t *)malloc(sizeof(uint64_t) * (N ? N : 1));
+    uint64_t(*lists)[OR_LIST] = malloc(sizeof(uint64_t) * OR_LIST * batch);
+    uint32_t cur[OR_LIST], pend[OR_LIST], nb = 0, npend = 0, cursor = 0, batches = 0;
+    int32_t won[OR_LIST];
+    nb = P < batch ? P : batch;
+    for (uint32_t i = 0; i < nb; i++) cur[i] = i;
+    cursor = nb;
+    while (nb > 0) {
+        ++batches;
+        /* each pod's 64 best keys against the batch-start state */
+        for (uint32_t i = 0; i < nb; i++) {
+            uint32_t j = order[cur[i]];
+            int64_t n_ = N;
+#pragma omp parallel for num_threads(nthreads) if (nthreads > 1)
+            for (int64_t n = 0; n < n_; n++) {
+                uint64_t k = node_key(cfg, nd, pd, (uint32_t)n, j, 0, 0, NULL);
+                keys[n] = (k && aa_ok(pd, j, (uint32_t)n, present, zcount, nd)) ? k : 0;
+            }
+            /* the 64 largest keys (keys are unique): a bounded selection, then sorted */
+            uint64_t top[OR_LIST];
+            uint32_t nt = 0;
+            for (uint32_t n = 0; n < N; n++) {
+                uint64_t k = keys[n];
+                if (!k) continue;
+                if (nt < OR_LIST) { top[nt++] = k; continue; }
+                uint32_t mi = 0;
+                for (uint32_t t = 1; t < OR_LIST; t++) if (top[t] < top[mi]) mi = t;
+                if (k > top[mi]) top[mi] = k;
+            }
+            qsort(top, nt, sizeof(uint64_t), cmp_key_desc);
+            for (uint32_t t = 0; t < OR_LIST; t++) lists[i][t] = t < nt ? top[t] : 0;
+        }
+        /* claims in batch order */
+        memset(claimed, 0, N ? N : 1);
+        memset(claimed_az, 0, (size_t)OR_APPS * OR_ZONES);
+        npend = 0;
+        for (uint32_t i = 0; i < nb; i++) {
+            uint32_t j = order[cur[i]];
+            uint64_t best = 0;
+            int any = 0;
+            for (uint32_t t = 0; t < OR_LIST; t++) {
+                uint64_t k = lists[i][t];
+                if (!k) continue;
+                any = 1;
+                uint32_t n = 0xFFFFFFFFu - (uint32_t)(k & 0xFFFFFFFFu);
+                if (claimed[n]) continue;
+                if (pd->anti_affinity[j] == 2 && claimed_az[pd->app[j] * OR_ZONES + nd->zone[n]]) continue;
+                if (k > best) best = k;
+            }
+            won[i] = -2;
+            if (best) {
+                uint32_t n = 0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFu);
+                claimed[n] = 1;
+                if (pd->anti_affinity[j] == 2) claimed_az[pd->app[j] * OR_ZONES + nd->zone[n]] = 1;
+                won[i] = (int32_t)n;
+                if (best_key) best_key[j] = best;
+            } else if (any) {
+                pend[npend++] = cur[i];
+            } else {
+                won[i] = -1;
+                if (best_key) best_key[j] = 0;
+            }
+        }
+        /* apply the batch */
+        for (uint32_t i = 0; i < nb; i++) {
+            uint32_t j = order[cur[i]];
+            if (won[i] == -2) continue;
+            placement[j] = won[i];
+            if (won[i] >= 0) {
+                uint32_t n = (uint32_t)won[i];
+                or_reserve(nd, pd, j, n, +1);
+                present[(size_t)pd->app[j] * N + n] = 1;
+                zcount[pd->app[j] * OR_ZONES + nd->zone[n]]++;
+            }
+        }
+        /* next batch: carried pods first, then fresh ones */
+        uint32_t take = batch - npend;
+        if (take > P - cursor) take = P - cursor;
+        for (uint32_t i = 0; i < npend; i++) cur[i] = pend[i];
+        for (uint32_t i = 0; i < take; i++) cur[npend + i] = cursor + i;
+        nb = npend + take;
+        cursor += take;
+    }
+    free(order); free(present); free(zcount); free(claimed); free(claimed_az); free(keys); free(lists);
+    return batches;
+}
+
 /* ---------------- spec/synth.md generator (independent restatement) ---------------- */
 static uint64_t sm_at(uint64_t seed, uint64_t c) {
     uint64_t z = seed + (c + 1) * 0x9E3779B97F4A7C15ULL;
@@ -273,7 +391,7 @@ static int pair_bit(int za, int zb) { /* za < zb, lexicographic index of the pai
 
 void or_generate(int config, uint64_t seed, or_nodes *nd, or_pods *pd) {
     uint32_t N = nd->n, P = pd->p;
-    int c4 = (config == 4);
+    int c4 = (config == 4), c5 = (config == 5);
     for (uint32_t i = 0; i < N; i++) {
         uint64_t c = 8ULL * i;
         int64_t cpu = NODE_CPU[pick(seed, c + 0, 6)];
@@ -285,6 +403,7 @@ void or_generate(int config, uint64_t seed, or_nodes *nd, or_pods *pd) {
         for (int k = 0; k < OR_MAX_EXT; k++) nd->alloc_ext[i * OR_MAX_EXT + k] = nd->req_ext[i * OR_MAX_EXT + k] = 0;
         nd->taint_hard[i] = nd->taint_soft[i] = 0;
         nd->label_bits[2 * i] = nd->label_bits[2 * i + 1] = 0;
+        if (nd->zone) nd->zone[i] = (c4 || c5) ? (int32_t)pick(seed, c + 4, 10) : 0;
         if (c4) {
             int gpu = pick(seed, c + 2, 10) == 0;
             int maint = pick(seed, c + 3, 20) == 0;
@@ -320,6 +439,15 @@ void or_generate(int config, uint64_t seed, or_nodes *nd, or_pods *pd) {
         else if (q == 1) { rc = zc = cpu; if (memmode != 0) { rm = zm = mem; } }
         pd->req_cpu[j] = rc; pd->req_mem[j] = rm; pd->nz_cpu[j] = zc; pd->nz_mem[j] = zm;
         pd->qos[j] = q; pd->priority[j] = 0;
+        if (pd->app) {
+            pd->app[j] = 0;
+            pd->anti_affinity[j] = 0;
+            if (c5) { /* spec/synth.md G5 */
+                pd->app[j] = (int32_t)pick(seed, c + 13, 1000);
+                uint32_t kind = pick(seed, 8ULL * N + 16ULL * P + (uint64_t)pd->app[j], 10);
+                pd->anti_affinity[j] = kind < 5 ? 1 : (kind == 5 ? 2 : 0);
+            }
+        }
         for (int k = 0; k < OR_MAX_EXT; k++) pd->req_ext[j * OR_MAX_EXT + k] = 0;
         pd->tol_hard[j] = pd->tol_soft[j] = 0;
         pd->sel[2 * j] = pd->sel[2 * j + 1] = 0;

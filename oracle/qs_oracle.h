@@ -25,6 +25,7 @@ typedef struct {
     int64_t *alloc_cpu, *alloc_mem, *alloc_ext /* [n*OR_MAX_EXT] */, *max_pods;
     int64_t *req_cpu, *req_mem, *req_ext /* [n*OR_MAX_EXT] */, *nz_cpu, *nz_mem, *pods;
     uint64_t *taint_hard, *taint_soft, *label_bits /* [n*2] */;
+    int32_t *zone; /* topology zone id (< 64), batched-mode zone anti-affinity */
 } or_nodes; /* mutable: or_schedule applies Reserve in place */
 
 typedef struct {
@@ -35,6 +36,7 @@ typedef struct {
     int32_t *n_req_terms, *n_pref_terms;
     uint64_t *req_terms /* [p*OR_MAX_TERMS*2] */, *pref_terms /* [p*OR_MAX_TERMS*2] */;
     int32_t *pref_weight /* [p*OR_MAX_TERMS] */;
+    int32_t *app, *anti_affinity; /* spec S11: group < 1024; 0 none, 1 hostname, 2 zone */
 } or_pods;
 
 typedef struct {
@@ -55,6 +57,15 @@ void or_score_pod(const or_config *cfg, const or_nodes *nodes, const or_pods *po
  * nthreads > 1 parallelises the node scan of each pod (upstream Parallelizer analogue). */
 void or_schedule(const or_config *cfg, or_nodes *nodes, const or_pods *pods, int32_t *placement,
                  uint64_t *best_key, uint32_t *order_out, int nthreads);
+
+/* Batched mode (spec S11): batches of `batch` (<= 64) pods; each pod's 64 best keys against the
+ * batch-start table (required anti-affinity to its app per hostname / zone included), claims in
+ * batch order (best key whose node, and for zone anti-affinity whose (app, zone), no earlier pod of
+ * the batch claimed), all claims applied after the batch, pods with every candidate claimed carried
+ * to the front of the next batch.  placement[j] by arrival position; best_key[j] = the claimed key
+ * (0 if unschedulable).  Returns the number of batches.  Profile: Fit + Balanced (+ ext). */
+uint32_t or_schedule_batched(const or_config *cfg, or_nodes *nodes, const or_pods *pods,
+                             uint32_t batch, int32_t *placement, uint64_t *best_key, int nthreads);
 
 /* Reserve / Unreserve of pod j on node n (spec S7). */
 void or_reserve(or_nodes *nodes, const or_pods *pods, uint32_t j, uint32_t n, int sign);

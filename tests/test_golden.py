@@ -20,6 +20,8 @@ def _digest(nodes, pods):
     h = hashlib.sha256()
     for d in (nodes, pods):
         for k in sorted(d):
+            if k in ("zone", "app", "anti_affinity"):  # ABI v2 columns, after the fixtures
+                continue
             h.update(k.encode())
             h.update(np.ascontiguousarray(d[k]).tobytes())
     return h.hexdigest()

@@ -74,7 +74,7 @@ def test_openmp_arm_matches_sequential():
     assert np.array_equal(pa, pb) and np.array_equal(ka, kb)
 
 
-@pytest.mark.parametrize("config,n,p", [(1, 100, 1000), (2, 300, 2000), (4, 300, 3000)])
+@pytest.mark.parametrize("config,n,p", [(1, 100, 1000), (2, 300, 2000), (4, 300, 3000), (5, 400, 3000)])
 def test_generators_agree(config, n, p):
     import qsched
     a_nodes, a_pods = O.generate(config, n, p)

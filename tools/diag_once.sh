@@ -1,7 +1,4 @@
 set -e
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
-tail -3 gpurun_out/pytest_gpu.log
-timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()"
-timeout -k 10 400 python -u bench.py > gpurun_out/bench.log 2>&1 || { tail -20 gpurun_out/bench.log; exit 1; }
-cat gpurun_out/bench.log
+timeout -k 10 400 python -u -m pytest tests/test_gpu_batched.py -x -q --timeout 300 --timeout-method thread 2>&1 | grep -v "claim diag" | tail -3
+MODE=batched CFG=5 N=10000 P=200000 timeout -k 10 120 python tools/kprof.py 2>&1
