@@ -255,12 +255,9 @@ __device__ __forceinline__ double fraction(int32_t a, int32_t r, double y) {
 }
 
 // ---- spec S5/S6: QoS-weighted total of one feasible node ------------------------------------
-template <uint32_t F>
-__device__ __forceinline__ uint32_t node_total(const Row &r, const RowX &x, const DPod &p,
-                                               const DPodX &px, const DevCfg &c, uint32_t mt,
-                                               double ymt, uint32_t ma, double yma, uint32_t *sc) {
-    // LeastAllocated (UP least_allocated.go#leastResourceScorer), NonZeroRequested + pod nz.
-    // Branch-free: a resource with alloc == 0 contributes weight 0 (its score is 0 as well).
+// LeastAllocated (UP least_allocated.go#leastResourceScorer), NonZeroRequested + pod nz.
+// Branch-free: a resource with alloc == 0 contributes weight 0 (its score is 0 as well).
+__device__ __forceinline__ uint32_t la_score(const Row &r, const DPod &p, const DevCfg &c) {
     const bool hc = r.ac != 0, hm = r.am != 0;
     const uint32_t sc_c = least_requested(r.ac, r.zc + p.zc, r.yc);
     const uint32_t sc_m = least_requested(r.am, r.zm + p.zm, r.ym);
@@ -274,8 +271,11 @@ __device__ __forceinline__ uint32_t node_total(const Row &r, const RowX &x, cons
     const double yd = __builtin_bit_cast(
         double, (__builtin_bit_cast(uint64_t, c.yd_both) & mb) |
                     (__builtin_bit_cast(uint64_t, c.yd_c) & mc) | (__builtin_bit_cast(uint64_t, c.yd_m) & mm));
-    const uint32_t la = den ? floor_div(num, yd) : 0u;
-    // BalancedAllocation (UP balanced_allocation.go#balancedResourceScorer), Requested + pod req
+    return den ? floor_div(num, yd) : 0u;
+}
+// BalancedAllocation (UP balanced_allocation.go#balancedResourceScorer), Requested + pod req
+__device__ __forceinline__ uint32_t ba_score(const Row &r, const DPod &p, const DevCfg &c) {
+    const bool hc = r.ac != 0, hm = r.am != 0;
     const double f0 = fraction(r.ac, r.rc + p.rc, r.yc);
     const double f1 = fraction(r.am, r.rm + p.rm, r.ym);
     double sd = 0.0;
@@ -283,6 +283,14 @@ __device__ __forceinline__ uint32_t node_total(const Row &r, const RowX &x, cons
     const double scaled = (1 - sd) * 100.0;
     uint32_t ba = (uint32_t)(int32_t)scaled;  // int64() truncation toward zero
     if (c.ba_skip_be && (p.flags & 3u) == 0) ba = 0;
+    return ba;
+}
+
+template <uint32_t F>
+__device__ __forceinline__ uint32_t node_total(const Row &r, const RowX &x, const DPod &p,
+                                               const DPodX &px, const DevCfg &c, uint32_t mt,
+                                               double ymt, uint32_t ma, double yma, uint32_t *sc) {
+    const uint32_t la = la_score(r, p, c), ba = ba_score(r, p, c);
     uint32_t total = __umul24((uint32_t)p.wfit, la) + __umul24((uint32_t)p.wbal, ba);
     uint32_t tt = 0, na = 0;
     if (F & kFeatTaint) {  // reverse DefaultNormalizeScore (UP helper/normalize_score.go)

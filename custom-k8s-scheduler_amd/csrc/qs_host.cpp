@@ -1008,13 +1008,15 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                             nwin, (int)overlap);
                 if (diag_on) {
                     uint64_t h[8] = {0};
-                    HIPCHK(hipMemcpyAsync(h, diag, 48, hipMemcpyDeviceToHost, c->stream));
+                    HIPCHK(hipMemcpyAsync(h, diag, 64, hipMemcpyDeviceToHost, c->stream));
                     HIPCHK(hipStreamSynchronize(c->stream));
                     const double np = h[5] ? (double)h[5] : 1.0;
                     fprintf(stderr, geo.waves == 1 ? "QS_DIAG resolve cycles/pod: cand %.0f issue %.0f fresh %.0f wmax %.0f commit %.0f (pods %llu, G=%u E=%u epl=%u)\n"
-                                                   : "QS_DIAG resolve4 busy cycles/pod: D %.0f A %.0f B %.0f C %.0f (-) %.0f (pods %llu, G=%u E=%u epl=%u)\n",
+                                                   : "QS_DIAG resolve4 busy cycles/pod: D %.0f A %.0f B %.0f C %.0f (C row wait %.0f) (pods %llu, G=%u E=%u epl=%u)\n",
                             h[0] / np, h[1] / np, h[2] / np, h[3] / np, h[4] / np,
                             (unsigned long long)h[5], geo.G, geo.E, geo.epl);
+                    if (geo.waves == 4)
+                        fprintf(stderr, "QS_DIAG resolve4 pre-score cycles/pod: A %.0f C %.0f\n", h[6] / np, h[7] / np);
                 }
             }
         }

@@ -397,11 +397,11 @@ struct SelBlock {
     uint32_t vs, v, k, g, start, end;
 };
 __device__ __forceinline__ SelBlock sel_block(const DevTable &t, const LaShard &sh, uint32_t G,
-                                              uint32_t chunk) {
+                                              uint32_t chunk, uint32_t bid) {
     SelBlock b;
     const uint32_t per = sh.kw * G;
-    b.vs = blockIdx.x / per;
-    const uint32_t rem = blockIdx.x % per;
+    b.vs = bid / per;
+    const uint32_t rem = bid % per;
     b.v = sh.v0 + b.vs;
     b.k = rem / G;
     b.g = rem % G;
@@ -422,7 +422,7 @@ __global__ __launch_bounds__(BS) void k_la_norm(DevTable t, const DPod *__restri
                                                 uint32_t chunk, uint4 *__restrict__ npart) {
     constexpr int NW = BS / kWave;
     __shared__ uint32_t red[4][NW];
-    const SelBlock b = sel_block(t, sh, G, chunk);
+    const SelBlock b = sel_block(t, sh, G, chunk, blockIdx.x);
     const uint32_t s = s0 + b.k;
     if (s >= P) return;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -490,17 +490,17 @@ __device__ __forceinline__ NormInfo norm_reduce(const uint4 *__restrict__ npart,
 // first combine the k_la_norm partials (uniform per pod: scalar loads) and block (0, k, 0) of
 // this process publishes the pod's NormInfo for the resolver.
 template <int BS, int E, uint32_t F>
-__global__ __launch_bounds__(BS) void k_la_select(DevTable t, const DPod *__restrict__ pods,
-                                                  const DPodX *__restrict__ podx, DevCfg c,
-                                                  uint32_t s0, uint32_t P, LaShard sh,
-                                                  uint32_t G, uint32_t L, uint32_t chunk,
-                                                  uint32_t GLp, uint64_t *__restrict__ lists,
-                                                  uint64_t *__restrict__ clists,
-                                                  const uint4 *__restrict__ npart, uint32_t K,
-                                                  NormInfo *__restrict__ norm_out,
-                                                  const uint32_t *__restrict__ pidx,
-                                                  const uint32_t *__restrict__ pcount) {
-    const SelBlock b = sel_block(t, sh, G, chunk);
+__device__ __forceinline__ void la_select_block(uint32_t bid, const DevTable &t, const DPod *__restrict__ pods,
+                                                const DPodX *__restrict__ podx, const DevCfg &c,
+                                                uint32_t s0, uint32_t P, const LaShard &sh,
+                                                uint32_t G, uint32_t L, uint32_t chunk,
+                                                uint32_t GLp, uint64_t *__restrict__ lists,
+                                                uint64_t *__restrict__ clists,
+                                                const uint4 *__restrict__ npart, uint32_t K,
+                                                NormInfo *__restrict__ norm_out,
+                                                const uint32_t *__restrict__ pidx,
+                                                const uint32_t *__restrict__ pcount) {
+    const SelBlock b = sel_block(t, sh, G, chunk, bid);
     uint32_t s;
     if (pidx) {  // batched mode: the batch's stream positions and size live on the device
         if (b.k >= *pcount) return;
@@ -539,14 +539,29 @@ __global__ __launch_bounds__(BS) void k_la_select(DevTable t, const DPod *__rest
     block_topl<BS, E>(tv, L, out, [&](int j) { return pack_key(tv[j], base + j * kWave); });
 }
 
+template <int BS, int E, uint32_t F>
+__global__ __launch_bounds__(BS) void k_la_select(DevTable t, const DPod *__restrict__ pods,
+                                                  const DPodX *__restrict__ podx, DevCfg c,
+                                                  uint32_t s0, uint32_t P, LaShard sh,
+                                                  uint32_t G, uint32_t L, uint32_t chunk,
+                                                  uint32_t GLp, uint64_t *__restrict__ lists,
+                                                  uint64_t *__restrict__ clists,
+                                                  const uint4 *__restrict__ npart, uint32_t K,
+                                                  NormInfo *__restrict__ norm_out,
+                                                  const uint32_t *__restrict__ pidx,
+                                                  const uint32_t *__restrict__ pcount) {
+    la_select_block<BS, E, F>(blockIdx.x, t, pods, podx, c, s0, P, sh, G, L, chunk, GLp, lists, clists,
+                              npart, K, norm_out, pidx, pcount);
+}
+
 // Grid: shards × pods.  Reduces a pod's G chunk lists (M = G*L keys, chunk-major: equal totals
 // sit in node-index order) to its top-L in the final [W][K][GLp] lists the resolver reads, so the
 // resolver scans L keys per pod instead of G*L.
 template <int E2>
-__global__ __launch_bounds__(256) void k_la_merge(const uint64_t *__restrict__ clists, uint32_t M,
-                                                  uint32_t L, LaShard sh, uint32_t GLp,
-                                                  uint64_t *__restrict__ lists) {
-    const uint32_t vs = blockIdx.x / sh.kw, k = blockIdx.x % sh.kw;
+__device__ __forceinline__ void la_merge_block(uint32_t bid, const uint64_t *__restrict__ clists, uint32_t M,
+                                               uint32_t L, const LaShard &sh, uint32_t GLp,
+                                               uint64_t *__restrict__ lists) {
+    const uint32_t vs = bid / sh.kw, k = bid % sh.kw;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint64_t *in = clists + ((size_t)vs * sh.kw + k) * M;
     uint64_t e[E2];
@@ -559,6 +574,13 @@ __global__ __launch_bounds__(256) void k_la_merge(const uint64_t *__restrict__ c
     }
     block_topl<256, E2>(tv, L, lists + (size_t)(sh.v0 + vs) * sh.RS + (size_t)k * GLp,
                         [&](int j) { return e[j]; });
+}
+
+template <int E2>
+__global__ __launch_bounds__(256) void k_la_merge(const uint64_t *__restrict__ clists, uint32_t M,
+                                                  uint32_t L, LaShard sh, uint32_t GLp,
+                                                  uint64_t *__restrict__ lists) {
+    la_merge_block<E2>(blockIdx.x, clists, M, L, sh, GLp, lists);
 }
 
 // Entry m (0 <= m < EPL) of resolver lane `lane` for window pod `pod`.  Lists are laid out
@@ -961,18 +983,17 @@ __device__ __forceinline__ ResPub read_pub(const ResPub *p) {
 }
 
 template <uint32_t F, int EPL, bool DIAG, bool K32>
-__global__ __launch_bounds__(256) void k_la_resolve4(DevTable t, const DPod *__restrict__ pods,
-                                                     DevCfg c, uint32_t s0, uint32_t P,
-                                                     uint32_t K, uint32_t GLp, uint32_t lr,
-                                                     LaShard sh,
-                                                     const uint64_t *__restrict__ lists,
-                                                     int32_t *__restrict__ out_node,
-                                                     uint64_t *__restrict__ out_key,
-                                                     uint64_t *__restrict__ stamps,
-                                                     uint64_t *__restrict__ diag,
-                                                     const uint32_t *__restrict__ dprev,
-                                                     uint32_t *__restrict__ dcur) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+__device__ __forceinline__ void la_resolve4_block(uint32_t *lds, const DevTable &t, const DPod *__restrict__ pods,
+                                                  const DevCfg &c, uint32_t s0, uint32_t P,
+                                                  uint32_t K, uint32_t GLp, uint32_t lr,
+                                                  const LaShard &sh,
+                                                  const uint64_t *__restrict__ lists,
+                                                  int32_t *__restrict__ out_node,
+                                                  uint64_t *__restrict__ out_key,
+                                                  uint64_t *__restrict__ stamps,
+                                                  uint64_t *__restrict__ diag,
+                                                  const uint32_t *__restrict__ dprev,
+                                                  uint32_t *__restrict__ dcur) {
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t nwords = (t.n + 31) / 32;
@@ -1005,7 +1026,7 @@ __global__ __launch_bounds__(256) void k_la_resolve4(DevTable t, const DPod *__r
     }
     __syncthreads();
     if (kend == 0) return;
-    uint64_t dsum = 0, tprev = 0;
+    uint64_t dsum = 0, tprev = 0, dpart = 0, dwait = 0;
 #define QS_DIAG_BEGIN() if (DIAG) tprev = diag_stamp();
 #define QS_DIAG_END() if (DIAG) { const uint64_t t_ = diag_stamp(); dsum += t_ - tprev; }
 
@@ -1113,6 +1134,7 @@ __global__ __launch_bounds__(256) void k_la_resolve4(DevTable t, const DPod *__r
             const int par = i & 1, pp = par ^ 1;
             const ResPub pv = read_pub(&pub[pp]);
             if (i > 0) apply(pv, pp, wpods[i - 1]);
+            if (DIAG) { const uint64_t t_ = diag_stamp(); dpart += t_ - tprev; }
             if (i + 1 < kend) {
                 const DPod pn1 = wpods[i + 1];
                 Row s2 = S;
@@ -1182,10 +1204,13 @@ __global__ __launch_bounds__(256) void k_la_resolve4(DevTable t, const DPod *__r
                                       __HIP_MEMORY_SCOPE_WORKGROUP);  // ds_or: no round trip
             const bool use2 = pv.ks != 0 && c1 != 0 && key_node(c1) == pv.w;
             const uint64_t cc = use2 ? c2 : c1;
+            uint64_t tw0 = 0;
+            if (DIAG) tw0 = diag_stamp();
             const Row crow = sel_row(use2, r2, r1);
             const RowX cx = sel_rowx(use2, x2, x1);
             stage[par][lane] = crow;
             if (F & kFeatExt) stagex[par][lane] = make_int4(cx.ae0, cx.re0, cx.ae1, cx.re1);
+            if (DIAG) { const uint64_t t_ = diag_stamp(); dwait += t_ - tw0; }
             if (i + 1 < kend) {
                 const DPod p = wpods[i], pn1 = wpods[i + 1];
                 top2(en, c1, c2);  // pod i+1 against the dirty set through pod i-1
@@ -1198,6 +1223,7 @@ __global__ __launch_bounds__(256) void k_la_resolve4(DevTable t, const DPod *__r
                     x2 = load_rowx<F>(t, c2 ? key_node(c2) : 0u);
                 }
                 load_ent(en, i + 3);
+                if (DIAG) { const uint64_t t_ = diag_stamp(); dpart += t_ - tprev; }
                 Row cr = crow;
                 RowX crx = cx;
                 reserve(cr, crx, p, +1);
@@ -1219,10 +1245,30 @@ __global__ __launch_bounds__(256) void k_la_resolve4(DevTable t, const DPod *__r
     if (DIAG && lane == 0) {
         atomicAdd((unsigned long long *)&diag[wv], (unsigned long long)dsum);
         if (wv == 0) atomicAdd((unsigned long long *)&diag[5], (unsigned long long)kend);
+        if (wv == 1) atomicAdd((unsigned long long *)&diag[6], (unsigned long long)dpart);
+        if (wv == 3) atomicAdd((unsigned long long *)&diag[7], (unsigned long long)dpart);
+        if (wv == 3) atomicAdd((unsigned long long *)&diag[4], (unsigned long long)dwait);
     }
     if (wv == 0) __syncthreads();  // pairs with the post-loop barrier of waves A/B and C
 #undef QS_DIAG_BEGIN
 #undef QS_DIAG_END
+}
+
+template <uint32_t F, int EPL, bool DIAG, bool K32>
+__global__ __launch_bounds__(256) void k_la_resolve4(DevTable t, const DPod *__restrict__ pods,
+                                                     DevCfg c, uint32_t s0, uint32_t P,
+                                                     uint32_t K, uint32_t GLp, uint32_t lr,
+                                                     LaShard sh,
+                                                     const uint64_t *__restrict__ lists,
+                                                     int32_t *__restrict__ out_node,
+                                                     uint64_t *__restrict__ out_key,
+                                                     uint64_t *__restrict__ stamps,
+                                                     uint64_t *__restrict__ diag,
+                                                     const uint32_t *__restrict__ dprev,
+                                                     uint32_t *__restrict__ dcur) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    la_resolve4_block<F, EPL, DIAG, K32>(lds, t, pods, c, s0, P, K, GLp, lr, sh, lists, out_node, out_key,
+                                         stamps, diag, dprev, dcur);
 }
 
 // =============================================================================================
