@@ -355,6 +355,19 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
     return ((uint64_t)hi << 32) | lo;
 }
 
+// RN_f64(1/a) for 1 <= a < 2^24 without the IEEE division sequence: v_rcp_f32's estimate (within
+// 1 ulp) refined by two fma Newton steps.  The second step leaves an error near 2^-92 relative,
+// while 1/a lies at least 2^-77 (relative) from every rounding midpoint, so the final rounding is
+// RN(1/a); tests/native/exact_arith.c mode 3 checks every a and every estimate within 2 ulps.
+__device__ __forceinline__ double rcp_int(int32_t a) {
+    const double A = (double)a;
+    double y = (double)__builtin_amdgcn_rcpf((float)a);
+    double e = __builtin_fma(-A, y, 1.0);
+    y = __builtin_fma(y, e, y);
+    e = __builtin_fma(-A, y, 1.0);
+    return __builtin_fma(y, e, y);
+}
+
 // RN_f64(1/d) of a per-pod normalize maximum (IEEE division; once per pod, off the node loop).
 __device__ __forceinline__ double rcp_exact(uint32_t d) { return d ? 1.0 / (double)d : 0.0; }
 

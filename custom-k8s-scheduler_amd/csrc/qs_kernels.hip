@@ -194,8 +194,8 @@ __global__ __launch_bounds__(256) void k_scan_key(DevTable t, const DPod *__rest
 }
 
 // Keys over the SoA copy (HBM-resident tables; F = 0 or kFeatExt): lane q covers nodes
-// 4q..4q+3 with one 16-byte load per column; RN(1/alloc) is recomputed with an IEEE division
-// (the same value the host stores in the row copy, so keys are bit-identical to k_scan_key).
+// 4q..4q+3 with one 16-byte load per column; RN(1/alloc) is recomputed in registers (rcp_int:
+// the same value the host stores in the row copy, so keys are bit-identical to k_scan_key).
 template <uint32_t F>
 __global__ __launch_bounds__(256) void k_scan_soa(DevTable t, const DPod *__restrict__ pods,
                                                   uint32_t s, DevCfg c, ScanScratch *sc,
@@ -205,22 +205,33 @@ __global__ __launch_bounds__(256) void k_scan_soa(DevTable t, const DPod *__rest
     const DPodX px{};
     const uint32_t nq = (t.n + 3) / 4;  // columns are zero-padded to a multiple of 64 nodes
     uint64_t best = 0;
-    for (uint32_t q = blockIdx.x * 256 + threadIdx.x; q < nq; q += gridDim.x * 256) {
-        int4 col[kSCols];
+    // two quads per lane in flight: both iterations' loads are issued before either is scored
+    const uint32_t stride = gridDim.x * 256;
+    for (uint32_t q0 = blockIdx.x * 256 + threadIdx.x; q0 < nq; q0 += 2 * stride) {
+        int4 cols[2][kSCols];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) col[k] = reinterpret_cast<const int4 *>(t.soa.c[k])[q];
-        if (F & kFeatExt) {
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t qh = min(q0 + h * stride, nq - 1);
 #pragma unroll
-            for (int k = 8; k < kSCols; ++k) col[k] = reinterpret_cast<const int4 *>(t.soa.c[k])[q];
+            for (int k = 0; k < 8; ++k) cols[h][k] = reinterpret_cast<const int4 *>(t.soa.c[k])[qh];
+            if (F & kFeatExt) {
+#pragma unroll
+                for (int k = 8; k < kSCols; ++k) cols[h][k] = reinterpret_cast<const int4 *>(t.soa.c[k])[qh];
+            }
         }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+        const uint32_t q = q0 + h * stride;
+        if (q >= nq) break;
+        const int4 *col = cols[h];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             auto el = [&](int k) { return e == 0 ? col[k].x : e == 1 ? col[k].y : e == 2 ? col[k].z : col[k].w; };
             Row r;
             r.ac = el(kSAc); r.am = el(kSAm); r.rc = el(kSRc); r.rm = el(kSRm);
             r.zc = el(kSZc); r.zm = el(kSZm); r.np = el(kSNp); r.mp = el(kSMp);
-            r.yc = r.ac ? 1.0 / (double)r.ac : 0.0;
-            r.ym = r.am ? 1.0 / (double)r.am : 0.0;
+            r.yc = r.ac ? rcp_int(r.ac) : 0.0;
+            r.ym = r.am ? rcp_int(r.am) : 0.0;
             RowX x{};
             if (F & kFeatExt) { x.ae0 = el(kSAe0); x.re0 = el(kSRe0); x.ae1 = el(kSAe1); x.re1 = el(kSRe1); }
             const uint32_t idx = 4 * q + e;
@@ -237,6 +248,7 @@ __global__ __launch_bounds__(256) void k_scan_soa(DevTable t, const DPod *__rest
                     for (int k = 0; k < 4; ++k) score_out[4 * (size_t)idx + k] = f ? (int32_t)sco[k] : 0;
                 }
             }
+        }
         }
     }
     best = block_max_u64<256>(best);
@@ -1600,7 +1612,22 @@ static hipError_t scan_pod_f(const DevTable &t, const DPod *pods, const DPodX *p
     const bool soa = !(F & kFeatNorm) && t.soa.c[0];
     // one partial key per block; a grid of <= 2048 blocks (8 four-wave blocks per CU) strides
     const uint32_t units = soa ? (t.n + 3) / 4 : t.n;
-    const uint32_t blocks = min(kScanBlocksMax, max(1u, (units + 255) / 256));
+    uint32_t blocks = min(kScanBlocksMax, max(1u, (units + 255) / 256));
+    if (soa) {
+        // SoA scan: exactly one resident wave of blocks (CUs x blocks per CU at this kernel's
+        // occupancy), so no CU runs a second, partial round of blocks at the end of the scan
+        static const uint32_t resident = [] {
+            int dev = 0, cus = 0, per = 0;
+            if (hipGetDevice(&dev) != hipSuccess ||
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)k_scan_soa<F>, 256, 0) != hipSuccess)
+                return kScanBlocksMax;
+            const char *env = getenv("QS_SCAN_BLOCKS");
+            if (env && atoi(env) > 0) return (uint32_t)atoi(env);
+            return (uint32_t)std::max(1, std::min((int)kScanBlocksMax, cus * per));
+        }();
+        blocks = min(blocks, min(kScanBlocksMax, resident));
+    }
     if (part & 1) {
         if (soa) {
             hipLaunchKernelGGL((k_scan_soa<F>), dim3(blocks), dim3(256), 0, stream, t, pods, s, c, sc,

@@ -16,6 +16,17 @@ static double fraction(int32_t a, int32_t r, double y) {
     double q = fma(rem, y, q0);
     return r >= a ? 1.0 : q;
 }
+/* RN(1/a), 1 <= a < 2^24, as the scan kernel computes it (qs_device.hpp rcp_int): an f32 reciprocal
+ * estimate (v_rcp_f32, within 1 ulp) refined by two fma Newton steps in f64.  y0 is passed in so the
+ * check covers every estimate within +-2 f32 ulps of 1/a. */
+static double rcp_int(int32_t a, float y0f) {
+    const double A = (double)a;
+    double y = (double)y0f;
+    double e = fma(-A, y, 1.0);
+    y = fma(y, e, y);
+    e = fma(-A, y, 1.0);
+    return fma(y, e, y);
+}
 static uint64_t sm = 0x5EED1234ULL;
 static uint64_t rnd(void) {
     uint64_t z = (sm += 0x9E3779B97F4A7C15ULL);
@@ -56,6 +67,16 @@ int main(int argc, char **argv) {
             int32_t a = (int32_t)(1 + rnd() % ((1u << 24) - 1));
             int32_t r = (int32_t)(rnd() % ((uint64_t)a + 1));
             if (check_la(a, r) || check_frac(a, r)) return 1;
+        }
+    } else if (mode == 3) { /* rcp_int == IEEE 1/a for every a in [1, 2^24), estimates +-2 ulp */
+        for (int32_t a = 1; a < (1 << 24); a++) {
+            volatile double want = 1.0 / (double)a;
+            float f = 1.0f / (float)a;
+            float lo = nextafterf(nextafterf(f, 0.0f), 0.0f), hi = nextafterf(nextafterf(f, 2.0f), 2.0f);
+            for (float y0 = lo; y0 <= hi; y0 = nextafterf(y0, 2.0f)) {
+                checks++;
+                if (rcp_int(a, y0) != want) { printf("RCP a=%d y0=%.9g got %.17g want %.17g\n", a, y0, rcp_int(a, y0), want); return 1; }
+            }
         }
     } else { /* small divisors (weight sums, normalize maxima): n/d <= 100 exhaustive */
         for (uint32_t d = 1; d <= 131070; d += (d < 2048 ? 1 : 97)) {

@@ -4,7 +4,8 @@ tests/native/exact_arith.c restates the two division formulas the gfx950 kernels
 (custom-k8s-scheduler_amd/csrc/qs_device.hpp floor_div / fraction) with the same IEEE operations
 (fma, -ffp-contract=off) and compares them with true integer and IEEE division: exhaustively over
 every allocatable value of spec/synth.md, exhaustively for small divisors, and on 20M random pairs
-over the whole compacted range [1, 2^24).  The GPU parity tests then confirm the device agrees.
+over the whole compacted range [1, 2^24); and the scan kernel's reciprocal RN(1/a) (f32 estimate +
+two f64 Newton steps) exhaustively over [1, 2^24) for every estimate within 2 f32 ulps.  The GPU parity tests then confirm the device agrees.
 """
 import os
 import subprocess
@@ -22,7 +23,7 @@ def exe(tmp_path_factory):
     return out
 
 
-@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
 def test_division_formulas_exact(exe, mode):
     r = subprocess.run([exe, str(mode)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout
