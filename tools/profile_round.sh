@@ -18,6 +18,13 @@ QS_GRAPH=0 QS_SYNC_EVERY=64 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $O
 echo "fetch done"
 QS_GRAPH=0 QS_SYNC_EVERY=64 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o run --output-format csv -- python3 bench.py $ARGS > $OUT/write.log 2>&1
 echo "write done"
+# configs 4 (normalizing lookahead) and 5 (batched): kernel-trace stats of their own streams
+for cfg in "4 5000 150000 exact 1" "5 10000 200000 batched 0"; do
+    set -- $cfg
+    CFG=$1 N=$2 P=$3 MODE=$4 TA=$5 QS_GRAPH=0 QS_SYNC_EVERY=64 timeout -k 10 300 rocprofv3 --kernel-trace --stats \
+        -d $OUT/cfg$1 -o run --output-format csv -- python3 tools/kprof.py > $OUT/cfg$1.log 2>&1
+    echo "config $1 trace done"
+done
 cp $(find $OUT/trace -name '*kernel_stats.csv' | head -1) profiles/${TAG}_kernel_stats.csv
 python3 tools/summarize_pmc.py $(find $OUT/fetch -name '*counter_collection.csv' | head -1) \
     $(find $OUT/write -name '*counter_collection.csv' | head -1) profiles/${TAG}_pmc_summary.csv
