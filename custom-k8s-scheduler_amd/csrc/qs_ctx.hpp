@@ -113,7 +113,7 @@ struct qs_ctx {
     bool saved = false;
     bool mirror_stale = false;  // device ran a stream since the last mirror sync
     qs_host::DevBuf diag;
-    qs_host::DevBuf scratch, lists, clists, dio, npart, normi, nfall, bctrl, one_pod, one_podx, out_feas, out_score, out_total;
+    qs_host::DevBuf scratch, lists, clists, dio, npart, normi, nfall, nrec, bctrl, one_pod, one_podx, out_feas, out_score, out_total;
     uint32_t cap = 0;
     // sharding (qs_open_shard): RCCL communicator of this rank, nullptr when unsharded
     int rank = 0, world = 1;

@@ -851,8 +851,16 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                 const bool norm = (c->dc.feat & (kFeatTaint | kFeatAffinity)) != 0;
                 // normalizing profiles: k_la_norm pre-pass + the single-wave k_la_resolve_norm
                 geo.waves = norm || (rw && rw[0] == '1' && !overlap) ? 1u : 4u;
+                // normalizing profiles: the four-wave resolver with its stop/resume hand-off
+                // (overlapped windows, merged lists); QS_NORM_WAVES=1 keeps the single-wave kernel
+                static const char *nw = getenv("QS_NORM_WAVES");
+                if (norm && overlap && geo.epl == 1 && !(nw && nw[0] == '1') &&
+                    !(getenv("QS_DIAG") && getenv("QS_DIAG")[0] == '1'))
+                    geo.waves = 4;
                 int64_t wmax = 0;
                 for (int q = 0; q < 3; q++) wmax = std::max<int64_t>(wmax, (int64_t)c->cfg.w_fit[q] + c->cfg.w_bal[q]);
+                if (c->dc.feat & kFeatTaint) wmax += c->cfg.w_taint;       // every plugin scores <= 100
+                if (c->dc.feat & kFeatAffinity) wmax += c->cfg.w_affinity;
                 geo.k32 = (100 * wmax + 1 < 1024 && n <= (1u << 22)) ? 1u : 0u;
                 if (geo.G == 0) fail(QS_EINVAL, "no lookahead geometry for this table size");
                 const size_t rank_entries = (size_t)geo.K * 64 * geo.eplr;  // [K][GLp] per shard
@@ -865,7 +873,8 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                 const size_t nparts = norm ? (size_t)geo.W * geo.K * geo.G : 1;  // uint4 per window
                 c->npart.ensure(16 * nparts * nbuf);
                 c->normi.ensure(16 * (size_t)geo.K * nbuf);
-                c->nfall.ensure(8);
+                c->nfall.ensure(16);
+                c->nrec.ensure(4 * kDioWords);
                 // QS_DIAG=1: diagnostic resolver with per-segment shader-clock stamps (stderr)
                 static const bool diag_on = getenv("QS_DIAG") && getenv("QS_DIAG")[0] == '1';
                 uint64_t *diag = nullptr;
@@ -886,12 +895,13 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                 auto enqueue = [&]() {
                 HIPCHK(hipMemsetAsync(c->lists.p, 0, 8 * lwords * nbuf, c->stream));  // padding stays 0
                 HIPCHK(hipMemsetAsync(c->dio.p, 0, 2 * kDioWords * 4, c->stream));
-                HIPCHK(hipMemsetAsync(c->nfall.p, 0, 8, c->stream));
+                HIPCHK(hipMemsetAsync(c->nfall.p, 0, 16, c->stream));
                 auto bufs = [&](uint32_t w) {
                     const int b = overlap ? (int)(w & 1) : 0;
                     LaBufs bf{L0 + b * lwords, C0 + b * cwords, c->npart.as<uint4>() + b * nparts,
                               c->normi.as<NormInfo>() + (size_t)b * geo.K, nullptr, nullptr,
                               c->nfall.as<unsigned long long>()};
+                    bf.rec = c->nrec.as<uint32_t>();
                     if (overlap) {
                         bf.dprev = dio + ((w + 1) & 1) * kDioWords;
                         bf.dcur = dio + (w & 1) * kDioWords;
@@ -1027,8 +1037,14 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
         (void)hipEventDestroy(e0);
         (void)hipEventDestroy(e1);
         uint64_t rescans = 0;
-        if (eng == QS_ENGINE_LOOKAHEAD && c->nfall.p)
-            HIPCHK(hipMemcpy(&rescans, c->nfall.p, 8, hipMemcpyDeviceToHost));
+        if (eng == QS_ENGINE_LOOKAHEAD && c->nfall.p) {
+            uint64_t h[2] = {0, 0};
+            HIPCHK(hipMemcpy(h, c->nfall.p, 16, hipMemcpyDeviceToHost));
+            rescans = h[0];
+            if (getenv("QS_NORM_DIAG"))
+                fprintf(stderr, "QS_NORM_DIAG rescans %llu resumed windows %llu\n", (unsigned long long)h[0],
+                        (unsigned long long)h[1]);
+        }
         s->ran = true;
         c->mirror_stale = true;
         if (eng != QS_ENGINE_SCAN) c->soa_valid = false;  // those engines update the rows only

@@ -775,9 +775,26 @@ __global__ __launch_bounds__(64) void k_la_resolve_norm(
     uint32_t s0, uint32_t P, uint32_t K, uint32_t GLp, uint32_t lr, LaShard sh,
     const uint64_t *__restrict__ lists, const NormInfo *__restrict__ norm,
     int32_t *__restrict__ out_node, uint64_t *__restrict__ out_key, uint64_t *__restrict__ stamps,
-    const uint32_t *__restrict__ dprev, uint32_t *__restrict__ dcur, unsigned long long *nfall) {
+    const uint32_t *__restrict__ dprev, uint32_t *__restrict__ dcur, unsigned long long *nfall,
+    const uint32_t *__restrict__ rec) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const int lane = threadIdx.x;
+    // Resume mode (rec != nullptr, after the four-wave resolver of the same window): nothing to do
+    // unless it stopped at pod rec[0]; then continue from there with its slots (rec[1] nodes at
+    // rec[4..], rows already stored, won mask rec[2..3]) as the initial dirty set.
+    uint32_t pbase = 0;
+    uint64_t won0 = 0;
+    const uint32_t *init = dprev;
+    if (rec) {
+        const uint32_t stop = rec[0];
+        if (stop == 0xFFFFFFFFu) return;
+        if (lane == 0 && nfall) atomicAdd(nfall + 1, 1ull);  // resumed windows (QS_NORM_DIAG)
+        pbase = stop;
+        s0 += stop;
+        K -= stop;
+        won0 = (uint64_t)rec[2] | ((uint64_t)rec[3] << 32);
+        init = rec + 3;  // init[1 + j] = rec[4 + j]; the count is rec[1]
+    }
     const uint32_t n = t.n, nwords = (n + 31) / 32;
     uint32_t *dirty = lds;
     Row *srow = (Row *)(lds + ((nwords + 3) & ~3u));  // [64] slot rows, staged for a rescan
@@ -787,19 +804,19 @@ __global__ __launch_bounds__(64) void k_la_resolve_norm(
     uint32_t *sidx = (uint32_t *)(stagex + 1);         // [64] slot -> node, staged for a rescan
     for (uint32_t i = lane; i < nwords; i += 64) dirty[i] = 0;
     const uint32_t kend = min(K, P - s0);
-    const uint32_t nd0 = dprev ? dprev[0] : 0u;
+    const uint32_t nd0 = rec ? rec[1] : (dprev ? dprev[0] : 0u);
     __syncthreads();
     Row dr = empty_row();
     RowX dx{};
     uint32_t didx = 0xFFFFFFFFu;
     if ((uint32_t)lane < nd0) {
-        didx = dprev[1 + lane];
+        didx = init[1 + lane];
         dr = load_row(t, didx);
         dx = load_rowx<F>(t, didx);
         atomicOr(&dirty[didx >> 5], 1u << (didx & 31));
     }
     uint32_t nd = nd0;
-    bool won = false;
+    bool won = (uint32_t)lane < nd0 && ((won0 >> lane) & 1ull);
     uint64_t res_key = 0, res_stamp = 0;
     __syncthreads();
     auto top2 = [&](const uint64_t(&e)[EPL], uint64_t &c1, uint64_t &c2) {
@@ -820,9 +837,9 @@ __global__ __launch_bounds__(64) void k_la_resolve_norm(
     };
     uint64_t ent1[EPL], ent2[EPL];
 #pragma unroll
-    for (int m = 0; m < EPL; ++m) ent1[m] = list_ent(lists, 0, GLp, lr, sh, m, lane);
+    for (int m = 0; m < EPL; ++m) ent1[m] = list_ent(lists, pbase, GLp, lr, sh, m, lane);
 #pragma unroll
-    for (int m = 0; m < EPL; ++m) ent2[m] = kend > 1 ? list_ent(lists, 1, GLp, lr, sh, m, lane) : 0ull;
+    for (int m = 0; m < EPL; ++m) ent2[m] = kend > 1 ? list_ent(lists, pbase + 1, GLp, lr, sh, m, lane) : 0ull;
     uint64_t c1, c2;
     top2(ent1, c1, c2);
     Row r1 = load_row(t, c1 ? key_node(c1) : 0u), r2 = load_row(t, c2 ? key_node(c2) : 0u);
@@ -832,7 +849,7 @@ __global__ __launch_bounds__(64) void k_la_resolve_norm(
     // of the 44-dword extension record spilled the SGPRs)
     DPod pn = load_vgpr(pods + s0);
     DPodX pxn = load_vgpr(podx + s0);
-    NormInfo nfn = load_vgpr(norm);
+    NormInfo nfn = load_vgpr(norm + pbase);
     for (uint32_t i = 0; i < kend; ++i) {
         const DPod p = pn;
         const DPodX px = pxn;
@@ -840,7 +857,7 @@ __global__ __launch_bounds__(64) void k_la_resolve_norm(
         if (i + 1 < kend) {
             pn = load_vgpr(pods + s0 + i + 1);
             pxn = load_vgpr(podx + s0 + i + 1);
-            nfn = load_vgpr(norm + i + 1);
+            nfn = load_vgpr(norm + pbase + i + 1);
         }
         const bool use2 = c1 && key_node(c1) == wprev;
         const uint64_t cand = use2 ? c2 : c1;
@@ -855,7 +872,7 @@ __global__ __launch_bounds__(64) void k_la_resolve_norm(
         }
         if (i + 2 < kend) {
 #pragma unroll
-            for (int m = 0; m < EPL; ++m) ent2[m] = list_ent(lists, i + 2, GLp, lr, sh, m, lane);
+            for (int m = 0; m < EPL; ++m) ent2[m] = list_ent(lists, pbase + i + 2, GLp, lr, sh, m, lane);
         }
         const double ymt = rcp_exact(nf.mt), yma = rcp_exact(nf.ma);
         const bool act = (uint32_t)lane < nd;
@@ -889,26 +906,47 @@ __global__ __launch_bounds__(64) void k_la_resolve_norm(
                     x = load_rowx<F>(t, idx);
                 }
             };
+            // both passes keep U rows per lane in flight (one wave, dependent loads otherwise)
+            constexpr uint32_t U = 4;
             uint32_t mt = 0, ma = 0;
-            for (uint32_t idx = lane; idx < n; idx += 64) {
-                Row r; RowX x;
-                row_at(idx, r, x);
-                if (feasible<F>(r, x, p, px)) {
-                    const uint32_t a = taint_raw(x, px), b2 = affinity_raw(x, p, px);
-                    mt = a > mt ? a : mt;
-                    ma = b2 > ma ? b2 : ma;
+            for (uint32_t b0 = lane; b0 < n; b0 += 64 * U) {
+                Row r[U];
+                RowX x[U];
+#pragma unroll
+                for (uint32_t u = 0; u < U; ++u) {
+                    r[u] = empty_row();
+                    x[u] = RowX{};
+                    if (b0 + 64 * u < n) row_at(b0 + 64 * u, r[u], x[u]);
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < U; ++u) {
+                    if (b0 + 64 * u < n && feasible<F>(r[u], x[u], p, px)) {
+                        const uint32_t a = taint_raw(x[u], px), b2 = affinity_raw(x[u], p, px);
+                        mt = a > mt ? a : mt;
+                        ma = b2 > ma ? b2 : ma;
+                    }
                 }
             }
             mt = (F & kFeatTaint) ? wave_max_u32(mt) : 0u;
             ma = (F & kFeatAffinity) ? wave_max_u32(ma) : 0u;
             const double ymt2 = rcp_exact(mt), yma2 = rcp_exact(ma);
             uint64_t best = 0;
-            for (uint32_t idx = lane; idx < n; idx += 64) {
-                Row r; RowX x;
-                row_at(idx, r, x);
-                const uint32_t tv = node_total<F>(r, x, p, px, c, mt, ymt2, ma, yma2, nullptr);
-                const uint64_t key = feasible<F>(r, x, p, px) ? pack_key(tv + 1, idx) : 0ull;
-                best = key > best ? key : best;
+            for (uint32_t b0 = lane; b0 < n; b0 += 64 * U) {
+                Row r[U];
+                RowX x[U];
+#pragma unroll
+                for (uint32_t u = 0; u < U; ++u) {
+                    r[u] = empty_row();
+                    x[u] = RowX{};
+                    if (b0 + 64 * u < n) row_at(b0 + 64 * u, r[u], x[u]);
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < U; ++u) {
+                    const uint32_t idx = b0 + 64 * u;
+                    const uint32_t tv = node_total<F>(r[u], x[u], p, px, c, mt, ymt2, ma, yma2, nullptr);
+                    const uint64_t key = (idx < n && feasible<F>(r[u], x[u], p, px)) ? pack_key(tv + 1, idx) : 0ull;
+                    best = key > best ? key : best;
+                }
             }
             ks = wave_max_u64(best);
             if (lane == 0 && nfall) atomicAdd(nfall, 1ull);
@@ -1005,7 +1043,11 @@ __device__ __forceinline__ void la_resolve4_block(uint32_t *lds, const DevTable 
                                                   uint64_t *__restrict__ stamps,
                                                   uint64_t *__restrict__ diag,
                                                   const uint32_t *__restrict__ dprev,
-                                                  uint32_t *__restrict__ dcur) {
+                                                  uint32_t *__restrict__ dcur,
+                                                  const DPodX *__restrict__ podx = nullptr,
+                                                  const NormInfo *__restrict__ norm = nullptr,
+                                                  uint32_t *__restrict__ rec = nullptr) {
+    constexpr bool NORM = (F & kFeatNorm) != 0;
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t nwords = (t.n + 31) / 32;
@@ -1020,12 +1062,29 @@ __device__ __forceinline__ void la_resolve4_block(uint32_t *lds, const DevTable 
     int4(*stagex)[64] = (int4(*)[64])base; base += 2 * 64 * sizeof(int4);
     ResPub *pub = (ResPub *)base; base += 2 * sizeof(ResPub);
     uint32_t *slotnode = (uint32_t *)base; base += 64 * 4;
-    DPod *wpods = (DPod *)base;  // the window's pod records (K <= 64)
+    DPod *wpods = (DPod *)base; base += 64 * sizeof(DPod);  // the window's pod records (K <= 64)
+    // normalizing profiles only (the host sizes the LDS accordingly): pod extensions, the
+    // selection-time maxima and their reciprocals, C's lost-holder flags, full staged RowX
+    DPodX *wpodx = (DPodX *)base; base += 64 * sizeof(DPodX);
+    NormInfo *wnorm = (NormInfo *)base; base += 64 * sizeof(NormInfo);
+    double2 *wrcp = (double2 *)base; base += 64 * sizeof(double2);
+    uint32_t(*flagC)[64] = (uint32_t(*)[64])base; base += 2 * 64 * 4;
+    RowX(*stagexN)[64] = (RowX(*)[64])base;
 
     for (uint32_t i = threadIdx.x; i < nwords; i += 256) dirty[i] = 0;
     if (threadIdx.x == 0) pub[1] = ResPub{0, 0xFFFFFFFFu, -1, -1, 0, {0, 0}};
     const uint32_t kend = min(K, P - s0);
     if (threadIdx.x < kend) wpods[threadIdx.x] = pods[s0 + threadIdx.x];
+    if (NORM) {
+        constexpr uint32_t q = sizeof(DPodX) / 16;
+        for (uint32_t j = threadIdx.x; j < kend * q; j += 256)
+            reinterpret_cast<uint4 *>(wpodx)[j] = reinterpret_cast<const uint4 *>(podx + s0)[j];
+        if (threadIdx.x < kend) {
+            const NormInfo nf = norm[threadIdx.x];
+            wnorm[threadIdx.x] = nf;
+            wrcp[threadIdx.x] = make_double2(rcp_exact(nf.mt), rcp_exact(nf.ma));
+        }
+    }
     const DPodX px{};
     // Overlapped windows (dprev != nullptr): this window's lists were selected against the table
     // as it stood BEFORE the previous window, so the nodes that window dirtied (dprev[1..nd0])
@@ -1049,6 +1108,7 @@ __device__ __forceinline__ void la_resolve4_block(uint32_t *lds, const DevTable 
         uint32_t nd = nd0, didx = (uint32_t)lane < nd0 ? dprev[1 + lane] : 0xFFFFFFFFu;
         bool won = false;  // slot won a pod of THIS window (it belongs to the next window's dprev)
         uint64_t res_key = 0, res_stamp = 0;
+        uint32_t kdone = kend;  // normalizing profiles: the pod a stop hands to the resume kernel
         ResPub pv{0, 0xFFFFFFFFu, -1, -1, 0, {0, 0}};  // D produced it: kept in registers
         __syncthreads();  // prologue barrier (wave C publishes pod 0's candidates)
         for (uint32_t i = 0; i < kend; ++i) {
@@ -1058,12 +1118,38 @@ __device__ __forceinline__ void la_resolve4_block(uint32_t *lds, const DevTable 
             const uint64_t a = keyA[pp][lane], b = keyB[pp][lane], cl = keyC[pp][lane];
             const uint64_t e1 = C1[pp][lane], e2 = EPL > 1 ? C2[pp][lane] : 0ull;
             const bool pnew = pv.ks != 0 && pv.slot < 0;
-            const uint64_t sc = (lane == pv.slot) ? b : a;
+            uint64_t sc = (lane == pv.slot) ? b : a;
+            uint32_t fl = 0;  // NORM: lost-holder flags of this slot (bit 0 taint, bit 1 affinity)
+            if (NORM) {
+                fl = (uint32_t)sc & 3u;
+                sc &= ~3ull;
+            }
             uint64_t fk = ((uint32_t)lane < nd && sc) ? (sc | (uint64_t)(0xFFFFFFFFu - didx)) : 0ull;
             if (pnew) {
                 const uint64_t cw = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(cl >> 32), pv.src) << 32) |
                                     (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)cl, pv.src);
                 if ((uint32_t)lane == pv.nd_old) fk = cw;
+                if (NORM) {
+                    const uint32_t fc = (uint32_t)__builtin_amdgcn_readlane((int)flagC[pp][lane], pv.src);
+                    if ((uint32_t)lane == pv.nd_old) fl = fc;
+                }
+            }
+            if (NORM) {
+                // do the selection-time maxima still hold for pod i?  A maximum is lost only when
+                // every node attaining it is dirty and infeasible now; then the resume kernel
+                // (k_la_resolve_norm) takes over from pod i with an exact rescan
+                const NormInfo nf = wnorm[i];
+                bool unsafe = false;
+                if (F & kFeatTaint)
+                    unsafe |= nf.mt > 0 && (uint32_t)__popcll(__ballot((uint32_t)lane < nd && (fl & 1u))) >= nf.ct;
+                if (F & kFeatAffinity)
+                    unsafe |= nf.ma > 0 && (uint32_t)__popcll(__ballot((uint32_t)lane < nd && (fl & 2u))) >= nf.ca;
+                if (unsafe) {
+                    if (lane == 0) pub[par] = ResPub{0, 0xFFFFFFFFu, -2, -1, nd, {0, 0}};  // STOP
+                    kdone = i;
+                    __syncthreads();
+                    break;
+                }
             }
             const uint64_t cand = (pv.ks != 0 && e1 != 0 && key_node(e1) == pv.w) ? e2 : e1;
             const uint64_t best = fk > cand ? fk : cand;
@@ -1097,17 +1183,31 @@ __device__ __forceinline__ void la_resolve4_block(uint32_t *lds, const DevTable 
             QS_DIAG_END()
             __syncthreads();
         }
-        if ((uint32_t)lane < kend) {
+        if ((uint32_t)lane < kdone) {
             const uint32_t s = s0 + lane;
             out_node[s] = res_key ? (int32_t)key_node(res_key) : -1;
             if (out_key) out_key[s] = res_key;
             if (stamps) stamps[s] = res_stamp;
         }
         if ((uint32_t)lane < nd) slotnode[lane] = didx;
-        if (dcur) {  // nodes dirtied in this window, for the next (overlapped) window
+        if (kdone < kend) {
+            // stopped: hand the window state to the resume kernel — rec = {first pod left, slots,
+            // won mask lo/hi, slot nodes}; it writes dcur when it finishes the window
             const uint64_t wm = __ballot(won && (uint32_t)lane < nd);
-            if (won && (uint32_t)lane < nd) dcur[1 + __popcll(wm & ((1ull << lane) - 1ull))] = didx;
-            if (lane == 0) dcur[0] = (uint32_t)__popcll(wm);
+            if (lane == 0) {
+                rec[0] = kdone;
+                rec[1] = nd;
+                rec[2] = (uint32_t)wm;
+                rec[3] = (uint32_t)(wm >> 32);
+            }
+            if ((uint32_t)lane < nd) rec[4 + lane] = didx;
+        } else {
+            if (rec && lane == 0) rec[0] = 0xFFFFFFFFu;
+            if (dcur) {  // nodes dirtied in this window, for the next (overlapped) window
+                const uint64_t wm = __ballot(won && (uint32_t)lane < nd);
+                if (won && (uint32_t)lane < nd) dcur[1 + __popcll(wm & ((1ull << lane) - 1ull))] = didx;
+                if (lane == 0) dcur[0] = (uint32_t)__popcll(wm);
+            }
         }
     } else if (wv <= 2) {
         // ---- A / B: apply pod i-1 to the slot copy, then the next pod's keys --------------------
@@ -1119,11 +1219,28 @@ __device__ __forceinline__ void la_resolve4_block(uint32_t *lds, const DevTable 
             S = load_row(t, nn);
             SX = load_rowx<F>(t, nn);
         }
-        if (wv == 1 && nd0 > 0) {  // pod 0's keys of the inherited slots ("not the winner" case)
-            const bool f = feasible<F>(S, SX, wpods[0], px);
-            const uint32_t tot = node_total<F>(S, SX, wpods[0], px, c, 0, 0.0, 0, 0.0, nullptr);
-            keyA[1][lane] = ((uint32_t)lane < nd && f) ? ((uint64_t)(tot + 1) << 32) : 0ull;
-        }
+        // score half of a slot key for window pod k (+ NORM lost-holder flags in bits 0-1)
+        auto slot_key = [&](const Row &r, const RowX &x, uint32_t k) -> uint64_t {
+            const DPod &q = wpods[k];
+            const bool act = (uint32_t)lane < nd;
+            if (NORM) {
+                const DPodX &qx = wpodx[k];
+                const NormInfo nf = wnorm[k];
+                const double2 yr = wrcp[k];
+                const bool f = feasible<F>(r, x, q, qx);
+                const uint32_t tot = node_total<F>(r, x, q, qx, c, nf.mt, yr.x, nf.ma, yr.y, nullptr);
+                uint32_t fl = 0;
+                if (act && !f) {
+                    if (F & kFeatTaint) fl |= taint_raw(x, qx) == nf.mt ? 1u : 0u;
+                    if (F & kFeatAffinity) fl |= affinity_raw(x, q, qx) == nf.ma ? 2u : 0u;
+                }
+                return ((act && f) ? ((uint64_t)(tot + 1) << 32) : 0ull) | fl;
+            }
+            const bool f = feasible<F>(r, x, q, px);
+            const uint32_t tot = node_total<F>(r, x, q, px, c, 0, 0.0, 0, 0.0, nullptr);
+            return (act && f) ? ((uint64_t)(tot + 1) << 32) : 0ull;
+        };
+        if (wv == 1 && nd0 > 0) keyA[1][lane] = slot_key(S, SX, 0);  // pod 0, inherited slots
         auto apply = [&](const ResPub &pv, int pp, const DPod &pprev) {
             if (pv.ks == 0) return;
             if (pv.slot >= 0) {
@@ -1131,7 +1248,9 @@ __device__ __forceinline__ void la_resolve4_block(uint32_t *lds, const DevTable 
             } else {
                 if ((uint32_t)lane == pv.nd_old) {
                     S = stage[pp][pv.src];
-                    if (F & kFeatExt) {
+                    if (NORM) {
+                        SX = stagexN[pp][pv.src];
+                    } else if (F & kFeatExt) {
                         const int4 e = stagex[pp][pv.src];
                         SX.ae0 = e.x; SX.re0 = e.y; SX.ae1 = e.z; SX.re1 = e.w;
                     }
@@ -1141,27 +1260,26 @@ __device__ __forceinline__ void la_resolve4_block(uint32_t *lds, const DevTable 
             }
         };
         __syncthreads();
+        bool stopped = false;
         for (uint32_t i = 0; i < kend; ++i) {
             QS_DIAG_BEGIN()
             const int par = i & 1, pp = par ^ 1;
             const ResPub pv = read_pub(&pub[pp]);
+            if (NORM && pv.slot == -2) { stopped = true; break; }  // D stopped at pod i-1
             if (i > 0) apply(pv, pp, wpods[i - 1]);
             if (DIAG) { const uint64_t t_ = diag_stamp(); dpart += t_ - tprev; }
             if (i + 1 < kend) {
-                const DPod pn1 = wpods[i + 1];
                 Row s2 = S;
                 RowX x2s = SX;
                 if (wv == 2) reserve(s2, x2s, wpods[i], +1);
-                const bool f = feasible<F>(s2, x2s, pn1, px);
-                const uint32_t tot = node_total<F>(s2, x2s, pn1, px, c, 0, 0.0, 0, 0.0, nullptr);
                 // score half only: wave D owns the slot -> node map and fills the index half
-                const uint64_t k = ((uint32_t)lane < nd && f) ? ((uint64_t)(tot + 1) << 32) : 0ull;
-                (wv == 1 ? keyA : keyB)[par][lane] = k;
+                (wv == 1 ? keyA : keyB)[par][lane] = slot_key(s2, x2s, i + 1);
             }
             QS_DIAG_END()
             __syncthreads();
         }
-        if (wv == 1) apply(read_pub(&pub[(kend - 1) & 1]), (kend - 1) & 1, wpods[kend - 1]);
+        // (a stop at the last pod publishes STOP, which apply() ignores: ks == 0)
+        if (wv == 1 && !stopped) apply(read_pub(&pub[(kend - 1) & 1]), (kend - 1) & 1, wpods[kend - 1]);
         __syncthreads();  // slotnode written by wave D
         if (wv == 1 && (uint32_t)lane < nd) {
             const uint32_t node = slotnode[lane];
@@ -1207,10 +1325,11 @@ __device__ __forceinline__ void la_resolve4_block(uint32_t *lds, const DevTable 
         Row r1 = load_row(t, c1 ? key_node(c1) : 0u), r2 = TWO ? load_row(t, c2 ? key_node(c2) : 0u) : empty_row();
         RowX x1 = load_rowx<F>(t, c1 ? key_node(c1) : 0u), x2 = TWO ? load_rowx<F>(t, c2 ? key_node(c2) : 0u) : RowX{};
         __syncthreads();
-        auto step = [&](uint32_t i, uint64_t(&en)[EPL]) {
+        auto step = [&](uint32_t i, uint64_t(&en)[EPL]) -> bool {
             QS_DIAG_BEGIN()
             const int par = i & 1, pp = par ^ 1;
             const ResPub pv = read_pub(&pub[pp]);
+            if (NORM && pv.slot == -2) return false;  // D stopped at pod i-1
             if (lane == 0 && pv.ks != 0 && pv.slot < 0)
                 __hip_atomic_fetch_or(&dirty[pv.w >> 5], 1u << (pv.w & 31), __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_WORKGROUP);  // ds_or: no round trip
@@ -1221,7 +1340,8 @@ __device__ __forceinline__ void la_resolve4_block(uint32_t *lds, const DevTable 
             const Row crow = sel_row(use2, r2, r1);
             const RowX cx = sel_rowx(use2, x2, x1);
             stage[par][lane] = crow;
-            if (F & kFeatExt) stagex[par][lane] = make_int4(cx.ae0, cx.re0, cx.ae1, cx.re1);
+            if (NORM) stagexN[par][lane] = cx;
+            else if (F & kFeatExt) stagex[par][lane] = make_int4(cx.ae0, cx.re0, cx.ae1, cx.re1);
             if (DIAG) { const uint64_t t_ = diag_stamp(); dwait += t_ - tw0; }
             if (i + 1 < kend) {
                 const DPod p = wpods[i], pn1 = wpods[i + 1];
@@ -1239,17 +1359,32 @@ __device__ __forceinline__ void la_resolve4_block(uint32_t *lds, const DevTable 
                 Row cr = crow;
                 RowX crx = cx;
                 reserve(cr, crx, p, +1);
-                const bool f = feasible<F>(cr, crx, pn1, px);
-                const uint32_t tot = node_total<F>(cr, crx, pn1, px, c, 0, 0.0, 0, 0.0, nullptr);
-                keyC[par][lane] = (cc != 0 && f) ? pack_key(tot + 1, key_node(cc)) : 0ull;
+                if (NORM) {
+                    const DPodX &qx = wpodx[i + 1];
+                    const NormInfo nf = wnorm[i + 1];
+                    const double2 yr = wrcp[i + 1];
+                    const bool f = feasible<F>(cr, crx, pn1, qx);
+                    const uint32_t tot = node_total<F>(cr, crx, pn1, qx, c, nf.mt, yr.x, nf.ma, yr.y, nullptr);
+                    keyC[par][lane] = (cc != 0 && f) ? pack_key(tot + 1, key_node(cc)) : 0ull;
+                    uint32_t fl = 0;
+                    if (!f) {
+                        if (F & kFeatTaint) fl |= taint_raw(crx, qx) == nf.mt ? 1u : 0u;
+                        if (F & kFeatAffinity) fl |= affinity_raw(crx, pn1, qx) == nf.ma ? 2u : 0u;
+                    }
+                    flagC[par][lane] = fl;
+                } else {
+                    const bool f = feasible<F>(cr, crx, pn1, px);
+                    const uint32_t tot = node_total<F>(cr, crx, pn1, px, c, 0, 0.0, 0, 0.0, nullptr);
+                    keyC[par][lane] = (cc != 0 && f) ? pack_key(tot + 1, key_node(cc)) : 0ull;
+                }
             }
             QS_DIAG_END()
             __syncthreads();
+            return true;
         };
         uint32_t i = 0;
         for (; i + 1 < kend; i += 2) {
-            step(i, eX);
-            step(i + 1, eY);
+            if (!step(i, eX) || !step(i + 1, eY)) { i = kend; break; }
         }
         if (i < kend) step(i, eX);
         __syncthreads();
@@ -1277,10 +1412,13 @@ __global__ __launch_bounds__(256) void k_la_resolve4(DevTable t, const DPod *__r
                                                      uint64_t *__restrict__ stamps,
                                                      uint64_t *__restrict__ diag,
                                                      const uint32_t *__restrict__ dprev,
-                                                     uint32_t *__restrict__ dcur) {
+                                                     uint32_t *__restrict__ dcur,
+                                                     const DPodX *__restrict__ podx,
+                                                     const NormInfo *__restrict__ norm,
+                                                     uint32_t *__restrict__ rec) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     la_resolve4_block<F, EPL, DIAG, K32>(lds, t, pods, c, s0, P, K, GLp, lr, sh, lists, out_node, out_key,
-                                         stamps, diag, dprev, dcur);
+                                         stamps, diag, dprev, dcur, podx, norm, rec);
 }
 
 // =============================================================================================
@@ -1707,8 +1845,26 @@ static hipError_t la_window_f(const DevTable &t, const DPod *pods, const DPodX *
         const size_t bm = (((t.n + 31) / 32 + 3) & ~3u) * 4;
         if constexpr ((F & kFeatNorm) != 0) {
             const size_t ldsn = bm + 64 * (sizeof(Row) + sizeof(RowX)) + sizeof(Row) + sizeof(RowX) + 64 * 4;
+            if (geo.waves == 4) {
+                // four-wave resolver with the maxima test; on a lost maximum it stops and the
+                // single-wave kernel resumes the window from that pod (rescan included)
+                if (geo.epl != 1 || !bf.rec || diag) return hipErrorInvalidValue;
+                const size_t lds4n = bm + 5 * 2 * 64 * 8 + 2 * 64 * (sizeof(Row) + sizeof(int4)) + 2 * sizeof(ResPub) +
+                                     64 * 4 + 64 * sizeof(DPod) + 64 * sizeof(DPodX) + 64 * sizeof(NormInfo) +
+                                     64 * sizeof(double2) + 2 * 64 * 4 + 2 * 64 * sizeof(RowX);
+                if (geo.k32)
+                    hipLaunchKernelGGL((k_la_resolve4<F, 1, false, true>), dim3(1), dim3(256), lds4n, stream, t, pods, c, s0, P,
+                                       K, GLp, geo.lr, sh, bf.lists, on, ok, st, diag, bf.dprev, bf.dcur, podx, bf.norm, bf.rec);
+                else
+                    hipLaunchKernelGGL((k_la_resolve4<F, 1, false, false>), dim3(1), dim3(256), lds4n, stream, t, pods, c, s0, P,
+                                       K, GLp, geo.lr, sh, bf.lists, on, ok, st, diag, bf.dprev, bf.dcur, podx, bf.norm, bf.rec);
+                QS_RET(hipGetLastError());
+                hipLaunchKernelGGL((k_la_resolve_norm<F, 1>), dim3(1), dim3(64), ldsn, stream, t, pods, podx, c, s0, P, K, GLp,
+                                   geo.lr, sh, bf.lists, bf.norm, on, ok, st, bf.dprev, bf.dcur, bf.nfall, bf.rec);
+                return hipGetLastError();
+            }
             switch (geo.epl) {
-#define QS_RESN(EP) case EP: hipLaunchKernelGGL((k_la_resolve_norm<F, EP>), dim3(1), dim3(64), ldsn, stream, t, pods, podx, c, s0, P, K, GLp, geo.lr, sh, bf.lists, bf.norm, on, ok, st, bf.dprev, bf.dcur, bf.nfall); break;
+#define QS_RESN(EP) case EP: hipLaunchKernelGGL((k_la_resolve_norm<F, EP>), dim3(1), dim3(64), ldsn, stream, t, pods, podx, c, s0, P, K, GLp, geo.lr, sh, bf.lists, bf.norm, on, ok, st, bf.dprev, bf.dcur, bf.nfall, nullptr); break;
                 QS_RESN(1) QS_RESN(2) QS_RESN(4) QS_RESN(8) QS_RESN(16)
 #undef QS_RESN
                 default: return hipErrorInvalidValue;
@@ -1726,9 +1882,9 @@ static hipError_t la_window_f(const DevTable &t, const DPod *pods, const DPodX *
                 if (diag) hipLaunchKernelGGL((k_la_resolve<F, EP, true>), dim3(1), dim3(64), lds, stream, t, pods, c, s0, P, K, GLp, geo.lr, sh, lists, on, ok, st, diag); \
                 else hipLaunchKernelGGL((k_la_resolve<F, EP, false>), dim3(1), dim3(64), lds, stream, t, pods, c, s0, P, K, GLp, geo.lr, sh, lists, on, ok, st, diag); \
             } else { \
-                if (diag) hipLaunchKernelGGL((k_la_resolve4<F, EP, true, false>), dim3(1), dim3(256), lds4, stream, t, pods, c, s0, P, K, GLp, geo.lr, sh, lists, on, ok, st, diag, dprev, dcur); \
-                else if (geo.k32) hipLaunchKernelGGL((k_la_resolve4<F, EP, false, true>), dim3(1), dim3(256), lds4, stream, t, pods, c, s0, P, K, GLp, geo.lr, sh, lists, on, ok, st, diag, dprev, dcur); \
-                else hipLaunchKernelGGL((k_la_resolve4<F, EP, false, false>), dim3(1), dim3(256), lds4, stream, t, pods, c, s0, P, K, GLp, geo.lr, sh, lists, on, ok, st, diag, dprev, dcur); \
+                if (diag) hipLaunchKernelGGL((k_la_resolve4<F, EP, true, false>), dim3(1), dim3(256), lds4, stream, t, pods, c, s0, P, K, GLp, geo.lr, sh, lists, on, ok, st, diag, dprev, dcur, nullptr, nullptr, nullptr); \
+                else if (geo.k32) hipLaunchKernelGGL((k_la_resolve4<F, EP, false, true>), dim3(1), dim3(256), lds4, stream, t, pods, c, s0, P, K, GLp, geo.lr, sh, lists, on, ok, st, diag, dprev, dcur, nullptr, nullptr, nullptr); \
+                else hipLaunchKernelGGL((k_la_resolve4<F, EP, false, false>), dim3(1), dim3(256), lds4, stream, t, pods, c, s0, P, K, GLp, geo.lr, sh, lists, on, ok, st, diag, dprev, dcur, nullptr, nullptr, nullptr); \
             } break;
             QS_RES(1) QS_RES(2) QS_RES(4) QS_RES(8) QS_RES(16)
 #undef QS_RES

@@ -68,6 +68,8 @@ struct LaBufs {
     unsigned long long *nfall;
     // batched mode: the batch's stream positions and size on the device (nullptr: s0 + k, kw)
     const uint32_t *pidx = nullptr, *pcount = nullptr;
+    // normalizing profiles, four-wave resolver: the stop record it hands to the resume kernel
+    uint32_t *rec = nullptr;
 };
 hipError_t launch_la_window(const DevTable &t, const DPod *pods, const DPodX *podx, uint32_t s0,
                             uint32_t P, const DevCfg &c, const LaGeom &geo, const LaBufs &bufs,
