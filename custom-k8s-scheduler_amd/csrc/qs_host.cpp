@@ -854,9 +854,7 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                 // normalizing profiles: the four-wave resolver with its stop/resume hand-off
                 // (overlapped windows, merged lists); QS_NORM_WAVES=1 keeps the single-wave kernel
                 static const char *nw = getenv("QS_NORM_WAVES");
-                if (norm && overlap && geo.epl == 1 && !(nw && nw[0] == '1') &&
-                    !(getenv("QS_DIAG") && getenv("QS_DIAG")[0] == '1'))
-                    geo.waves = 4;
+                if (norm && overlap && geo.epl == 1 && !(nw && nw[0] == '1')) geo.waves = 4;
                 int64_t wmax = 0;
                 for (int q = 0; q < 3; q++) wmax = std::max<int64_t>(wmax, (int64_t)c->cfg.w_fit[q] + c->cfg.w_bal[q]);
                 if (c->dc.feat & kFeatTaint) wmax += c->cfg.w_taint;       // every plugin scores <= 100

@@ -1220,13 +1220,24 @@ __device__ __forceinline__ void la_resolve4_block(uint32_t *lds, const DevTable 
             SX = load_rowx<F>(t, nn);
         }
         // score half of a slot key for window pod k (+ NORM lost-holder flags in bits 0-1)
-        auto slot_key = [&](const Row &r, const RowX &x, uint32_t k) -> uint64_t {
+        // NORM: pod k's extension record, maxima and reciprocals, read from LDS one step ahead
+        struct PodN {
+            DPodX x;
+            NormInfo nf;
+            double2 yr;
+        };
+        auto podn = [&](uint32_t k) -> PodN {
+            PodN r{};
+            if (NORM && k < kend) r = PodN{wpodx[k], wnorm[k], wrcp[k]};
+            return r;
+        };
+        auto slot_key = [&](const Row &r, const RowX &x, uint32_t k, const PodN &pn) -> uint64_t {
             const DPod &q = wpods[k];
             const bool act = (uint32_t)lane < nd;
             if (NORM) {
-                const DPodX &qx = wpodx[k];
-                const NormInfo nf = wnorm[k];
-                const double2 yr = wrcp[k];
+                const DPodX &qx = pn.x;
+                const NormInfo nf = pn.nf;
+                const double2 yr = pn.yr;
                 const bool f = feasible<F>(r, x, q, qx);
                 const uint32_t tot = node_total<F>(r, x, q, qx, c, nf.mt, yr.x, nf.ma, yr.y, nullptr);
                 uint32_t fl = 0;
@@ -1240,7 +1251,8 @@ __device__ __forceinline__ void la_resolve4_block(uint32_t *lds, const DevTable 
             const uint32_t tot = node_total<F>(r, x, q, px, c, 0, 0.0, 0, 0.0, nullptr);
             return (act && f) ? ((uint64_t)(tot + 1) << 32) : 0ull;
         };
-        if (wv == 1 && nd0 > 0) keyA[1][lane] = slot_key(S, SX, 0);  // pod 0, inherited slots
+        if (wv == 1 && nd0 > 0) keyA[1][lane] = slot_key(S, SX, 0, podn(0));  // pod 0, inherited slots
+        PodN pnx = podn(1);  // pod i+1's record at step i
         auto apply = [&](const ResPub &pv, int pp, const DPod &pprev) {
             if (pv.ks == 0) return;
             if (pv.slot >= 0) {
@@ -1269,11 +1281,13 @@ __device__ __forceinline__ void la_resolve4_block(uint32_t *lds, const DevTable 
             if (i > 0) apply(pv, pp, wpods[i - 1]);
             if (DIAG) { const uint64_t t_ = diag_stamp(); dpart += t_ - tprev; }
             if (i + 1 < kend) {
+                const PodN pcur = pnx;
+                if (NORM) pnx = podn(i + 2);  // next step's record: its LDS reads overlap this score
                 Row s2 = S;
                 RowX x2s = SX;
                 if (wv == 2) reserve(s2, x2s, wpods[i], +1);
                 // score half only: wave D owns the slot -> node map and fills the index half
-                (wv == 1 ? keyA : keyB)[par][lane] = slot_key(s2, x2s, i + 1);
+                (wv == 1 ? keyA : keyB)[par][lane] = slot_key(s2, x2s, i + 1, pcur);
             }
             QS_DIAG_END()
             __syncthreads();
@@ -1848,11 +1862,14 @@ static hipError_t la_window_f(const DevTable &t, const DPod *pods, const DPodX *
             if (geo.waves == 4) {
                 // four-wave resolver with the maxima test; on a lost maximum it stops and the
                 // single-wave kernel resumes the window from that pod (rescan included)
-                if (geo.epl != 1 || !bf.rec || diag) return hipErrorInvalidValue;
+                if (geo.epl != 1 || !bf.rec) return hipErrorInvalidValue;
                 const size_t lds4n = bm + 5 * 2 * 64 * 8 + 2 * 64 * (sizeof(Row) + sizeof(int4)) + 2 * sizeof(ResPub) +
                                      64 * 4 + 64 * sizeof(DPod) + 64 * sizeof(DPodX) + 64 * sizeof(NormInfo) +
                                      64 * sizeof(double2) + 2 * 64 * 4 + 2 * 64 * sizeof(RowX);
-                if (geo.k32)
+                if (diag)
+                    hipLaunchKernelGGL((k_la_resolve4<F, 1, true, false>), dim3(1), dim3(256), lds4n, stream, t, pods, c, s0, P,
+                                       K, GLp, geo.lr, sh, bf.lists, on, ok, st, diag, bf.dprev, bf.dcur, podx, bf.norm, bf.rec);
+                else if (geo.k32)
                     hipLaunchKernelGGL((k_la_resolve4<F, 1, false, true>), dim3(1), dim3(256), lds4n, stream, t, pods, c, s0, P,
                                        K, GLp, geo.lr, sh, bf.lists, on, ok, st, diag, bf.dprev, bf.dcur, podx, bf.norm, bf.rec);
                 else
@@ -1900,7 +1917,7 @@ hipError_t launch_la_window(const DevTable &t, const DPod *pods, const DPodX *po
                             hipStream_t stream, int part) {
     if (bf.dprev && geo.waves == 1 && !(c.feat & kFeatNorm)) return hipErrorInvalidValue;
     if (c.feat & kFeatNorm) {
-        if (diag) return hipErrorInvalidValue;
+        if (diag && geo.waves != 4) return hipErrorInvalidValue;
         return la_window_f<kFeatExt | kFeatTaint | kFeatAffinity>(t, pods, podx, s0, P, c, geo, bf, on, ok, st, diag, stream, part);
     }
     if (c.feat & kFeatExt) return la_window_f<kFeatExt>(t, pods, podx, s0, P, c, geo, bf, on, ok, st, diag, stream, part);
