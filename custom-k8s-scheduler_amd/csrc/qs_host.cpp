@@ -877,8 +877,8 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                 static const bool diag_on = getenv("QS_DIAG") && getenv("QS_DIAG")[0] == '1';
                 uint64_t *diag = nullptr;
                 if (diag_on) {
-                    c->diag.ensure(64);
-                    HIPCHK(hipMemsetAsync(c->diag.p, 0, 64, c->stream));
+                    c->diag.ensure(128);
+                    HIPCHK(hipMemsetAsync(c->diag.p, 0, 128, c->stream));
                     diag = c->diag.as<uint64_t>();
                 }
                 uint64_t *L0 = c->lists.as<uint64_t>(), *C0 = c->clists.as<uint64_t>();
@@ -1015,8 +1015,8 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                             std::chrono::duration<double>(std::chrono::steady_clock::now() - th0).count() * 1e3,
                             nwin, (int)overlap);
                 if (diag_on) {
-                    uint64_t h[8] = {0};
-                    HIPCHK(hipMemcpyAsync(h, diag, 64, hipMemcpyDeviceToHost, c->stream));
+                    uint64_t h[16] = {0};
+                    HIPCHK(hipMemcpyAsync(h, diag, 128, hipMemcpyDeviceToHost, c->stream));
                     HIPCHK(hipStreamSynchronize(c->stream));
                     const double np = h[5] ? (double)h[5] : 1.0;
                     fprintf(stderr, geo.waves == 1 ? "QS_DIAG resolve cycles/pod: cand %.0f issue %.0f fresh %.0f wmax %.0f commit %.0f (pods %llu, G=%u E=%u epl=%u)\n"
@@ -1024,7 +1024,8 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                             h[0] / np, h[1] / np, h[2] / np, h[3] / np, h[4] / np,
                             (unsigned long long)h[5], geo.G, geo.E, geo.epl);
                     if (geo.waves == 4)
-                        fprintf(stderr, "QS_DIAG resolve4 pre-score cycles/pod: A %.0f C %.0f\n", h[6] / np, h[7] / np);
+                        fprintf(stderr, "QS_DIAG resolve4 pre-score cycles/pod: A %.0f C %.0f; per window: prologue %.0f epilogue %.0f\n",
+                                h[6] / np, h[7] / np, h[8] / (double)nwin, h[9] / (double)nwin);
                 }
             }
         }

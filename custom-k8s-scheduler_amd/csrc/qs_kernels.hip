@@ -1050,6 +1050,8 @@ __device__ __forceinline__ void la_resolve4_block(uint32_t *lds, const DevTable 
     constexpr bool NORM = (F & kFeatNorm) != 0;
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t t_start = DIAG ? diag_stamp() : 0ull;
+    uint64_t t_loop = 0;
     const uint32_t nwords = (t.n + 31) / 32;
     uint32_t *dirty = lds;
     char *base = (char *)(lds + ((nwords + 3) & ~3u));
@@ -1111,6 +1113,7 @@ __device__ __forceinline__ void la_resolve4_block(uint32_t *lds, const DevTable 
         uint32_t kdone = kend;  // normalizing profiles: the pod a stop hands to the resume kernel
         ResPub pv{0, 0xFFFFFFFFu, -1, -1, 0, {0, 0}};  // D produced it: kept in registers
         __syncthreads();  // prologue barrier (wave C publishes pod 0's candidates)
+        if (DIAG && lane == 0) atomicAdd((unsigned long long *)&diag[8], (unsigned long long)(diag_stamp() - t_start));
         for (uint32_t i = 0; i < kend; ++i) {
             QS_DIAG_BEGIN()
             const int par = i & 1, pp = par ^ 1;
@@ -1183,6 +1186,7 @@ __device__ __forceinline__ void la_resolve4_block(uint32_t *lds, const DevTable 
             QS_DIAG_END()
             __syncthreads();
         }
+        if (DIAG) t_loop = diag_stamp();
         if ((uint32_t)lane < kdone) {
             const uint32_t s = s0 + lane;
             out_node[s] = res_key ? (int32_t)key_node(res_key) : -1;
@@ -1409,6 +1413,7 @@ __device__ __forceinline__ void la_resolve4_block(uint32_t *lds, const DevTable 
         if (wv == 1) atomicAdd((unsigned long long *)&diag[6], (unsigned long long)dpart);
         if (wv == 3) atomicAdd((unsigned long long *)&diag[7], (unsigned long long)dpart);
         if (wv == 3) atomicAdd((unsigned long long *)&diag[4], (unsigned long long)dwait);
+        if (wv == 0) atomicAdd((unsigned long long *)&diag[9], (unsigned long long)(diag_stamp() - t_loop));
     }
     if (wv == 0) __syncthreads();  // pairs with the post-loop barrier of waves A/B and C
 #undef QS_DIAG_BEGIN
