@@ -1,3 +1,3 @@
 set -e
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
-QS_DIAG=1 timeout -k 10 120 python tools/kprof.py 2>&1 | tail -4
+timeout -k 10 120 python tools/run_workload.py tests/golden/workloads/qos_mix.yaml 500Nodes --check
