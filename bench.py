@@ -158,18 +158,20 @@ def pmc_traffic(kernel_prefix):
     return None
 
 
-def cpu_baseline(nodes, pods, n_nodes, n_pods, sample):
-    """Oracle (C restatement, 1 thread) on the first `sample` pods of the same stream."""
+def cpu_baseline(nodes, pods, n_nodes, n_pods, sample, threads=1):
+    """Oracle (C restatement) on the first `sample` pods of the same stream: 1 thread, or the
+    node-parallel OpenMP arm (SURVEY §8(d) arm 2: upstream's Parallelizer runs 16 workers)."""
     from oracle import oracle as O
 
     sub = qsched.pods_from_struct(pods[:sample])
     on = {k: v.copy() for k, v in nodes.items()}
     t0 = time.perf_counter()
-    O.schedule(on, sub, nthreads=1)
+    O.schedule(on, sub, nthreads=threads)
     dt = time.perf_counter() - t0
-    return {"value": round(sample / dt, 1), "unit": "pods/s", "cores": 1, "kind": "port",
+    how = "1 thread" if threads == 1 else f"{threads} OpenMP threads over the nodes of each pod"
+    return {"value": round(sample / dt, 1), "unit": "pods/s", "cores": threads, "kind": "port",
             "sample": f"first {sample} of the {n_pods:,} pods (QoS-sorted within the sample) onto "
-                      f"the empty {n_nodes:,}-node cluster, oracle/qs_oracle.c 1 thread, {dt:.2f} s",
+                      f"the empty {n_nodes:,}-node cluster, oracle/qs_oracle.c {how}, {dt:.2f} s",
             "evals_per_s": round(sample * n_nodes / dt, 1)}
 
 
@@ -311,6 +313,8 @@ def main():
         if cx.world == 1 and not a.no_cpu:
             out["cpu_baseline"] = cpu_baseline(m["nodes"], m["pods"], m["n_nodes"], m["n_pods"],
                                                a.cpu_sample)
+            out["cpu_baseline_parallel"] = cpu_baseline(m["nodes"], m["pods"], m["n_nodes"], m["n_pods"],
+                                                        a.cpu_sample, threads=16)
         print(json.dumps(out), flush=True)
     if cx.dist is not None:
         cx.dist.destroy_process_group()
