@@ -56,7 +56,8 @@ def parse():
     ap.add_argument("--workload", default="auto", choices=["auto", "config2", "config3"])
     ap.add_argument("--engine", default="auto")
     ap.add_argument("--lookahead", type=int, default=0)
-    ap.add_argument("--cpu-sample", type=int, default=20000, help="pods in the CPU-baseline sample")
+    ap.add_argument("--cpu-sample", type=int, default=0,
+                    help="pods in the CPU-baseline sample (0 = the whole stream, diffed against the GPU)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-config3", action="store_true", help="skip the N=1 config-3 reference point")
     ap.add_argument("--no-scan", action="store_true", help="skip the HBM-resident scan roofline leg")
@@ -158,21 +159,29 @@ def pmc_traffic(kernel_prefix):
     return None
 
 
-def cpu_baseline(nodes, pods, n_nodes, n_pods, sample, threads=1):
-    """Oracle (C restatement) on the first `sample` pods of the same stream: 1 thread, or the
-    node-parallel OpenMP arm (SURVEY §8(d) arm 2: upstream's Parallelizer runs 16 workers)."""
+def cpu_baseline(nodes, pods, n_nodes, n_pods, sample, threads=1, gpu_placement=None):
+    """Oracle (C restatement) on the same stream: 1 thread, or the node-parallel OpenMP arm
+    (SURVEY §8(d) arm 2: upstream's Parallelizer runs 16 workers).  sample = 0 runs the whole
+    stream, and its placements are diffed against the GPU's (`placements_match`)."""
     from oracle import oracle as O
 
+    whole = sample <= 0 or sample >= n_pods
+    sample = n_pods if whole else sample
     sub = qsched.pods_from_struct(pods[:sample])
     on = {k: v.copy() for k, v in nodes.items()}
     t0 = time.perf_counter()
-    O.schedule(on, sub, nthreads=threads)
+    placement, _, _ = O.schedule(on, sub, nthreads=threads)
     dt = time.perf_counter() - t0
     how = "1 thread" if threads == 1 else f"{threads} OpenMP threads over the nodes of each pod"
-    return {"value": round(sample / dt, 1), "unit": "pods/s", "cores": threads, "kind": "port",
-            "sample": f"first {sample} of the {n_pods:,} pods (QoS-sorted within the sample) onto "
-                      f"the empty {n_nodes:,}-node cluster, oracle/qs_oracle.c {how}, {dt:.2f} s",
-            "evals_per_s": round(sample * n_nodes / dt, 1)}
+    what = (f"the whole {n_pods:,}-pod stream" if whole else
+            f"first {sample} of the {n_pods:,} pods (QoS-sorted within the sample)")
+    out = {"value": round(sample / dt, 1), "unit": "pods/s", "cores": threads, "kind": "port",
+           "sample": f"{what} onto the empty {n_nodes:,}-node cluster, oracle/qs_oracle.c {how}, "
+                     f"{dt:.2f} s",
+           "evals_per_s": round(sample * n_nodes / dt, 1)}
+    if whole and gpu_placement is not None:
+        out["placements_match"] = bool(np.array_equal(placement, gpu_placement))
+    return out
 
 
 def measure(cx, a, workload, steps, warmup, with_diag=True):
@@ -209,6 +218,7 @@ def measure(cx, a, workload, steps, warmup, with_diag=True):
     value = n_pods * steps * ranks_work / elapsed
     out = {"value": value, "ms_per_step": elapsed / steps * 1e3, "engine": last["engine_used"],
            "unschedulable_frac": float((placement < 0).mean()), "n_nodes": n_nodes,
+           "placement": placement.copy(),
            "n_pods": n_pods, "desc": desc, "sharded": sharded, "nodes": nodes, "pods": pods,
            "replicas": ranks_work}
     if with_diag:
@@ -312,9 +322,10 @@ def main():
             out["scan"] = scan
         if cx.world == 1 and not a.no_cpu:
             out["cpu_baseline"] = cpu_baseline(m["nodes"], m["pods"], m["n_nodes"], m["n_pods"],
-                                               a.cpu_sample)
+                                               a.cpu_sample, gpu_placement=m["placement"])
             out["cpu_baseline_parallel"] = cpu_baseline(m["nodes"], m["pods"], m["n_nodes"], m["n_pods"],
-                                                        a.cpu_sample, threads=16)
+                                                        a.cpu_sample, threads=16,
+                                                        gpu_placement=m["placement"])
         print(json.dumps(out), flush=True)
     if cx.dist is not None:
         cx.dist.destroy_process_group()
