@@ -28,7 +28,7 @@ done
 cp $(find $OUT/trace -name '*kernel_stats.csv' | head -1) profiles/${TAG}_kernel_stats.csv
 python3 tools/summarize_pmc.py $(find $OUT/fetch -name '*counter_collection.csv' | head -1) \
     $(find $OUT/write -name '*counter_collection.csv' | head -1) profiles/${TAG}_pmc_summary.csv
-tail -1 $OUT/trace.log > profiles/${TAG}_bench_under_rocprof.json || true
+grep '^{' $OUT/trace.log | tail -1 > profiles/${TAG}_bench_under_rocprof.json || true
 # keep gpurun_out small: drop the raw traces (the summaries are what is committed)
 find $OUT -name '*.csv' -size +20M -delete
 ls -la profiles
