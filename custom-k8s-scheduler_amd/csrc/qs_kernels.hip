@@ -895,29 +895,34 @@ __global__ __launch_bounds__(64) void k_la_resolve_norm(
         } else {
             // exact rescan at the current state: slot rows from LDS, every other row from HBM
             if (act) { srow[lane] = dr; sx[lane] = dx; sidx[lane] = didx; }
-            auto row_at = [&](uint32_t idx, Row &r, RowX &x) {
-                if ((dirty[idx >> 5] >> (idx & 31)) & 1u) {
-                    uint32_t j = 0;
-                    while (j < nd && sidx[j] != idx) ++j;  // dirty => held by a slot
-                    r = srow[j];
-                    x = sx[j];
-                } else {
-                    r = load_row(t, idx);
-                    x = load_rowx<F>(t, idx);
+            // both passes keep U rows per lane in flight (one wave, dependent loads otherwise):
+            // every row is loaded unconditionally first, and only then are the few dirty ones
+            // (held by a slot, stale in HBM) replaced from LDS, so no branch or search loop sits
+            // between the loads and forces them to complete one by one
+            constexpr uint32_t U = 8;
+            auto rows_at = [&](uint32_t b0, Row (&r)[U], RowX (&x)[U]) {
+#pragma unroll
+                for (uint32_t u = 0; u < U; ++u) {
+                    const uint32_t idx = b0 + 64 * u < n ? b0 + 64 * u : 0u;
+                    r[u] = load_row(t, idx);
+                    x[u] = load_rowx<F>(t, idx);
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < U; ++u) {
+                    const uint32_t idx = b0 + 64 * u;
+                    if (idx < n && ((dirty[idx >> 5] >> (idx & 31)) & 1u)) {
+                        uint32_t j = 0;
+                        while (j < nd && sidx[j] != idx) ++j;  // dirty => held by a slot
+                        r[u] = srow[j];
+                        x[u] = sx[j];
+                    }
                 }
             };
-            // both passes keep U rows per lane in flight (one wave, dependent loads otherwise)
-            constexpr uint32_t U = 4;
             uint32_t mt = 0, ma = 0;
             for (uint32_t b0 = lane; b0 < n; b0 += 64 * U) {
                 Row r[U];
                 RowX x[U];
-#pragma unroll
-                for (uint32_t u = 0; u < U; ++u) {
-                    r[u] = empty_row();
-                    x[u] = RowX{};
-                    if (b0 + 64 * u < n) row_at(b0 + 64 * u, r[u], x[u]);
-                }
+                rows_at(b0, r, x);
 #pragma unroll
                 for (uint32_t u = 0; u < U; ++u) {
                     if (b0 + 64 * u < n && feasible<F>(r[u], x[u], p, px)) {
@@ -934,12 +939,7 @@ __global__ __launch_bounds__(64) void k_la_resolve_norm(
             for (uint32_t b0 = lane; b0 < n; b0 += 64 * U) {
                 Row r[U];
                 RowX x[U];
-#pragma unroll
-                for (uint32_t u = 0; u < U; ++u) {
-                    r[u] = empty_row();
-                    x[u] = RowX{};
-                    if (b0 + 64 * u < n) row_at(b0 + 64 * u, r[u], x[u]);
-                }
+                rows_at(b0, r, x);
 #pragma unroll
                 for (uint32_t u = 0; u < U; ++u) {
                     const uint32_t idx = b0 + 64 * u;
