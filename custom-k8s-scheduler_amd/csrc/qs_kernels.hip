@@ -768,9 +768,12 @@ __global__ __launch_bounds__(64) void k_la_resolve(DevTable t, const DPod *__res
 // maximum still holds whenever fewer of its holders than nf.ct / nf.ca are dirty AND infeasible
 // now; otherwise (rare: few holders left) the wave rescans every node at the current state for
 // the exact maxima and keys (`nfall` counts those pods).  Supports overlapped windows (dprev/dcur)
-// like k_la_resolve4.
+// like k_la_resolve4.  Four waves run the walk redundantly (identical lane state, LDS writes of
+// identical values, one barrier per pod) so that an exact rescan is spread over all four SIMDs;
+// only wave 0 writes results.
+constexpr uint32_t kResNormWaves = 4;
 template <uint32_t F, int EPL>
-__global__ __launch_bounds__(64) void k_la_resolve_norm(
+__global__ __launch_bounds__(64 * kResNormWaves) void k_la_resolve_norm(
     DevTable t, const DPod *__restrict__ pods, const DPodX *__restrict__ podx, DevCfg c,
     uint32_t s0, uint32_t P, uint32_t K, uint32_t GLp, uint32_t lr, LaShard sh,
     const uint64_t *__restrict__ lists, const NormInfo *__restrict__ norm,
@@ -778,7 +781,10 @@ __global__ __launch_bounds__(64) void k_la_resolve_norm(
     const uint32_t *__restrict__ dprev, uint32_t *__restrict__ dcur, unsigned long long *nfall,
     const uint32_t *__restrict__ rec) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    const int lane = threadIdx.x;
+    __shared__ uint32_t red_m[2 * kResNormWaves];  // per-wave rescan maxima (taint, affinity)
+    __shared__ uint64_t red_k[kResNormWaves];      // per-wave rescan best keys
+    const int lane = threadIdx.x & 63;
+    const uint32_t wid = threadIdx.x >> 6;
     // Resume mode (rec != nullptr, after the four-wave resolver of the same window): nothing to do
     // unless it stopped at pod rec[0]; then continue from there with its slots (rec[1] nodes at
     // rec[4..], rows already stored, won mask rec[2..3]) as the initial dirty set.
@@ -788,7 +794,7 @@ __global__ __launch_bounds__(64) void k_la_resolve_norm(
     if (rec) {
         const uint32_t stop = rec[0];
         if (stop == 0xFFFFFFFFu) return;
-        if (lane == 0 && nfall) atomicAdd(nfall + 1, 1ull);  // resumed windows (QS_NORM_DIAG)
+        if (threadIdx.x == 0 && nfall) atomicAdd(nfall + 1, 1ull);  // resumed windows (QS_NORM_DIAG)
         pbase = stop;
         s0 += stop;
         K -= stop;
@@ -919,7 +925,7 @@ __global__ __launch_bounds__(64) void k_la_resolve_norm(
                 }
             };
             uint32_t mt = 0, ma = 0;
-            for (uint32_t b0 = lane; b0 < n; b0 += 64 * U) {
+            for (uint32_t b0 = wid * 64 * U + lane; b0 < n; b0 += kResNormWaves * 64 * U) {
                 Row r[U];
                 RowX x[U];
                 rows_at(b0, r, x);
@@ -934,9 +940,16 @@ __global__ __launch_bounds__(64) void k_la_resolve_norm(
             }
             mt = (F & kFeatTaint) ? wave_max_u32(mt) : 0u;
             ma = (F & kFeatAffinity) ? wave_max_u32(ma) : 0u;
+            if (lane == 0) { red_m[2 * wid] = mt; red_m[2 * wid + 1] = ma; }
+            __syncthreads();
+#pragma unroll
+            for (uint32_t w = 0; w < kResNormWaves; ++w) {
+                mt = red_m[2 * w] > mt ? red_m[2 * w] : mt;
+                ma = red_m[2 * w + 1] > ma ? red_m[2 * w + 1] : ma;
+            }
             const double ymt2 = rcp_exact(mt), yma2 = rcp_exact(ma);
             uint64_t best = 0;
-            for (uint32_t b0 = lane; b0 < n; b0 += 64 * U) {
+            for (uint32_t b0 = wid * 64 * U + lane; b0 < n; b0 += kResNormWaves * 64 * U) {
                 Row r[U];
                 RowX x[U];
                 rows_at(b0, r, x);
@@ -949,8 +962,13 @@ __global__ __launch_bounds__(64) void k_la_resolve_norm(
                 }
             }
             ks = wave_max_u64(best);
-            if (lane == 0 && nfall) atomicAdd(nfall, 1ull);
+            if (lane == 0) red_k[wid] = ks;
+            __syncthreads();
+#pragma unroll
+            for (uint32_t w = 0; w < kResNormWaves; ++w) ks = red_k[w] > ks ? red_k[w] : ks;
+            if (threadIdx.x == 0 && nfall) atomicAdd(nfall, 1ull);
         }
+        __syncthreads();  // every wave has read this pod's dirty bits before any marks the winner
         if (ks) {
             const uint32_t win = key_node(ks);
             const uint64_t own = __ballot(act && didx == win);
@@ -984,7 +1002,9 @@ __global__ __launch_bounds__(64) void k_la_resolve_norm(
             res_key = ks;
             if (stamps) res_stamp = __builtin_amdgcn_s_memrealtime();
         }
+        __syncthreads();  // no wave overwrites stage / the rescan partials while another reads them
     }
+    if (wid != 0) return;
     if ((uint32_t)lane < kend) {
         const uint32_t s = s0 + lane;
         out_node[s] = res_key ? (int32_t)key_node(res_key) : -1;
@@ -1881,12 +1901,12 @@ static hipError_t la_window_f(const DevTable &t, const DPod *pods, const DPodX *
                     hipLaunchKernelGGL((k_la_resolve4<F, 1, false, false>), dim3(1), dim3(256), lds4n, stream, t, pods, c, s0, P,
                                        K, GLp, geo.lr, sh, bf.lists, on, ok, st, diag, bf.dprev, bf.dcur, podx, bf.norm, bf.rec);
                 QS_RET(hipGetLastError());
-                hipLaunchKernelGGL((k_la_resolve_norm<F, 1>), dim3(1), dim3(64), ldsn, stream, t, pods, podx, c, s0, P, K, GLp,
+                hipLaunchKernelGGL((k_la_resolve_norm<F, 1>), dim3(1), dim3(64 * kResNormWaves), ldsn, stream, t, pods, podx, c, s0, P, K, GLp,
                                    geo.lr, sh, bf.lists, bf.norm, on, ok, st, bf.dprev, bf.dcur, bf.nfall, bf.rec);
                 return hipGetLastError();
             }
             switch (geo.epl) {
-#define QS_RESN(EP) case EP: hipLaunchKernelGGL((k_la_resolve_norm<F, EP>), dim3(1), dim3(64), ldsn, stream, t, pods, podx, c, s0, P, K, GLp, geo.lr, sh, bf.lists, bf.norm, on, ok, st, bf.dprev, bf.dcur, bf.nfall, nullptr); break;
+#define QS_RESN(EP) case EP: hipLaunchKernelGGL((k_la_resolve_norm<F, EP>), dim3(1), dim3(64 * kResNormWaves), ldsn, stream, t, pods, podx, c, s0, P, K, GLp, geo.lr, sh, bf.lists, bf.norm, on, ok, st, bf.dprev, bf.dcur, bf.nfall, nullptr); break;
                 QS_RESN(1) QS_RESN(2) QS_RESN(4) QS_RESN(8) QS_RESN(16)
 #undef QS_RESN
                 default: return hipErrorInvalidValue;
