@@ -15,6 +15,13 @@
 namespace qs_host {
 
 constexpr int64_t kLimit = (1LL << 24) - 1;  // 24-bit multiplier range of the kernels (spec S10)
+// Wide layout (f64 memory columns in bytes): every memory quantity below 2^46 (64 TiB) keeps
+// (alloc - reqd) * 100 and the quotient-correction products exact in f64.
+constexpr int64_t kWideMemLimit = (1LL << 46) - 1;
+// Largest value a Requested / NonZeroRequested column may reach during a stream: int32 columns
+// (compact layout, cpu in both layouts) and f64-exact integers (wide memory).
+constexpr int64_t kGrowLimit32 = (1LL << 31) - 1;
+constexpr int64_t kGrowLimitF64 = (1LL << 53) - 1;
 // Tables at least this large also keep the SoA copy the SCAN engine streams (L2-resident below).
 constexpr uint32_t kSoaMinNodes = 1u << 16;
 // Tables up to this size also keep the batched-mode anti-affinity state (128 B of app bits per
@@ -86,6 +93,7 @@ struct qs_stream {
     qs_host::DevBuf d_pods, d_podx, d_node, d_key, d_stamp;
     bool ran = false;
     int shift = 0;
+    bool wide = false;  // pod records are DPodW (the table's wide layout) when set
     // LOOKAHEAD window sequence as an instantiated HIP graph, valid while gkey matches
     hipGraphExec_t gexec = nullptr;
     std::vector<uint8_t> gkey;
@@ -102,7 +110,8 @@ struct qs_ctx {
     hipStream_t stream2 = nullptr;  // lookahead select chain (overlapped windows)
     std::string err;
     qs_host::Mirror m;
-    int shift = 20;  // memory unit 2^shift bytes on the device
+    int shift = 20;  // memory unit 2^shift bytes on the device (compact layout)
+    bool wide = false;  // wide layout: f64 memory columns in bytes (DevTable::wrows)
     bool dev_valid = false;
     qs::DevTable dt{};
     qs::DevCfg dc{};
@@ -110,8 +119,12 @@ struct qs_ctx {
     qs_host::DevBuf soa;  // SoA int32 copy (kSCols x cap) when n >= soa_min_nodes
     bool soa_valid = false;  // SoA copy matches the rows (engines that update rows only clear it)
     qs_host::DevBuf tbl_saved;  // qs_table_save snapshot (whole allocation)
+    qs_host::Mirror m_saved;    // ... and the host mirror it corresponds to
     bool saved = false;
-    bool mirror_stale = false;  // device ran a stream since the last mirror sync
+    bool saved_wide = false;
+    int saved_shift = 20;
+    bool mirror_stale = false;  // device table changed since the last mirror sync
+    uint64_t device_faults = 0; // QS_EDEVICE results so far (each one drops the device table)
     qs_host::DevBuf diag;
     qs_host::DevBuf scratch, lists, clists, dio, npart, normi, nfall, nrec, bctrl, one_pod, one_podx, out_feas, out_score, out_total;
     uint32_t cap = 0;

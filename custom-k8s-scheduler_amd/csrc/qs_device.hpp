@@ -11,6 +11,8 @@
 #include <hip/hip_fp16.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace qs {
 
 constexpr int kWave = 64;
@@ -26,6 +28,18 @@ struct alignas(16) DRow {
     double yc, ym;           // RN_f64(1/alloc) (0 where alloc == 0)
     int32_t ae0, re0, ae1, re1;  // extended resources
 };
+// Wide layout (spec S10 fallback): used when the table's memory quantities cannot
+// be stored exactly as int32 multiples of 2^u bytes below 2^24 (odd-Ki kubelet allocatable,
+// decimal "100M" requests).  Memory columns are f64 integers in bytes (exact below 2^53); cpu,
+// pod counts and extended resources stay int32 as in DRow.  80 bytes.
+struct alignas(16) DRowW {
+    int32_t ac, rc, zc, np;      // q0
+    double am, rm;               // q1  Allocatable / Requested memory (bytes)
+    double zm, ym;               // q2  NonZeroRequested memory, RN_f64(1/am)
+    double yc;                   // q3  RN_f64(1/ac)
+    int32_t mp, pad;
+    int32_t ae0, re0, ae1, re1;  // q4  extended resources
+};
 struct alignas(16) DMask {
     uint64_t th, ts;         // taint_hard, taint_soft
     uint64_t lb0, lb1;       // label requirement bits
@@ -34,7 +48,7 @@ struct alignas(16) DMask {
 // SCAN engine and qs_score_pod stream 4 nodes per lane with one 16-byte load per column, so a
 // scan moves exactly the 32 algorithmic bytes per node.  Reciprocals are
 // recomputed in registers.  c[0] == nullptr: no SoA copy.
-enum : int { kSAc, kSAm, kSRc, kSRm, kSZc, kSZm, kSNp, kSMp, kSAe0, kSRe0, kSAe1, kSRe1, kSCols };
+enum SoaCol : int { kSAc, kSAm, kSRc, kSRm, kSZc, kSZm, kSNp, kSMp, kSAe0, kSRe0, kSAe1, kSRe1, kSCols };
 struct DevSoa {
     int32_t *c[kSCols];
 };
@@ -43,7 +57,8 @@ struct DevSoa {
 // nodes reads consecutive words), per (app, zone) a pod count.  apps == nullptr: not kept.
 constexpr uint32_t kMaxApps = 1024, kMaxZones = 64, kAppWords = kMaxApps / 32;
 struct DevTable {
-    DRow *rows;
+    DRow *rows;       // compact layout (nullptr in the wide layout)
+    DRowW *wrows;     // wide layout (nullptr in the compact layout)
     DMask *masks;
     uint32_t n;
     DevSoa soa;
@@ -53,7 +68,8 @@ struct DevTable {
     uint32_t cap;     // row capacity (stride of the app words)
 };
 
-enum : uint32_t { kFeatTaint = 1u, kFeatAffinity = 2u, kFeatExt = 4u };
+// kFeatWide selects the wide row / pod layout (DRowW, DPodW); the host sets it with kFeatExt.
+enum FeatBits : uint32_t { kFeatTaint = 1u, kFeatAffinity = 2u, kFeatExt = 4u, kFeatWide = 8u };
 
 // pod flags: bits 0-1 QoS, 4-6 required terms, 8-10 preferred terms, 12-13 anti-affinity kind,
 // 16-25 app group (spec S11)
@@ -83,6 +99,14 @@ struct alignas(16) DPod {
     uint16_t wfit, wbal;
     uint32_t flags;           // bits 0-1 qos, 4-6 n_req_terms, 8-10 n_pref_terms
 };
+// Pod record of the wide layout (48 B): memory requests as f64 bytes.
+struct alignas(16) DPodW {
+    int32_t rc, zc, re0, re1;
+    uint16_t wfit, wbal;
+    uint32_t flags;
+    uint32_t pad0, pad1;
+    double rm, zm;
+};
 // Config-4 extension record (176 B), only read when kFeatTaint|kFeatAffinity.
 struct alignas(16) DPodX {
     uint64_t tol_hard, tol_soft, sel0, sel1;
@@ -107,28 +131,53 @@ __device__ __forceinline__ T load_vgpr(const T *p) {
     return out;
 }
 
-// One node row in registers.
+// One node row in registers (compact layout).
 struct Row {
     int32_t ac, am, rc, rm, zc, zm, np, mp;
     double yc, ym;
+};
+// One node row in registers (wide layout: memory as f64 bytes).
+struct RowW {
+    int32_t ac, rc, zc, np, mp;
+    double am, rm, zm, yc, ym;
 };
 struct RowX {
     int32_t ae0, re0, ae1, re1;
     uint64_t th, ts, lb0, lb1;
 };
+// Register row / pod record types of a feature set (kFeatWide picks the wide layout).
+template <uint32_t F>
+using RowT = typename std::conditional<(F & kFeatWide) != 0, RowW, Row>::type;
+template <uint32_t F>
+using PodT = typename std::conditional<(F & kFeatWide) != 0, DPodW, DPod>::type;
 
-__device__ __forceinline__ Row load_row(const DevTable &t, uint32_t i) {
-    const int4 *q = reinterpret_cast<const int4 *>(t.rows + i);
-    const int4 a = q[0], b = q[1];
-    const double2 y = reinterpret_cast<const double2 *>(t.rows + i)[2];
-    Row r;
-    r.ac = a.x; r.am = a.y; r.rc = a.z; r.rm = a.w;
-    r.zc = b.x; r.zm = b.y; r.np = b.z; r.mp = b.w;
-    r.yc = y.x; r.ym = y.y;
-    return r;
+template <uint32_t F>
+__device__ __forceinline__ RowT<F> load_row(const DevTable &t, uint32_t i) {
+    if constexpr ((F & kFeatWide) != 0) {
+        const int4 *q = reinterpret_cast<const int4 *>(t.wrows + i);
+        const int4 a = q[0], d = q[3];
+        const double2 *y = reinterpret_cast<const double2 *>(t.wrows + i);
+        const double2 b = y[1], c = y[2];
+        RowW r;
+        r.ac = a.x; r.rc = a.y; r.zc = a.z; r.np = a.w;
+        r.am = b.x; r.rm = b.y; r.zm = c.x; r.ym = c.y;
+        r.yc = __builtin_bit_cast(double, ((uint64_t)(uint32_t)d.y << 32) | (uint32_t)d.x);
+        r.mp = d.z;
+        return r;
+    } else {
+        const int4 *q = reinterpret_cast<const int4 *>(t.rows + i);
+        const int4 a = q[0], b = q[1];
+        const double2 y = reinterpret_cast<const double2 *>(t.rows + i)[2];
+        Row r;
+        r.ac = a.x; r.am = a.y; r.rc = a.z; r.rm = a.w;
+        r.zc = b.x; r.zm = b.y; r.np = b.z; r.mp = b.w;
+        r.yc = y.x; r.ym = y.y;
+        return r;
+    }
 }
-__device__ __forceinline__ Row empty_row() {
-    Row r;
+template <uint32_t F>
+__device__ __forceinline__ RowT<F> empty_row() {
+    RowT<F> r;
     r.ac = r.am = r.rc = r.rm = r.zc = r.zm = 0;
     r.np = 0; r.mp = 0;  // pods + 1 > max_pods -> never feasible
     r.yc = r.ym = 0.0;
@@ -137,6 +186,13 @@ __device__ __forceinline__ Row empty_row() {
 // Per-field select (a ternary on whole structs is lowered through scratch memory).
 __device__ __forceinline__ Row sel_row(bool c, const Row &a, const Row &b) {
     Row r;
+    r.ac = c ? a.ac : b.ac; r.am = c ? a.am : b.am; r.rc = c ? a.rc : b.rc; r.rm = c ? a.rm : b.rm;
+    r.zc = c ? a.zc : b.zc; r.zm = c ? a.zm : b.zm; r.np = c ? a.np : b.np; r.mp = c ? a.mp : b.mp;
+    r.yc = c ? a.yc : b.yc; r.ym = c ? a.ym : b.ym;
+    return r;
+}
+__device__ __forceinline__ RowW sel_row(bool c, const RowW &a, const RowW &b) {
+    RowW r;
     r.ac = c ? a.ac : b.ac; r.am = c ? a.am : b.am; r.rc = c ? a.rc : b.rc; r.rm = c ? a.rm : b.rm;
     r.zc = c ? a.zc : b.zc; r.zm = c ? a.zm : b.zm; r.np = c ? a.np : b.np; r.mp = c ? a.mp : b.mp;
     r.yc = c ? a.yc : b.yc; r.ym = c ? a.ym : b.ym;
@@ -155,7 +211,8 @@ __device__ __forceinline__ RowX load_rowx(const DevTable &t, uint32_t i) {
     x.ae0 = x.re0 = x.ae1 = x.re1 = 0;
     x.th = x.ts = x.lb0 = x.lb1 = 0;
     if (F & kFeatExt) {
-        const int4 e = reinterpret_cast<const int4 *>(t.rows + i)[3];
+        const int4 e = (F & kFeatWide) ? reinterpret_cast<const int4 *>(t.wrows + i)[4]
+                                       : reinterpret_cast<const int4 *>(t.rows + i)[3];
         x.ae0 = e.x; x.re0 = e.y; x.ae1 = e.z; x.re1 = e.w;
     }
     if (F & (kFeatTaint | kFeatAffinity)) {
@@ -164,22 +221,33 @@ __device__ __forceinline__ RowX load_rowx(const DevTable &t, uint32_t i) {
     }
     return x;
 }
-__device__ __forceinline__ void store_dyn(const DevTable &t, uint32_t i, const Row &r) {
-    int32_t *w = reinterpret_cast<int32_t *>(t.rows + i);
-    *reinterpret_cast<int2 *>(w + 2) = make_int2(r.rc, r.rm);
-    *reinterpret_cast<int2 *>(w + 4) = make_int2(r.zc, r.zm);
-    w[6] = r.np;
+template <uint32_t F>
+__device__ __forceinline__ void store_dyn(const DevTable &t, uint32_t i, const RowT<F> &r) {
+    if constexpr ((F & kFeatWide) != 0) {
+        int32_t *w = reinterpret_cast<int32_t *>(t.wrows + i);
+        w[1] = r.rc; w[2] = r.zc; w[3] = r.np;
+        double *d = reinterpret_cast<double *>(t.wrows + i);
+        d[3] = r.rm;  // q1.y
+        d[4] = r.zm;  // q2.x
+    } else {
+        int32_t *w = reinterpret_cast<int32_t *>(t.rows + i);
+        *reinterpret_cast<int2 *>(w + 2) = make_int2(r.rc, r.rm);
+        *reinterpret_cast<int2 *>(w + 4) = make_int2(r.zc, r.zm);
+        w[6] = r.np;
+    }
 }
 template <uint32_t F>
 __device__ __forceinline__ void store_dynx(const DevTable &t, uint32_t i, const RowX &x) {
     if (F & kFeatExt) {
-        int32_t *w = reinterpret_cast<int32_t *>(t.rows + i);
-        w[13] = x.re0;
-        w[15] = x.re1;
+        int32_t *w = (F & kFeatWide) ? reinterpret_cast<int32_t *>(t.wrows + i) + 16
+                                     : reinterpret_cast<int32_t *>(t.rows + i) + 12;
+        w[1] = x.re0;
+        w[3] = x.re1;
     }
 }
 // Reserve (spec S7; UP framework/types.go#NodeInfo.update(+1))
-__device__ __forceinline__ void reserve(Row &r, RowX &x, const DPod &p, int sign) {
+template <class R, class P>
+__device__ __forceinline__ void reserve(R &r, RowX &x, const P &p, int sign) {
     r.rc += sign * p.rc; r.rm += sign * p.rm;
     r.zc += sign * p.zc; r.zm += sign * p.zm;
     r.np += sign;
@@ -188,8 +256,8 @@ __device__ __forceinline__ void reserve(Row &r, RowX &x, const DPod &p, int sign
 
 // ---- spec S4: NodeResourcesFit.Filter (UP noderesources/fit.go#fitsRequest) ------------------
 // Per-resource checks are skipped for zero requests, which also covers the all-zero early return.
-template <uint32_t F>
-__device__ __forceinline__ bool fits(const Row &r, const RowX &x, const DPod &p) {
+template <uint32_t F, class R, class P>
+__device__ __forceinline__ bool fits(const R &r, const RowX &x, const P &p) {
     bool ok = r.np < r.mp;
     ok &= (p.rc <= 0) | (p.rc <= r.ac - r.rc);
     ok &= (p.rm <= 0) | (p.rm <= r.am - r.rm);
@@ -202,8 +270,8 @@ __device__ __forceinline__ bool fits(const Row &r, const RowX &x, const DPod &p)
 __device__ __forceinline__ bool subset128(uint64_t m0, uint64_t m1, uint64_t b0, uint64_t b1) {
     return ((m0 & ~b0) | (m1 & ~b1)) == 0;
 }
-template <uint32_t F>
-__device__ __forceinline__ bool feasible(const Row &r, const RowX &x, const DPod &p, const DPodX &px) {
+template <uint32_t F, class R, class P>
+__device__ __forceinline__ bool feasible(const R &r, const RowX &x, const P &p, const DPodX &px) {
     bool ok = fits<F>(r, x, p);
     if (F & kFeatTaint) ok &= (x.th & ~px.tol_hard) == 0;  // UP tainttoleration#Filter
     if (F & kFeatAffinity) {                                 // UP nodeaffinity#Filter
@@ -222,7 +290,8 @@ __device__ __forceinline__ uint32_t taint_raw(const RowX &x, const DPodX &px) {
     return (uint32_t)__popcll(x.ts & ~px.tol_soft);
 }
 // raw NodeAffinity score: weights of matching preferred terms (UP nodeaffinity#Score)
-__device__ __forceinline__ uint32_t affinity_raw(const RowX &x, const DPod &p, const DPodX &px) {
+template <class P>
+__device__ __forceinline__ uint32_t affinity_raw(const RowX &x, const P &p, const DPodX &px) {
     const uint32_t nt = (p.flags >> 8) & 7u;
     uint32_t s = 0;
 #pragma unroll
@@ -254,13 +323,30 @@ __device__ __forceinline__ double fraction(int32_t a, int32_t r, double y) {
     return r >= a ? 1.0 : q;
 }
 
+// Wide layout (memory in f64 bytes, every value < 2^46, so (a - r) * 100 and q * a are exact):
+// floor((a - reqd) * 100 / a) from the f64 quotient and a one-step integer correction (SURVEY.md
+// A.4 note): n * RN(1/a) is within 100 * 2^-52 of n / a, i.e. within one of the floor.
+__device__ __forceinline__ uint32_t least_requested_w(double a, double reqd, double ya) {
+    const double rq = reqd < a ? reqd : a;
+    const double n = (a - rq) * 100.0;
+    double q = __builtin_trunc(n * ya);
+    if (q * a > n) q -= 1.0;
+    else if ((q + 1.0) * a <= n) q += 1.0;
+    return reqd > a ? 0u : (uint32_t)q;
+}
+// min(RN(r / a), 1): IEEE division (correctly rounded; -ffp-contract=off, no fast-math)
+__device__ __forceinline__ double fraction_w(double a, double r) { return r >= a ? 1.0 : r / a; }
+
 // ---- spec S5/S6: QoS-weighted total of one feasible node ------------------------------------
 // LeastAllocated (UP least_allocated.go#leastResourceScorer), NonZeroRequested + pod nz.
 // Branch-free: a resource with alloc == 0 contributes weight 0 (its score is 0 as well).
-__device__ __forceinline__ uint32_t la_score(const Row &r, const DPod &p, const DevCfg &c) {
+template <class R, class P>
+__device__ __forceinline__ uint32_t la_score(const R &r, const P &p, const DevCfg &c) {
     const bool hc = r.ac != 0, hm = r.am != 0;
     const uint32_t sc_c = least_requested(r.ac, r.zc + p.zc, r.yc);
-    const uint32_t sc_m = least_requested(r.am, r.zm + p.zm, r.ym);
+    uint32_t sc_m;
+    if constexpr (std::is_same<R, RowW>::value) sc_m = least_requested_w(r.am, r.zm + p.zm, r.ym);
+    else sc_m = least_requested(r.am, r.zm + p.zm, r.ym);
     const uint32_t wce = hc ? (uint32_t)c.wc : 0u, wme = hm ? (uint32_t)c.wm : 0u;
     const uint32_t num = __umul24(sc_c, wce) + __umul24(sc_m, wme);
     const uint32_t den = wce + wme;
@@ -274,10 +360,13 @@ __device__ __forceinline__ uint32_t la_score(const Row &r, const DPod &p, const 
     return den ? floor_div(num, yd) : 0u;
 }
 // BalancedAllocation (UP balanced_allocation.go#balancedResourceScorer), Requested + pod req
-__device__ __forceinline__ uint32_t ba_score(const Row &r, const DPod &p, const DevCfg &c) {
+template <class R, class P>
+__device__ __forceinline__ uint32_t ba_score(const R &r, const P &p, const DevCfg &c) {
     const bool hc = r.ac != 0, hm = r.am != 0;
     const double f0 = fraction(r.ac, r.rc + p.rc, r.yc);
-    const double f1 = fraction(r.am, r.rm + p.rm, r.ym);
+    double f1;
+    if constexpr (std::is_same<R, RowW>::value) f1 = fraction_w(r.am, r.rm + p.rm);
+    else f1 = fraction(r.am, r.rm + p.rm, r.ym);
     double sd = 0.0;
     if (hc & hm) sd = __builtin_fabs((f0 - f1) / 2);
     const double scaled = (1 - sd) * 100.0;
@@ -286,8 +375,8 @@ __device__ __forceinline__ uint32_t ba_score(const Row &r, const DPod &p, const 
     return ba;
 }
 
-template <uint32_t F>
-__device__ __forceinline__ uint32_t node_total(const Row &r, const RowX &x, const DPod &p,
+template <uint32_t F, class R, class P>
+__device__ __forceinline__ uint32_t node_total(const R &r, const RowX &x, const P &p,
                                                const DPodX &px, const DevCfg &c, uint32_t mt,
                                                double ymt, uint32_t ma, double yma, uint32_t *sc) {
     const uint32_t la = la_score(r, p, c), ba = ba_score(r, p, c);

@@ -84,38 +84,59 @@ int table_shift(const Mirror &m) {
     return s;
 }
 
-void check_range(int64_t v, const char *what, uint32_t i) {
-    if (v < 0 || v > kLimit)
-        fail(QS_EINVAL, std::string("node ") + std::to_string(i) + ": " + what +
-                            " outside the device range [0, 2^24) after compaction");
+void check_range(int64_t v, const char *what, uint32_t i, int64_t limit = kLimit) {
+    if (v < 0 || v > limit)
+        fail(QS_EINVAL, std::string("node ") + std::to_string(i) + ": " + what + " = " + std::to_string(v) +
+                            " outside the device range [0, " + std::to_string(limit) + "]");
 }
 
-HostRow compact_row(const Mirror &m, uint32_t i, int shift) {
-    HostRow r{};
+// Value ranges every layout needs (cpu, counts and extended resources are int32 columns in both;
+// memory is bounded by the wide layout's f64 exactness, kWideMemLimit).
+void check_row_values(const Mirror &m, uint32_t i) {
     check_range(m.ac[i], "alloc_cpu", i);
     check_range(m.rc[i], "req_cpu", i);
     check_range(m.zc[i], "nz_cpu", i);
-    check_range(m.am[i] >> shift, "alloc_mem", i);
-    check_range(m.rm[i] >> shift, "req_mem", i);
-    check_range(m.zm[i] >> shift, "nz_mem", i);
     check_range(m.np[i], "pods", i);
     check_range(m.mp[i], "max_pods", i);
-    if (m.zone[i] < 0 || m.zone[i] >= (int32_t)kMaxZones)
-        fail(QS_EINVAL, "node " + std::to_string(i) + ": zone outside [0, 64)");
-    r.zone = m.zone[i];
-    r.ac = (int32_t)m.ac[i];
-    r.am = (int32_t)(m.am[i] >> shift);
-    r.rc = (int32_t)m.rc[i];
-    r.rm = (int32_t)(m.rm[i] >> shift);
-    r.zc = (int32_t)m.zc[i];
-    r.zm = (int32_t)(m.zm[i] >> shift);
-    r.np = (int32_t)m.np[i];
-    r.mp = (int32_t)m.mp[i];
-    r.yc = r.ac ? 1.0 / (double)r.ac : 0.0;  // RN(1/alloc): IEEE division on the host
-    r.ym = r.am ? 1.0 / (double)r.am : 0.0;
+    check_range(m.am[i], "alloc_mem", i, kWideMemLimit);
+    check_range(m.rm[i], "req_mem", i, kWideMemLimit);
+    check_range(m.zm[i], "nz_mem", i, kWideMemLimit);
     for (int k = 0; k < QS_MAX_EXT; k++) {
         check_range(m.ae[(size_t)i * QS_MAX_EXT + k], "alloc_ext", i);
         check_range(m.re[(size_t)i * QS_MAX_EXT + k], "req_ext", i);
+    }
+    if (m.zone[i] < 0 || m.zone[i] >= (int32_t)kMaxZones)
+        fail(QS_EINVAL, "node " + std::to_string(i) + ": zone outside [0, 64)");
+}
+
+// Compact layout possible at this shift: every memory quantity is a multiple of 2^shift (true by
+// construction of the shift) and below 2^24 units.
+bool row_compact_ok(const Mirror &m, uint32_t i, int shift) {
+    return (m.am[i] >> shift) <= kLimit && (m.rm[i] >> shift) <= kLimit && (m.zm[i] >> shift) <= kLimit;
+}
+
+HostRow compact_row(const Mirror &m, uint32_t i, int shift, bool wide) {
+    HostRow r{};
+    check_row_values(m, i);
+    if (!wide && !row_compact_ok(m, i, shift))
+        fail(QS_EINVAL, "node " + std::to_string(i) + ": memory outside the compact layout");  // cannot happen
+    r.zone = m.zone[i];
+    r.ac = (int32_t)m.ac[i];
+    r.rc = (int32_t)m.rc[i];
+    r.zc = (int32_t)m.zc[i];
+    r.np = (int32_t)m.np[i];
+    r.mp = (int32_t)m.mp[i];
+    r.yc = r.ac ? 1.0 / (double)r.ac : 0.0;  // RN(1/alloc): IEEE division on the host
+    if (wide) {
+        r.wam = (double)m.am[i];
+        r.wrm = (double)m.rm[i];
+        r.wzm = (double)m.zm[i];
+        r.ym = m.am[i] ? 1.0 / r.wam : 0.0;
+    } else {
+        r.am = (int32_t)(m.am[i] >> shift);
+        r.rm = (int32_t)(m.rm[i] >> shift);
+        r.zm = (int32_t)(m.zm[i] >> shift);
+        r.ym = r.am ? 1.0 / (double)r.am : 0.0;
     }
     r.ae0 = (int32_t)m.ae[(size_t)i * QS_MAX_EXT + 0];
     r.ae1 = (int32_t)m.ae[(size_t)i * QS_MAX_EXT + 1];
@@ -128,19 +149,23 @@ HostRow compact_row(const Mirror &m, uint32_t i, int shift) {
     return r;
 }
 
-// Table layout inside ctx->tbl: cap rows of 64 B, then cap mask rows of 32 B.  Returns the size;
-// assigns the pointers when base != nullptr.
-// Table layout inside ctx->tbl: cap rows of 64 B, cap mask rows of 32 B, cap zone ids, then (tables
-// up to kAaMaxNodes) the anti-affinity state: kAppWords x cap app words and the (app, zone)
-// counts.  Returns the size; assigns the pointers when base != nullptr.
-size_t carve(DevTable &t, uint32_t cap, char *base) {
+// Table layout inside ctx->tbl: cap rows (64 B compact, 80 B wide), cap mask rows of 32 B, cap zone
+// ids, then (tables up to kAaMaxNodes) the anti-affinity state: kAppWords x cap app words and the
+// (app, zone) counts.  Returns the size; assigns the pointers when base != nullptr.
+size_t carve(DevTable &t, uint32_t cap, bool wide, char *base) {
     size_t off = 0;
     auto take = [&](size_t bytes) {
         char *p = base ? base + off : nullptr;
         off += (bytes + 255) & ~(size_t)255;
         return p;
     };
-    t.rows = (DRow *)take((size_t)cap * sizeof(DRow));
+    if (wide) {
+        t.rows = nullptr;
+        t.wrows = (DRowW *)take((size_t)cap * sizeof(DRowW));
+    } else {
+        t.wrows = nullptr;
+        t.rows = (DRow *)take((size_t)cap * sizeof(DRow));
+    }
     t.masks = (DMask *)take((size_t)cap * sizeof(DMask));
     t.zone = (int32_t *)take((size_t)cap * 4);
     t.cap = cap;
@@ -167,24 +192,37 @@ uint32_t soa_min_nodes(const qs_ctx *c) {
     return v == 0 ? kSoaMinNodes : (v < 0 ? 0xFFFFFFFFu : (uint32_t)v);
 }
 
-// Upload the whole mirror (compacted) to the device.
+DRowW to_drow_wide(const HostRow &r) {
+    DRowW d;
+    d.ac = r.ac; d.rc = r.rc; d.zc = r.zc; d.np = r.np;
+    d.am = r.wam; d.rm = r.wrm; d.zm = r.wzm; d.ym = r.ym;
+    d.yc = r.yc; d.mp = r.mp; d.pad = 0;
+    d.ae0 = r.ae0; d.re0 = r.re0; d.ae1 = r.ae1; d.re1 = r.re1;
+    return d;
+}
+
+// Upload the whole mirror to the device in the context's layout (c->wide, c->shift).
 void upload_table(qs_ctx *c) {
     const uint32_t n = c->m.n;
     const uint32_t cap = std::max<uint32_t>(64, (n + 63) & ~63u);
-    if (cap > c->cap || !c->tbl.p) {
-        c->tbl.ensure(carve(c->dt, cap, nullptr));
-        c->cap = cap;
+    const bool wide = c->wide;
+    const size_t need = carve(c->dt, cap, wide, nullptr);
+    if (cap > c->cap || !c->tbl.p || need > c->tbl.bytes) {
+        c->tbl.ensure(need);
+        c->cap = std::max(cap, c->cap);
     }
-    carve(c->dt, c->cap, c->tbl.as<char>());
+    carve(c->dt, c->cap, wide, c->tbl.as<char>());
     c->dt.n = n;
-    const bool soa = n > 0 && n >= soa_min_nodes(c);
+    const bool soa = !wide && n > 0 && n >= soa_min_nodes(c);
     std::memset(&c->dt.soa, 0, sizeof c->dt.soa);
-    std::vector<DRow> rows(n);
+    std::vector<DRow> rows(wide ? 0 : n);
+    std::vector<DRowW> wrows(wide ? n : 0);
     std::vector<DMask> masks(n);
     std::vector<int32_t> cols(soa ? (size_t)kSCols * c->cap : 0, 0);  // zero padding: infeasible
     for (uint32_t i = 0; i < n; i++) {
-        const HostRow r = compact_row(c->m, i, c->shift);
-        rows[i] = to_drow(r);
+        const HostRow r = compact_row(c->m, i, c->shift, wide);
+        if (wide) wrows[i] = to_drow_wide(r);
+        else rows[i] = to_drow(r);
         masks[i] = DMask{r.th, r.ts, r.lb0, r.lb1};
         if (soa) {
             const int32_t f[kSCols] = {r.ac, r.am, r.rc, r.rm, r.zc, r.zm, r.np, r.mp, r.ae0, r.re0, r.ae1, r.re1};
@@ -192,7 +230,8 @@ void upload_table(qs_ctx *c) {
         }
     }
     if (n) {
-        HIPCHK(hipMemcpyAsync(c->dt.rows, rows.data(), n * sizeof(DRow), hipMemcpyHostToDevice, c->stream));
+        if (wide) HIPCHK(hipMemcpyAsync(c->dt.wrows, wrows.data(), n * sizeof(DRowW), hipMemcpyHostToDevice, c->stream));
+        else HIPCHK(hipMemcpyAsync(c->dt.rows, rows.data(), n * sizeof(DRow), hipMemcpyHostToDevice, c->stream));
         HIPCHK(hipMemcpyAsync(c->dt.masks, masks.data(), n * sizeof(DMask), hipMemcpyHostToDevice, c->stream));
         HIPCHK(hipMemcpyAsync(c->dt.zone, c->m.zone.data(), n * 4, hipMemcpyHostToDevice, c->stream));
     }
@@ -208,6 +247,7 @@ void upload_table(qs_ctx *c) {
     HIPCHK(hipStreamSynchronize(c->stream));
     c->dev_valid = true;
     c->soa_valid = soa;
+    c->mirror_stale = false;
 }
 
 // The SCAN engine reads the SoA copy: rebuild it after engines that only update the rows.
@@ -219,30 +259,45 @@ void ensure_soa(qs_ctx *c) {
 
 void push_row(qs_ctx *c, uint32_t i) {
     if (!c->dev_valid) return;
-    const HostRow r = compact_row(c->m, i, c->shift);
+    const HostRow r = compact_row(c->m, i, c->shift, c->wide);
     hipLaunchKernelGGL(k_set_row, dim3(1), dim3(1), 0, c->stream, c->dt, i, r,
                        kFeatExt | kFeatTaint | kFeatAffinity);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->stream));
 }
 
-// Refresh the dynamic mirror columns from the device after stream runs (values are multiples of
-// 2^shift by construction, so decompaction is exact).
+// Refresh the dynamic mirror columns from the device after stream runs (compact values are
+// multiples of 2^shift by construction and wide values are exact f64 integers, so decoding is exact).
 void sync_mirror(qs_ctx *c) {
     if (!c->mirror_stale || !c->dev_valid) return;
     const uint32_t n = c->m.n;
-    std::vector<DRow> rows(n);
-    if (n) HIPCHK(hipMemcpyAsync(rows.data(), c->dt.rows, n * sizeof(DRow), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
     Mirror &m = c->m;
-    for (uint32_t i = 0; i < n; i++) {
-        m.rc[i] = rows[i].rc;
-        m.rm[i] = (int64_t)rows[i].rm << c->shift;
-        m.zc[i] = rows[i].zc;
-        m.zm[i] = (int64_t)rows[i].zm << c->shift;
-        m.np[i] = rows[i].np;
-        m.re[(size_t)i * QS_MAX_EXT] = rows[i].re0;
-        m.re[(size_t)i * QS_MAX_EXT + 1] = rows[i].re1;
+    if (c->wide) {
+        std::vector<DRowW> rows(n);
+        if (n) HIPCHK(hipMemcpyAsync(rows.data(), c->dt.wrows, n * sizeof(DRowW), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        for (uint32_t i = 0; i < n; i++) {
+            m.rc[i] = rows[i].rc;
+            m.rm[i] = (int64_t)rows[i].rm;
+            m.zc[i] = rows[i].zc;
+            m.zm[i] = (int64_t)rows[i].zm;
+            m.np[i] = rows[i].np;
+            m.re[(size_t)i * QS_MAX_EXT] = rows[i].re0;
+            m.re[(size_t)i * QS_MAX_EXT + 1] = rows[i].re1;
+        }
+    } else {
+        std::vector<DRow> rows(n);
+        if (n) HIPCHK(hipMemcpyAsync(rows.data(), c->dt.rows, n * sizeof(DRow), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        for (uint32_t i = 0; i < n; i++) {
+            m.rc[i] = rows[i].rc;
+            m.rm[i] = (int64_t)rows[i].rm << c->shift;
+            m.zc[i] = rows[i].zc;
+            m.zm[i] = (int64_t)rows[i].zm << c->shift;
+            m.np[i] = rows[i].np;
+            m.re[(size_t)i * QS_MAX_EXT] = rows[i].re0;
+            m.re[(size_t)i * QS_MAX_EXT + 1] = rows[i].re1;
+        }
     }
     c->mirror_stale = false;
 }
@@ -258,6 +313,7 @@ void check_pod(const qs_pod &p, uint32_t j) {
     for (int k = 0; k < QS_MAX_EXT; k++)
         if (p.req_ext[k] < 0 || p.req_ext[k] > kLimit) bad("req_ext out of range");
     if (p.req_cpu > kLimit || p.nz_cpu > kLimit) bad("cpu request out of range");
+    if (p.req_mem > kWideMemLimit || p.nz_mem > kWideMemLimit) bad("memory request above 2^46 bytes");
     if (p.n_req_terms < 0 || p.n_req_terms > QS_MAX_TERMS || p.n_pref_terms < 0 ||
         p.n_pref_terms > QS_MAX_TERMS)
         bad("term count out of range");
@@ -267,10 +323,33 @@ void check_pod(const qs_pod &p, uint32_t j) {
     if (p.anti_affinity < QS_AA_NONE || p.anti_affinity > QS_AA_ZONE) bad("anti_affinity must be 0..2");
 }
 
-DPod compact_pod(const qs_ctx *c, const qs_pod &p, uint32_t j, int shift) {
+uint32_t pod_flags(const qs_pod &p) {
+    return (uint32_t)p.qos | ((uint32_t)p.n_req_terms << 4) | ((uint32_t)p.n_pref_terms << 8) |
+           ((uint32_t)p.anti_affinity << 12) | ((uint32_t)p.app << 16);
+}
+
+// Device pod record in the context's layout: DPod (compact, memory in 2^shift units) or DPodW
+// (wide, memory in f64 bytes).  ensure_layout has already checked the ranges.
+size_t pod_record_bytes(bool wide) { return wide ? sizeof(DPodW) : sizeof(DPod); }
+
+void compact_pod(const qs_ctx *c, const qs_pod &p, uint32_t j, int shift, bool wide, void *dst) {
     check_pod(p, j);
+    if (wide) {
+        DPodW d{};
+        d.rc = (int32_t)p.req_cpu;
+        d.zc = (int32_t)p.nz_cpu;
+        d.rm = (double)p.req_mem;
+        d.zm = (double)p.nz_mem;
+        d.re0 = (int32_t)p.req_ext[0];
+        d.re1 = (int32_t)p.req_ext[1];
+        d.wfit = (uint16_t)c->cfg.w_fit[p.qos];
+        d.wbal = (uint16_t)c->cfg.w_bal[p.qos];
+        d.flags = pod_flags(p);
+        std::memcpy(dst, &d, sizeof d);
+        return;
+    }
     if ((p.req_mem >> shift) > kLimit || (p.nz_mem >> shift) > kLimit)
-        fail(QS_EINVAL, "pod " + std::to_string(j) + ": memory request out of the device range");
+        fail(QS_EINVAL, "pod " + std::to_string(j) + ": memory request out of the compact range");  // cannot happen
     DPod d{};
     d.rc = (int32_t)p.req_cpu;
     d.rm = (int32_t)(p.req_mem >> shift);
@@ -280,9 +359,8 @@ DPod compact_pod(const qs_ctx *c, const qs_pod &p, uint32_t j, int shift) {
     d.re1 = (int32_t)p.req_ext[1];
     d.wfit = (uint16_t)c->cfg.w_fit[p.qos];
     d.wbal = (uint16_t)c->cfg.w_bal[p.qos];
-    d.flags = (uint32_t)p.qos | ((uint32_t)p.n_req_terms << 4) | ((uint32_t)p.n_pref_terms << 8) |
-              ((uint32_t)p.anti_affinity << 12) | ((uint32_t)p.app << 16);
-    return d;
+    d.flags = pod_flags(p);
+    std::memcpy(dst, &d, sizeof d);
 }
 
 DPodX compact_podx(const qs_pod &p) {
@@ -322,13 +400,83 @@ void mirror_reserve(Mirror &m, uint32_t i, const qs_pod &p, int sign) {
     m.np[i] += sign;
 }
 
-void ensure_shift(qs_ctx *c, int want) {
-    if (want < c->shift) {
-        sync_mirror(c);  // a finer memory unit is needed: recompact from the mirror
-        c->shift = want;
+// Device layout for the mirror plus the pods about to be scored (spec S10):
+//  * compact: every memory quantity of the table and the pods is a multiple of 2^shift bytes and
+//    below 2^24 units, and no NonZeroRequested memory column can pass 2^31 units while the pods
+//    are placed;
+//  * wide otherwise (f64 memory columns in bytes: odd-Ki allocatable, decimal requests, ...).
+// The layout only gets finer (smaller shift, compact -> wide) until the next qs_nodes_load.  Cpu
+// columns are int32 in both layouts: a stream whose NonZeroRequested cpu could pass 2^31 m, or wide
+// memory past 2^53 bytes, is rejected up front.  Re-uploads the table when the layout changes.
+void ensure_layout(qs_ctx *c, const qs_pod *pods, uint32_t p, int extra_shift = 64) {
+    const Mirror &m = c->m;
+    int want = std::min(c->shift, extra_shift);
+    int64_t mem_max = 0, nzm = 0, nzc = 0;
+    for (uint32_t j = 0; j < p; j++) {
+        want = std::min(want, pod_min_shift(pods[j]));
+        mem_max = std::max({mem_max, pods[j].req_mem, pods[j].nz_mem});
+        nzm = std::max(nzm, pods[j].nz_mem);
+        nzc = std::max(nzc, pods[j].nz_cpu);
+    }
+    want = std::max(0, want);
+    bool wide = c->wide;
+    for (uint32_t i = 0; i < m.n; i++) {
+        // pods this node can still take (+1: the evaluation of one more before Fit rejects it)
+        const __int128 more = (__int128)std::max<int64_t>(0, m.mp[i] - m.np[i]) + 1;
+        if ((__int128)m.zc[i] + more * nzc > kGrowLimit32)
+            fail(QS_EINVAL, "node " + std::to_string(i) + ": NonZeroRequested cpu could pass 2^31 m during the stream");
+        if (!wide && (!row_compact_ok(m, i, want) ||
+                      (__int128)(m.zm[i] >> want) + more * (nzm >> want) > kGrowLimit32))
+            wide = true;
+        if (wide && (__int128)m.zm[i] + more * nzm > kGrowLimitF64)
+            fail(QS_EINVAL, "node " + std::to_string(i) + ": NonZeroRequested memory could pass 2^53 B during the stream");
+    }
+    if (!wide && (mem_max >> want) > kLimit) wide = true;
+    if (wide != c->wide || (!wide && want < c->shift)) {
+        sync_mirror(c);  // the device table is re-laid out from the mirror
+        c->wide = wide;
+        if (!wide) c->shift = want;
         c->dev_valid = false;
+        c->saved = false;  // a snapshot of the old layout cannot be restored into the new one
     }
     if (!c->dev_valid) upload_table(c);
+}
+
+// One mirror row, for rolling back a rejected upsert / reserve (the mirror must keep matching
+// the device table).
+struct RowSnap {
+    int64_t ac, am, mp, rc, rm, zc, zm, np, ae[QS_MAX_EXT], re[QS_MAX_EXT];
+    uint64_t th, ts, lb0, lb1, gen;
+    int32_t zone;
+};
+RowSnap snap_row(const Mirror &m, uint32_t i) {
+    RowSnap r{m.ac[i], m.am[i], m.mp[i], m.rc[i], m.rm[i], m.zc[i], m.zm[i], m.np[i], {}, {},
+              m.th[i], m.ts[i], m.lb[2 * (size_t)i], m.lb[2 * (size_t)i + 1], m.gen[i], m.zone[i]};
+    for (int k = 0; k < QS_MAX_EXT; k++) {
+        r.ae[k] = m.ae[(size_t)i * QS_MAX_EXT + k];
+        r.re[k] = m.re[(size_t)i * QS_MAX_EXT + k];
+    }
+    return r;
+}
+void put_row(Mirror &m, uint32_t i, const RowSnap &r) {
+    m.ac[i] = r.ac; m.am[i] = r.am; m.mp[i] = r.mp; m.rc[i] = r.rc; m.rm[i] = r.rm;
+    m.zc[i] = r.zc; m.zm[i] = r.zm; m.np[i] = r.np;
+    for (int k = 0; k < QS_MAX_EXT; k++) {
+        m.ae[(size_t)i * QS_MAX_EXT + k] = r.ae[k];
+        m.re[(size_t)i * QS_MAX_EXT + k] = r.re[k];
+    }
+    m.th[i] = r.th; m.ts[i] = r.ts; m.lb[2 * (size_t)i] = r.lb0; m.lb[2 * (size_t)i + 1] = r.lb1;
+    m.gen[i] = r.gen; m.zone[i] = r.zone;
+}
+
+// Test hook for the recovery path (tests/test_gpu_recovery.py): QS_INJECT_FAULT=<entry> makes the
+// next call of that entry point fail as a device error after its device work; one-shot.
+void maybe_inject_fault(const char *entry) {
+    const char *e = getenv("QS_INJECT_FAULT");
+    if (e && std::strcmp(e, entry) == 0) {
+        unsetenv("QS_INJECT_FAULT");
+        fail(QS_EDEVICE, std::string("injected device fault in ") + entry);
+    }
 }
 
 template <class F>
@@ -341,6 +489,15 @@ qs_status guarded(qs_ctx *c, F &&f) {
         return QS_OK;
     } catch (const QsError &e) {
         c->err = e.msg;
+        if (e.st == QS_EDEVICE) {
+            // failure recovery: the host mirror is authoritative — it is synced
+            // after every stream, so it holds every placement the caller has been told about.
+            // Drop the device table; the next call re-uploads it from the mirror.
+            c->dev_valid = false;
+            c->mirror_stale = false;
+            c->saved = false;
+            c->device_faults++;
+        }
         return e.st;
     } catch (const std::bad_alloc &) {
         c->err = "out of host memory";
@@ -451,7 +608,7 @@ void percentile_stats(const std::vector<uint64_t> &st, qs_stats *s) {
 // resolves the batch, applies it and builds the next one on the device.  The ceil(P/B) batches of
 // a stream are captured once as a HIP graph; the few pods still carried at the end (all their
 // candidates claimed by earlier pods of their batch) run in extra batches.  Returns the batch count.
-uint64_t run_batched(qs_ctx *c, qs_stream *s, const DPod *dp, const DPodX *dx, int32_t *on, uint64_t *ok,
+uint64_t run_batched(qs_ctx *c, qs_stream *s, const void *dp, const DPodX *dx, int32_t *on, uint64_t *ok,
                      KernelTimer &kt) {
     const uint32_t n = c->m.n, P = s->p;
     if (c->dc.feat & (kFeatTaint | kFeatAffinity))
@@ -497,7 +654,7 @@ uint64_t run_batched(qs_ctx *c, qs_stream *s, const DPod *dp, const DPodX *dx, i
     if (!kt.on && !(genv && genv[0] == '0')) {
         std::vector<uint8_t> key;
         auto put = [&](const void *p, size_t nb) { key.insert(key.end(), (const uint8_t *)p, (const uint8_t *)p + nb); };
-        const void *ptrs[] = {c->dt.rows, c->dt.apps, bf.lists, bf.clists, ctrl, dp, on, ok};
+        const void *ptrs[] = {c->dt.rows, c->dt.wrows, c->dt.apps, bf.lists, bf.clists, ctrl, dp, on, ok};
         put(ptrs, sizeof ptrs);
         put(&c->dt.n, sizeof c->dt.n);
         put(&c->dc, sizeof c->dc);
@@ -636,7 +793,10 @@ qs_status qs_nodes_load(qs_ctx *c, const qs_node_soa *nd, uint32_t n) {
             m.lb[2 * (size_t)i] = nd->label_bits ? nd->label_bits[2 * (size_t)i] : 0;
             m.lb[2 * (size_t)i + 1] = nd->label_bits ? nd->label_bits[2 * (size_t)i + 1] : 0;
         }
+        for (uint32_t i = 0; i < n; i++) check_row_values(m, i);
         c->shift = table_shift(m);
+        c->wide = false;
+        for (uint32_t i = 0; i < n && !c->wide; i++) c->wide = !row_compact_ok(m, i, c->shift);
         c->dev_valid = false;
         c->saved = false;
         c->mirror_stale = false;
@@ -670,6 +830,20 @@ qs_status qs_node_upsert(qs_ctx *c, uint32_t idx, const qs_node_row *r, uint64_t
         sync_mirror(c);
         Mirror &m = c->m;
         if (idx > m.n) fail(QS_EINVAL, "idx beyond table end (append only at idx == n)");
+        if (idx < m.n && generation != 0 && generation <= m.gen[idx]) return;  // already applied (UP NodeInfo.Generation diff)
+        // validate the new row on its own before any state changes (a rejected row leaves the
+        // mirror, the layout and the device table untouched)
+        Mirror one;
+        one.resize(1);
+        one.ac[0] = r->alloc_cpu; one.am[0] = r->alloc_mem; one.mp[0] = r->max_pods;
+        one.rc[0] = r->req_cpu; one.rm[0] = r->req_mem; one.zc[0] = r->nz_cpu; one.zm[0] = r->nz_mem;
+        one.np[0] = r->pods;
+        for (int k = 0; k < QS_MAX_EXT; k++) { one.ae[k] = r->alloc_ext[k]; one.re[k] = r->req_ext[k]; }
+        one.th[0] = r->taint_hard; one.ts[0] = r->taint_soft;
+        one.lb[0] = r->label_bits[0]; one.lb[1] = r->label_bits[1];
+        one.zone[0] = r->zone;
+        one.gen[0] = generation;
+        check_row_values(one, 0);
         if (idx == m.n) {  // append one node
             Mirror old = m;
             m.resize(old.n + 1);
@@ -682,24 +856,16 @@ qs_status qs_node_upsert(qs_ctx *c, uint32_t idx, const qs_node_row *r, uint64_t
             std::copy(old.gen.begin(), old.gen.end(), m.gen.begin());
             std::copy(old.zone.begin(), old.zone.end(), m.zone.begin());
             c->dev_valid = false;
-        } else if (generation != 0 && generation <= m.gen[idx]) {
-            return;  // already applied (UP NodeInfo.Generation diff)
+            c->saved = false;
         }
-        m.ac[idx] = r->alloc_cpu; m.am[idx] = r->alloc_mem; m.mp[idx] = r->max_pods;
-        m.rc[idx] = r->req_cpu; m.rm[idx] = r->req_mem; m.zc[idx] = r->nz_cpu; m.zm[idx] = r->nz_mem;
-        m.np[idx] = r->pods;
-        for (int k = 0; k < QS_MAX_EXT; k++) {
-            m.ae[(size_t)idx * QS_MAX_EXT + k] = r->alloc_ext[k];
-            m.re[(size_t)idx * QS_MAX_EXT + k] = r->req_ext[k];
-        }
-        m.th[idx] = r->taint_hard; m.ts[idx] = r->taint_soft;
-        m.lb[2 * (size_t)idx] = r->label_bits[0]; m.lb[2 * (size_t)idx + 1] = r->label_bits[1];
-        m.zone[idx] = r->zone;
-        m.gen[idx] = generation;
+        put_row(m, idx, snap_row(one, 0));
+        // the new row's memory may need a finer unit or the wide layout (re-upload), else one row
         const int want = std::min({ctz64(r->alloc_mem), ctz64(r->req_mem), ctz64(r->nz_mem)});
-        if (want < c->shift) { c->shift = want; c->dev_valid = false; }
-        if (!c->dev_valid) upload_table(c);
-        else push_row(c, idx);
+        const bool was_valid = c->dev_valid;
+        const int old_shift = c->shift;
+        const bool old_wide = c->wide;
+        ensure_layout(c, nullptr, 0, want);
+        if (was_valid && c->dev_valid && c->shift == old_shift && c->wide == old_wide) push_row(c, idx);
     });
 }
 
@@ -710,9 +876,19 @@ static qs_status reserve_impl(qs_ctx *c, uint32_t node, const qs_pod *p, int sig
         check_pod(*p, 0);
         HIPCHK(hipSetDevice(c->device));
         sync_mirror(c);
+        const RowSnap before = snap_row(c->m, node);
         mirror_reserve(c->m, node, *p, sign);
-        ensure_shift(c, pod_min_shift(*p));
-        push_row(c, node);
+        try {
+            check_row_values(c->m, node);  // e.g. an Unreserve that drives a column negative
+        } catch (...) {
+            put_row(c->m, node, before);
+            throw;
+        }
+        const bool was_valid = c->dev_valid;
+        const int old_shift = c->shift;
+        const bool old_wide = c->wide;
+        ensure_layout(c, p, 1);
+        if (was_valid && c->shift == old_shift && c->wide == old_wide) push_row(c, node);
     });
 }
 qs_status qs_reserve(qs_ctx *c, uint32_t node, const qs_pod *p) { return reserve_impl(c, node, p, +1); }
@@ -724,21 +900,24 @@ qs_status qs_score_pod(qs_ctx *c, const qs_pod *pod, uint8_t *feas, int32_t *sco
         if (!pod) fail(QS_EINVAL, "null pod");
         HIPCHK(hipSetDevice(c->device));
         const uint32_t n = c->m.n;
-        ensure_shift(c, pod_min_shift(*pod));
-        const DPod dp = compact_pod(c, *pod, 0, c->shift);
+        check_pod(*pod, 0);
+        ensure_layout(c, pod, 1);
+        alignas(16) uint8_t dp[sizeof(DPodW)];
+        compact_pod(c, *pod, 0, c->shift, c->wide, dp);
         const DPodX dx = compact_podx(*pod);
-        c->dc.feat = feat_of(c->cfg) | ((pod->req_ext[0] || pod->req_ext[1]) ? kFeatExt : 0u);
-        c->one_pod.ensure(sizeof(DPod));
+        c->dc.feat = feat_of(c->cfg) | ((pod->req_ext[0] || pod->req_ext[1]) ? kFeatExt : 0u) |
+                     (c->wide ? kFeatWide | kFeatExt : 0u);
+        c->one_pod.ensure(sizeof(DPodW));
         c->one_podx.ensure(sizeof(DPodX));
         c->out_feas.ensure(std::max<size_t>(n, 1));
         c->out_score.ensure(std::max<size_t>(16 * (size_t)n, 16));
         c->out_total.ensure(std::max<size_t>(4 * (size_t)n, 4));
-        HIPCHK(hipMemcpyAsync(c->one_pod.p, &dp, sizeof dp, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(c->one_pod.p, dp, pod_record_bytes(c->wide), hipMemcpyHostToDevice, c->stream));
         HIPCHK(hipMemcpyAsync(c->one_podx.p, &dx, sizeof dx, hipMemcpyHostToDevice, c->stream));
         HIPCHK(hipMemsetAsync(c->scratch.p, 0, scan_scratch_bytes(), c->stream));
         if (n) {
             ensure_soa(c);
-            HIPCHK(launch_scan_pod(c->dt, c->one_pod.as<DPod>(), c->one_podx.as<DPodX>(), 0, c->dc,
+            HIPCHK(launch_scan_pod(c->dt, c->one_pod.p, c->one_podx.as<DPodX>(), 0, c->dc,
                                    c->scratch.p, nullptr, nullptr, nullptr, c->out_feas.as<uint8_t>(),
                                    c->out_score.as<int32_t>(), c->out_total.as<int32_t>(), 3,
                                    c->stream));  // scan + reduce (no Reserve: out_node == nullptr)
@@ -763,32 +942,30 @@ qs_status qs_stream_prepare(qs_ctx *c, const qs_pod *pods, uint32_t p, qs_stream
         s = new qs_stream();
         s->p = p;
         s->pods.assign(pods, pods + p);
-        int want = c->shift;
-        for (uint32_t j = 0; j < p; j++) {
-            check_pod(pods[j], j);
-            want = std::min(want, pod_min_shift(pods[j]));
-        }
-        ensure_shift(c, want);
+        for (uint32_t j = 0; j < p; j++) check_pod(pods[j], j);
+        ensure_layout(c, pods, p);
         s->shift = c->shift;
-        s->feat = feat_of(c->cfg);
+        s->wide = c->wide;
+        s->feat = feat_of(c->cfg) | (c->wide ? kFeatWide | kFeatExt : 0u);
         for (uint32_t j = 0; j < p; j++)
             if (pods[j].req_ext[0] || pods[j].req_ext[1]) { s->feat |= kFeatExt; break; }
         s->order = qos_order(pods, p, c->cfg.qos_sort != 0);
-        std::vector<DPod> dp(std::max<uint32_t>(p, 1));
+        const size_t rb = pod_record_bytes(c->wide);
+        std::vector<uint8_t> dp(rb * std::max<uint32_t>(p, 1));
         const bool needx = feat_of(c->cfg) & (kFeatTaint | kFeatAffinity);
         std::vector<DPodX> dx(needx ? std::max<uint32_t>(p, 1) : 1);
         for (uint32_t k = 0; k < p; k++) {
             const uint32_t j = s->order[k];
-            dp[k] = compact_pod(c, pods[j], j, c->shift);
+            compact_pod(c, pods[j], j, c->shift, c->wide, dp.data() + rb * k);
             if (needx) dx[k] = compact_podx(pods[j]);
         }
         const size_t P1 = std::max<uint32_t>(p, 1);
-        s->d_pods.ensure(sizeof(DPod) * P1);
+        s->d_pods.ensure(rb * P1);
         s->d_podx.ensure(sizeof(DPodX) * dx.size());
         s->d_node.ensure(4 * P1);
         s->d_key.ensure(8 * P1);
         if (c->cfg.record_timestamps) s->d_stamp.ensure(8 * P1);
-        HIPCHK(hipMemcpyAsync(s->d_pods.p, dp.data(), sizeof(DPod) * p, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(s->d_pods.p, dp.data(), rb * p, hipMemcpyHostToDevice, c->stream));
         HIPCHK(hipMemcpyAsync(s->d_podx.p, dx.data(), sizeof(DPodX) * dx.size(), hipMemcpyHostToDevice, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
     });
@@ -804,8 +981,9 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
     return guarded(c, [&] {
         if (!s) fail(QS_EINVAL, "null stream");
         if (mode != QS_MODE_EXACT && mode != QS_MODE_BATCHED) fail(QS_EINVAL, "unknown qs_mode");
-        if (s->shift != c->shift || !c->dev_valid) fail(QS_ESTATE, "node table recompacted after prepare");
+        if (s->shift != c->shift || s->wide != c->wide) fail(QS_ESTATE, "node table re-laid out after prepare");
         HIPCHK(hipSetDevice(c->device));
+        if (!c->dev_valid) upload_table(c);  // recovery after a device fault: rebuild from the mirror
         const uint32_t n = c->m.n, P = s->p;
         c->dc.feat = s->feat;
         const int eng = mode == QS_MODE_BATCHED ? QS_ENGINE_BATCHED : pick_engine(c, n);
@@ -823,7 +1001,7 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
             HIPCHK(hipMemsetAsync(on, 0xFF, 4 * (size_t)P, c->stream));
             HIPCHK(hipMemsetAsync(ok, 0, 8 * (size_t)P, c->stream));
         } else if (P > 0) {
-            const DPod *dp = s->d_pods.as<DPod>();
+            const void *dp = s->d_pods.p;
             const DPodX *dx = s->d_podx.as<DPodX>();
             if (eng == QS_ENGINE_BATCHED) {
                 batches = run_batched(c, s, dp, dx, on, ok, kt);
@@ -853,7 +1031,7 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                 geo.waves = norm || (rw && rw[0] == '1' && !overlap) ? 1u : 4u;
                 // normalizing profiles: the four-wave resolver with its stop/resume hand-off
                 // (overlapped windows, merged lists); QS_NORM_WAVES=1 keeps the single-wave kernel
-                static const char *nw = getenv("QS_NORM_WAVES");
+                const char *nw = getenv("QS_NORM_WAVES");  // read per run (tests pin it per case)
                 if (norm && overlap && geo.epl == 1 && !(nw && nw[0] == '1')) geo.waves = 4;
                 int64_t wmax = 0;
                 for (int q = 0; q < 3; q++) wmax = std::max<int64_t>(wmax, (int64_t)c->cfg.w_fit[q] + c->cfg.w_bal[q]);
@@ -978,7 +1156,7 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                     auto put = [&](const void *p, size_t nb) {
                         key.insert(key.end(), (const uint8_t *)p, (const uint8_t *)p + nb);
                     };
-                    const void *ptrs[] = {c->dt.rows, c->dt.masks, L0, C0, dio, st, (void *)c->comm, dp, dx,
+                    const void *ptrs[] = {c->dt.rows, c->dt.wrows, c->dt.masks, L0, C0, dio, st, (void *)c->comm, dp, dx,
                                           c->npart.p, c->normi.p, c->nfall.p};
                     put(ptrs, sizeof ptrs);
                     put(&c->dt.n, sizeof c->dt.n);
@@ -1035,19 +1213,24 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
         HIPCHK(hipEventElapsedTime(&ms, e0, e1));
         (void)hipEventDestroy(e0);
         (void)hipEventDestroy(e1);
-        uint64_t rescans = 0;
+        uint64_t rescans = 0, resumed = 0;
         if (eng == QS_ENGINE_LOOKAHEAD && c->nfall.p) {
             uint64_t h[2] = {0, 0};
             HIPCHK(hipMemcpy(h, c->nfall.p, 16, hipMemcpyDeviceToHost));
             rescans = h[0];
+            resumed = h[1];
             if (getenv("QS_NORM_DIAG"))
                 fprintf(stderr, "QS_NORM_DIAG rescans %llu resumed windows %llu\n", (unsigned long long)h[0],
                         (unsigned long long)h[1]);
         }
-        s->ran = true;
         c->mirror_stale = true;
         if (eng != QS_ENGINE_SCAN) c->soa_valid = false;  // those engines update the rows only
         kt.finish();
+        maybe_inject_fault("stream_run");
+        // keep the host mirror authoritative after every stream (one D2H of the rows, outside
+        // the timed region): a later device fault rebuilds the table from it
+        sync_mirror(c);
+        s->ran = true;
         if (stats) {
             std::memset(stats, 0, sizeof(*stats));
             for (int k = 0; k < 4; k++) {
@@ -1060,6 +1243,9 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
             stats->batches = batches;
             stats->truncations = rescans;
             stats->engine_used = eng;
+            stats->table_layout = c->wide ? 1 : 0;
+            stats->resumed_windows = resumed;
+            stats->device_faults = c->device_faults;
         }
     });
 }
@@ -1094,21 +1280,27 @@ qs_status qs_table_save(qs_ctx *c) {
     return guarded(c, [&] {
         if (!c->dev_valid) fail(QS_ESTATE, "no node table loaded");
         HIPCHK(hipSetDevice(c->device));
+        sync_mirror(c);
         c->tbl_saved.ensure(c->tbl.bytes);
         HIPCHK(hipMemcpyAsync(c->tbl_saved.p, c->tbl.p, c->tbl.bytes, hipMemcpyDeviceToDevice, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
+        c->m_saved = c->m;
+        c->saved_wide = c->wide;
+        c->saved_shift = c->shift;
         c->saved = true;
     });
 }
 
 qs_status qs_table_restore(qs_ctx *c) {
     return guarded(c, [&] {
-        if (!c->saved || !c->dev_valid || c->tbl_saved.bytes != c->tbl.bytes)
+        if (!c->saved || !c->dev_valid || c->tbl_saved.bytes != c->tbl.bytes || c->saved_wide != c->wide ||
+            c->saved_shift != c->shift)
             fail(QS_ESTATE, "no matching qs_table_save snapshot");
         HIPCHK(hipSetDevice(c->device));
         HIPCHK(hipMemcpyAsync(c->tbl.p, c->tbl_saved.p, c->tbl.bytes, hipMemcpyDeviceToDevice, c->stream));
-        c->mirror_stale = true;  // mirror re-reads the restored rows on demand
-        c->soa_valid = false;    // the SoA copy is rebuilt from the restored rows on demand
+        c->m = c->m_saved;        // the mirror of the snapshot
+        c->mirror_stale = false;
+        c->soa_valid = false;     // the SoA copy is rebuilt from the restored rows on demand
     });
 }
 

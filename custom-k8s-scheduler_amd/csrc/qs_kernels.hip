@@ -1,259 +1,10 @@
-// qs_kernels.hip — gfx950 kernels of the exact per-pod scheduling cycle (spec/semantics.md S4–S7).
-//
-// Engines (all bit-exact with the oracle):
-//   PERSISTENT  k_persistent: ONE resident workgroup runs the whole pod stream; node rows live in
-//               VGPRs (NPT rows per lane), Filter+Score in registers, DPP wave argmax, one LDS
-//               exchange + one barrier per pod, Reserve applied by the owning lane.  N <= 8192.
-//   SCAN        k_scan_norm / k_scan_key / k_scan_commit: per-pod grid scan over the HBM table with
-//               u64 atomicMax of packed keys, then a 1-thread commit that applies Reserve.  Any N.
-//   LOOKAHEAD   k_la_select + k_la_resolve: exact top-K lookahead.  For a window of K pods the
-//               whole chip scores all K×N (pod, node) pairs against the window-start table and
-//               keeps, per pod and node-chunk, the top-L keys (L = K).  One wave then resolves the
-//               window sequentially: pod i's winner is the max of (fresh keys of the <= i nodes
-//               modified earlier in the window) and (the best stale key of an unmodified node,
-//               which is always inside the top-L lists).  Bit-exact; SURVEY.md §7 H4 option 3.
-#include <algorithm>
-
-#include "qs_device.hpp"
-#include "qs_launch.hpp"
+// qs_kernels.hip — the compact-layout translation unit of the gfx950 kernels (qs_kernels.hpp,
+// DESIGN.md §4): the non-template kernels, the instantiations for the compact row layout
+// (F in {0, kFeatExt, kFeatExt|kFeatTaint|kFeatAffinity}) and the host-callable dispatchers of
+// qs_launch.hpp, which route wide-layout tables (DevTable::wrows) to qs_kernels_wide.hip.
+#include "qs_kernels.hpp"
 
 namespace qs {
-
-constexpr uint32_t kFeatNorm = kFeatTaint | kFeatAffinity;
-
-// =============================================================================================
-// PERSISTENT engine
-// =============================================================================================
-template <int NPT, int BS, uint32_t F>
-__global__ __launch_bounds__(BS) void k_persistent(DevTable t, const DPod *__restrict__ pods,
-                                                   const DPodX *__restrict__ podx, uint32_t P,
-                                                   DevCfg c, int32_t *__restrict__ out_node,
-                                                   uint64_t *__restrict__ out_key,
-                                                   uint64_t *__restrict__ stamps) {
-    constexpr int NW = BS / kWave;
-    __shared__ uint64_t red[2][NW];
-    __shared__ uint32_t redn[2][2][NW];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const uint32_t n = t.n;
-    Row r[NPT];
-    RowX x[NPT];
-#pragma unroll
-    for (int k = 0; k < NPT; ++k) {
-        const uint32_t idx = tid + k * BS;
-        if (idx < n) { r[k] = load_row(t, idx); x[k] = load_rowx<F>(t, idx); }
-        else { r[k] = empty_row(); x[k] = RowX{0, 0, 0, 0, 0, 0, 0, 0}; }
-    }
-    DPod pn = pods[0];
-    for (uint32_t s = 0; s < P; ++s) {
-        const DPod p = pn;
-        pn = pods[s + 1 < P ? s + 1 : s];  // prefetch the next pod record (scalar loads)
-        DPodX px;
-        if (F & kFeatNorm) px = podx[s];
-        uint32_t mt = 0, ma = 0;
-        double ymt = 0.0, yma = 0.0;
-        if (F & kFeatNorm) {  // NormalizeScore maxima over feasible nodes (spec S5)
-            uint32_t lt = 0, la = 0;
-#pragma unroll
-            for (int k = 0; k < NPT; ++k) {
-                const bool f = feasible<F>(r[k], x[k], p, px);
-                const uint32_t a = f ? taint_raw(x[k], px) : 0u;
-                const uint32_t b = f ? affinity_raw(x[k], p, px) : 0u;
-                lt = a > lt ? a : lt;
-                la = b > la ? b : la;
-            }
-            lt = wave_max_u32(lt);
-            la = wave_max_u32(la);
-            if (lane == 0) { redn[s & 1][0][w] = lt; redn[s & 1][1][w] = la; }
-            __syncthreads();
-#pragma unroll
-            for (int i = 0; i < NW; ++i) {
-                const uint32_t a = redn[s & 1][0][i], b = redn[s & 1][1][i];
-                mt = a > mt ? a : mt;
-                ma = b > ma ? b : ma;
-            }
-            ymt = rcp_exact(mt);
-            yma = rcp_exact(ma);
-        }
-        uint64_t best = 0;
-#pragma unroll
-        for (int k = 0; k < NPT; ++k) {
-            const bool f = feasible<F>(r[k], x[k], p, px);
-            const uint32_t tot = node_total<F>(r[k], x[k], p, px, c, mt, ymt, ma, yma, nullptr);
-            const uint64_t key = f ? pack_key(tot + 1, tid + k * BS) : 0ull;
-            best = key > best ? key : best;
-        }
-        best = wave_max_u64(best);
-        if (lane == 0) red[s & 1][w] = best;
-        __syncthreads();
-        uint64_t ks = 0;
-#pragma unroll
-        for (int i = 0; i < NW; ++i) {
-            const uint64_t v = red[s & 1][i];
-            ks = v > ks ? v : ks;
-        }
-        const uint32_t win = key_node(ks);
-        if (ks != 0) {
-#pragma unroll
-            for (int k = 0; k < NPT; ++k)
-                if (tid + k * BS == win) reserve(r[k], x[k], p, +1);
-        }
-        if (tid == 0) {
-            out_node[s] = ks ? (int32_t)win : -1;
-            if (out_key) out_key[s] = ks;
-            if (stamps) stamps[s] = __builtin_amdgcn_s_memrealtime();
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < NPT; ++k) {
-        const uint32_t idx = tid + k * BS;
-        if (idx < n) { store_dyn(t, idx, r[k]); store_dynx<F>(t, idx, x[k]); }
-    }
-}
-
-// =============================================================================================
-// SCAN engine (and qs_score_pod)
-// =============================================================================================
-// Per-pod scratch: normalize maxima (taint / affinity) and one partial argmax key per block of the
-// key scan; the commit kernel reduces the partials (no single-address atomics on the hot path:
-// thousands of blocks hitting one u64 serialise at the memory-side atomic unit).
-constexpr uint32_t kScanBlocksMax = 2048;
-struct ScanScratch {
-    unsigned long long best;  // reduced key of the last commit (qs_score_pod reads it)
-    uint32_t mt, ma;          // normalize maxima (k_scan_norm)
-    uint32_t nblk, pad;       // partials written by the last key scan
-    uint64_t partial[kScanBlocksMax];
-};
-
-// Block-wide max of a u64 key: wave DPP max, then one LDS exchange.
-template <int BS>
-__device__ __forceinline__ uint64_t block_max_u64(uint64_t v) {
-    __shared__ uint64_t red[BS / kWave];
-    v = wave_max_u64(v);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-    __syncthreads();
-    uint64_t m = 0;
-#pragma unroll
-    for (int i = 0; i < BS / kWave; ++i) m = red[i] > m ? red[i] : m;
-    return m;
-}
-
-template <uint32_t F>
-__global__ __launch_bounds__(256) void k_scan_norm(DevTable t, const DPod *__restrict__ pods,
-                                                   const DPodX *__restrict__ podx, uint32_t s,
-                                                   ScanScratch *sc) {
-    const DPod p = pods[s];
-    const DPodX px = podx[s];
-    uint32_t lt = 0, la = 0;
-    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < t.n; i += gridDim.x * 256) {
-        const Row r = load_row(t, i);
-        const RowX x = load_rowx<F>(t, i);
-        if (feasible<F>(r, x, p, px)) {
-            const uint32_t a = taint_raw(x, px), b = affinity_raw(x, p, px);
-            lt = a > lt ? a : lt;
-            la = b > la ? b : la;
-        }
-    }
-    // (normalizing profiles run this scan on row tables of a few thousand nodes: few blocks)
-    lt = wave_max_u32(lt);
-    la = wave_max_u32(la);
-    if ((threadIdx.x & 63) == 0) {
-        if (lt) atomicMax(&sc->mt, lt);
-        if (la) atomicMax(&sc->ma, la);
-    }
-}
-
-// Keys for every node from the row table; optionally per-node outputs for qs_score_pod.
-template <uint32_t F>
-__global__ __launch_bounds__(256) void k_scan_key(DevTable t, const DPod *__restrict__ pods,
-                                                  const DPodX *__restrict__ podx, uint32_t s,
-                                                  DevCfg c, ScanScratch *sc, uint8_t *feas_out,
-                                                  int32_t *score_out, int32_t *total_out) {
-    const DPod p = pods[s];
-    DPodX px;
-    uint32_t mt = 0, ma = 0;
-    if (F & kFeatNorm) { px = podx[s]; mt = sc->mt; ma = sc->ma; }
-    const double ymt = rcp_exact(mt), yma = rcp_exact(ma);
-    uint64_t best = 0;
-    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < t.n; i += gridDim.x * 256) {
-        const Row r = load_row(t, i);
-        const RowX x = load_rowx<F>(t, i);
-        const bool f = feasible<F>(r, x, p, px);
-        uint32_t sco[4];
-        const uint32_t tot = node_total<F>(r, x, p, px, c, mt, ymt, ma, yma, score_out ? sco : nullptr);
-        const uint64_t key = f ? pack_key(tot + 1, i) : 0ull;
-        best = key > best ? key : best;
-        if (feas_out) feas_out[i] = f;
-        if (total_out) total_out[i] = f ? (int32_t)tot : -1;
-        if (score_out) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) score_out[4 * (size_t)i + q] = f ? (int32_t)sco[q] : 0;
-        }
-    }
-    best = block_max_u64<256>(best);
-    if (threadIdx.x == 0) sc->partial[blockIdx.x] = best;
-}
-
-// Keys over the SoA copy (HBM-resident tables; F = 0 or kFeatExt): lane q covers nodes
-// 4q..4q+3 with one 16-byte load per column; RN(1/alloc) is recomputed in registers (rcp_int:
-// the same value the host stores in the row copy, so keys are bit-identical to k_scan_key).
-template <uint32_t F>
-__global__ __launch_bounds__(256) void k_scan_soa(DevTable t, const DPod *__restrict__ pods,
-                                                  uint32_t s, DevCfg c, ScanScratch *sc,
-                                                  uint8_t *feas_out, int32_t *score_out,
-                                                  int32_t *total_out) {
-    const DPod p = pods[s];
-    const DPodX px{};
-    const uint32_t nq = (t.n + 3) / 4;  // columns are zero-padded to a multiple of 64 nodes
-    uint64_t best = 0;
-    // two quads per lane in flight: both iterations' loads are issued before either is scored
-    const uint32_t stride = gridDim.x * 256;
-    for (uint32_t q0 = blockIdx.x * 256 + threadIdx.x; q0 < nq; q0 += 2 * stride) {
-        int4 cols[2][kSCols];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const uint32_t qh = min(q0 + h * stride, nq - 1);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) cols[h][k] = reinterpret_cast<const int4 *>(t.soa.c[k])[qh];
-            if (F & kFeatExt) {
-#pragma unroll
-                for (int k = 8; k < kSCols; ++k) cols[h][k] = reinterpret_cast<const int4 *>(t.soa.c[k])[qh];
-            }
-        }
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-        const uint32_t q = q0 + h * stride;
-        if (q >= nq) break;
-        const int4 *col = cols[h];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            auto el = [&](int k) { return e == 0 ? col[k].x : e == 1 ? col[k].y : e == 2 ? col[k].z : col[k].w; };
-            Row r;
-            r.ac = el(kSAc); r.am = el(kSAm); r.rc = el(kSRc); r.rm = el(kSRm);
-            r.zc = el(kSZc); r.zm = el(kSZm); r.np = el(kSNp); r.mp = el(kSMp);
-            r.yc = r.ac ? rcp_int(r.ac) : 0.0;
-            r.ym = r.am ? rcp_int(r.am) : 0.0;
-            RowX x{};
-            if (F & kFeatExt) { x.ae0 = el(kSAe0); x.re0 = el(kSRe0); x.ae1 = el(kSAe1); x.re1 = el(kSRe1); }
-            const uint32_t idx = 4 * q + e;
-            const bool f = feasible<F>(r, x, p, px);  // padding rows: max_pods 0 -> infeasible
-            uint32_t sco[4];
-            const uint32_t tot = node_total<F>(r, x, p, px, c, 0, 0.0, 0, 0.0, score_out ? sco : nullptr);
-            const uint64_t key = f ? pack_key(tot + 1, idx) : 0ull;
-            best = key > best ? key : best;
-            if (idx < t.n) {
-                if (feas_out) feas_out[idx] = f;
-                if (total_out) total_out[idx] = f ? (int32_t)tot : -1;
-                if (score_out) {
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) score_out[4 * (size_t)idx + k] = f ? (int32_t)sco[k] : 0;
-                }
-            }
-        }
-        }
-    }
-    best = block_max_u64<256>(best);
-    if (threadIdx.x == 0) sc->partial[blockIdx.x] = best;
-}
 
 // Rebuild the SoA copy from the row table (after engines that update rows only).
 __global__ __launch_bounds__(256) void k_rows_to_soa(DevTable t) {
@@ -265,1405 +16,10 @@ __global__ __launch_bounds__(256) void k_rows_to_soa(DevTable t) {
     t.soa.c[kSAe0][i] = r.ae0; t.soa.c[kSRe0][i] = r.re0; t.soa.c[kSAe1][i] = r.ae1; t.soa.c[kSRe1][i] = r.re1;
 }
 
-// One 256-thread block: reduce the key scan's partials to the pod's winner, then (stream mode,
-// out_node != nullptr) apply Reserve to the row (and SoA) copy and emit the outputs.  Resets the
-// normalize maxima for the next pod.
-template <uint32_t F>
-__global__ __launch_bounds__(256) void k_scan_commit(DevTable t, const DPod *__restrict__ pods,
-                                                     uint32_t s, uint32_t nblk, ScanScratch *sc,
-                                                     int32_t *out_node, uint64_t *out_key,
-                                                     uint64_t *stamps) {
-    uint64_t v = 0;
-    for (uint32_t i = threadIdx.x; i < nblk; i += 256) v = sc->partial[i] > v ? sc->partial[i] : v;
-    const uint64_t ks = block_max_u64<256>(v);
-    if (threadIdx.x != 0) return;
-    sc->best = ks;
-    sc->mt = 0;
-    sc->ma = 0;
-    if (!out_node) return;
-    const DPod p = pods[s];
-    if (ks) {
-        const uint32_t w = key_node(ks);
-        Row r = load_row(t, w);
-        RowX x = load_rowx<F>(t, w);
-        reserve(r, x, p, +1);
-        store_dyn(t, w, r);
-        store_dynx<F>(t, w, x);
-        if (t.soa.c[0]) {
-            t.soa.c[kSRc][w] = r.rc; t.soa.c[kSRm][w] = r.rm;
-            t.soa.c[kSZc][w] = r.zc; t.soa.c[kSZm][w] = r.zm;
-            t.soa.c[kSNp][w] = r.np;
-            if (F & kFeatExt) { t.soa.c[kSRe0][w] = x.re0; t.soa.c[kSRe1][w] = x.re1; }
-        }
-    }
-    out_node[s] = ks ? (int32_t)key_node(ks) : -1;
-    if (out_key) out_key[s] = ks;
-    if (stamps) stamps[s] = __builtin_amdgcn_s_memrealtime();
-}
-
-// =============================================================================================
-// LOOKAHEAD engine
-// =============================================================================================
-// Block-wide sum of a wave-uniform per-wave value (one barrier; parity-buffered LDS).
-template <int NW>
-__device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t (*buf)[NW], int &par, int lane,
-                                              int w) {
-    if (lane == 0) buf[par][w] = v;
-    __syncthreads();
-    uint32_t s = 0;
-#pragma unroll
-    for (int i = 0; i < NW; ++i) s += buf[par][i];
-    par ^= 1;
-    return s;
-}
-
-// Block-wide top-L of per-position values tv (0 = empty).  Position order is (wave, j, lane):
-// wave w owns positions [w*E*64, (w+1)*E*64), so when positions follow node-index order, ranks
-// come from ballots and one cross-wave prefix.  Writes the keys of the L largest values to
-// out[0..L): every value > T (the L-th largest) in position order, then the ties at T lowest
-// position first; zero-fills the rest.  keyf(j) = key of this lane's j-th position.
-// Used twice: per node chunk in k_la_select (positions = node indices) and per pod in
-// k_la_merge (positions = chunk-major list slots, so equal totals stay in node-index order).
-template <int BS, int E, class KeyF>
-__device__ __forceinline__ void block_topl(const uint32_t (&tv)[E], uint32_t L,
-                                           uint64_t *__restrict__ out, KeyF keyf) {
-    constexpr int NW = BS / kWave;
-    __shared__ uint32_t cnt[2][NW];
-    __shared__ uint32_t cnt2[NW];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    uint32_t lmax = 0;
-#pragma unroll
-    for (int j = 0; j < E; ++j) lmax = tv[j] > lmax ? tv[j] : lmax;
-    int par = 0;
-    // block max of tv (a max of wave maxima through the sum buffer)
-    const uint32_t wmax = wave_max_u32(lmax);
-    if (lane == 0) cnt[par][w] = wmax;
-    __syncthreads();
-    uint32_t maxtv = 0;
-#pragma unroll
-    for (int i = 0; i < NW; ++i) maxtv = cnt[par][i] > maxtv ? cnt[par][i] : maxtv;
-    par ^= 1;
-    auto count_ge = [&](uint32_t thr) -> uint32_t {
-        uint32_t cw = 0;
-#pragma unroll
-        for (int j = 0; j < E; ++j) cw += (uint32_t)__popcll(__ballot(tv[j] >= thr));
-        return block_sum<NW>(cw, cnt, par, lane, w);
-    };
-    // T = largest threshold with count(tv >= T) >= L, or 1 if fewer than L non-empty positions.
-    uint32_t T = 1;
-    if (maxtv > 0) {
-        const uint32_t call = count_ge(1);
-        if (call > L) {
-            if (count_ge(maxtv) >= L) {
-                T = maxtv;
-            } else {
-                uint32_t lo = 1, hi = maxtv;  // count(>=lo) >= L > count(>=hi)
-                while (hi - lo > 1) {
-                    const uint32_t mid = lo + (hi - lo) / 2;
-                    if (count_ge(mid) >= L) lo = mid; else hi = mid;
-                }
-                T = lo;
-            }
-        }
-    }
-    // ballots of "> T" and "== T" per j; one barrier publishes both per-wave counts
-    uint64_t gb[E], tb[E];
-    uint32_t gt_w = 0, tie_w = 0;
-#pragma unroll
-    for (int j = 0; j < E; ++j) {
-        gb[j] = __ballot(tv[j] > T);
-        tb[j] = __ballot(tv[j] == T && maxtv > 0);
-        gt_w += (uint32_t)__popcll(gb[j]);
-        tie_w += (uint32_t)__popcll(tb[j]);
-    }
-    if (lane == 0) { cnt[par][w] = gt_w; cnt2[w] = tie_w; }
-    __syncthreads();
-    uint32_t rg = 0, rt = 0, c_gt = 0, ties_total = 0;
-#pragma unroll
-    for (int i = 0; i < NW; ++i) {
-        const uint32_t a = cnt[par][i], b = cnt2[i];
-        rg += i < w ? a : 0u;
-        rt += i < w ? b : 0u;
-        c_gt += a;
-        ties_total += b;
-    }
-    const uint32_t need = L > c_gt ? L - c_gt : 0;  // c_gt < L unless fewer than L positions
-    const uint64_t lane_mask_lt = (1ull << lane) - 1ull;
-#pragma unroll
-    for (int j = 0; j < E; ++j) {
-        if ((gb[j] >> lane) & 1ull) {
-            out[rg + (uint32_t)__popcll(gb[j] & lane_mask_lt)] = keyf(j);
-        } else if ((tb[j] >> lane) & 1ull) {
-            const uint32_t rk = rt + (uint32_t)__popcll(tb[j] & lane_mask_lt);
-            if (rk < need) out[c_gt + rk] = keyf(j);
-        }
-        rg += (uint32_t)__popcll(gb[j]);
-        rt += (uint32_t)__popcll(tb[j]);
-    }
-    const uint32_t written = c_gt + (ties_total < need ? ties_total : need);
-    for (uint32_t i = written + tid; i < L; i += BS) out[i] = 0;
-}
-
-// Block (v, k, g) of the select grid: shard v owns nodes [v*n/W, (v+1)*n/W).
-struct SelBlock {
-    uint32_t vs, v, k, g, start, end;
-};
-__device__ __forceinline__ SelBlock sel_block(const DevTable &t, const LaShard &sh, uint32_t G,
-                                              uint32_t chunk, uint32_t bid) {
-    SelBlock b;
-    const uint32_t per = sh.kw * G;
-    b.vs = bid / per;
-    const uint32_t rem = bid % per;
-    b.v = sh.v0 + b.vs;
-    b.k = rem / G;
-    b.g = rem % G;
-    const uint32_t lo = (uint32_t)((uint64_t)b.v * t.n / sh.W);
-    const uint32_t hi = (uint32_t)((uint64_t)(b.v + 1) * t.n / sh.W);
-    b.start = lo + b.g * chunk;
-    b.end = min(hi, b.start + chunk);
-    return b;
-}
-
-// Normalizing profiles, pass 1 (same grid as k_la_select): per (shard, pod, chunk) the maxima of
-// the raw TaintToleration / NodeAffinity scores over the chunk's feasible nodes and their counts,
-// into npart[(v*K + k)*G + g] (the [W][K][G] layout the RCCL all-gather completes).
-template <int BS, int E, uint32_t F>
-__global__ __launch_bounds__(BS) void k_la_norm(DevTable t, const DPod *__restrict__ pods,
-                                                const DPodX *__restrict__ podx, uint32_t s0,
-                                                uint32_t P, LaShard sh, uint32_t G, uint32_t K,
-                                                uint32_t chunk, uint4 *__restrict__ npart) {
-    constexpr int NW = BS / kWave;
-    __shared__ uint32_t red[4][NW];
-    const SelBlock b = sel_block(t, sh, G, chunk, blockIdx.x);
-    const uint32_t s = s0 + b.k;
-    if (s >= P) return;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const DPod p = pods[s];
-    const DPodX px = load_vgpr(podx + s);
-    const uint32_t base = b.start + (uint32_t)w * E * kWave + lane;
-    uint32_t rt[E], ra[E], mt = 0, ma = 0;
-#pragma unroll
-    for (int j = 0; j < E; ++j) {
-        const uint32_t idx = base + j * kWave;
-        rt[j] = ra[j] = 0xFFFFFFFFu;  // not feasible / not in the chunk
-        if (idx < b.end) {
-            const Row r = load_row(t, idx);
-            const RowX x = load_rowx<F>(t, idx);
-            if (feasible<F>(r, x, p, px)) {
-                rt[j] = taint_raw(x, px);
-                ra[j] = affinity_raw(x, p, px);
-                mt = rt[j] > mt ? rt[j] : mt;
-                ma = ra[j] > ma ? ra[j] : ma;
-            }
-        }
-    }
-    mt = wave_max_u32(mt);
-    ma = wave_max_u32(ma);
-    if (lane == 0) { red[0][w] = mt; red[1][w] = ma; }
-    __syncthreads();
-    mt = ma = 0;
-#pragma unroll
-    for (int i = 0; i < NW; ++i) { mt = red[0][i] > mt ? red[0][i] : mt; ma = red[1][i] > ma ? red[1][i] : ma; }
-    uint32_t ct = 0, ca = 0;
-#pragma unroll
-    for (int j = 0; j < E; ++j) {
-        ct += (uint32_t)__popcll(__ballot(rt[j] == mt));
-        ca += (uint32_t)__popcll(__ballot(ra[j] == ma));
-    }
-    if (lane == 0) { red[2][w] = ct; red[3][w] = ca; }
-    __syncthreads();
-    if (tid == 0) {
-        uint4 o = make_uint4(mt, 0, ma, 0);
-#pragma unroll
-        for (int i = 0; i < NW; ++i) { o.y += red[2][i]; o.w += red[3][i]; }
-        npart[((size_t)b.v * K + b.k) * G + b.g] = o;
-    }
-}
-
-// Combine a pod's [W][G] partials into its NormInfo (max, and the count of nodes attaining it).
-__device__ __forceinline__ NormInfo norm_reduce(const uint4 *__restrict__ npart, uint32_t W,
-                                                uint32_t K, uint32_t G, uint32_t k) {
-    NormInfo r{0, 0, 0, 0};
-    for (uint32_t v = 0; v < W; ++v)
-        for (uint32_t g = 0; g < G; ++g) {
-            const uint4 q = npart[((size_t)v * K + k) * G + g];
-            if (q.x > r.mt) { r.mt = q.x; r.ct = 0; }
-            if (q.x == r.mt) r.ct += q.y;
-            if (q.z > r.ma) { r.ma = q.z; r.ca = 0; }
-            if (q.z == r.ma) r.ca += q.w;
-        }
-    return r;
-}
-
-// Grid: shards × pods × G node-chunks.  Block (v, k, g) scores pod s0+k on chunk g of shard v
-// (Filter + Score in registers, against the window-start table) and writes the chunk's top-L
-// keys to out: straight into the final lists when G == 1, else into the chunk-list scratch
-// [nv][kw][G][L] that k_la_merge reduces to one top-L per pod and shard.  Normalizing profiles
-// first combine the k_la_norm partials (uniform per pod: scalar loads) and block (0, k, 0) of
-// this process publishes the pod's NormInfo for the resolver.
-template <int BS, int E, uint32_t F>
-__device__ __forceinline__ void la_select_block(uint32_t bid, const DevTable &t, const DPod *__restrict__ pods,
-                                                const DPodX *__restrict__ podx, const DevCfg &c,
-                                                uint32_t s0, uint32_t P, const LaShard &sh,
-                                                uint32_t G, uint32_t L, uint32_t chunk,
-                                                uint32_t GLp, uint64_t *__restrict__ lists,
-                                                uint64_t *__restrict__ clists,
-                                                const uint4 *__restrict__ npart, uint32_t K,
-                                                NormInfo *__restrict__ norm_out,
-                                                const uint32_t *__restrict__ pidx,
-                                                const uint32_t *__restrict__ pcount) {
-    const SelBlock b = sel_block(t, sh, G, chunk, bid);
-    uint32_t s;
-    if (pidx) {  // batched mode: the batch's stream positions and size live on the device
-        if (b.k >= *pcount) return;
-        s = pidx[b.k];
-    } else {
-        s = s0 + b.k;
-        if (s >= P) return;
-    }
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const DPod p = pods[s];
-    const bool aa = t.apps && pod_aa(p.flags) != 0;  // batched-mode anti-affinity (spec S11)
-    DPodX px{};
-    NormInfo nf{0, 0, 0, 0};
-    if (F & kFeatNorm) {
-        px = load_vgpr(podx + s);
-        nf = norm_reduce(npart, sh.W, K, G, b.k);
-        if (tid == 0 && b.vs == 0 && b.g == 0) norm_out[b.k] = nf;
-    }
-    const double ymt = rcp_exact(nf.mt), yma = rcp_exact(nf.ma);
-    const uint32_t base = b.start + (uint32_t)w * E * kWave + lane;
-    uint32_t tv[E];
-#pragma unroll
-    for (int j = 0; j < E; ++j) {
-        const uint32_t idx = base + j * kWave;
-        tv[j] = 0;
-        if (idx < b.end) {
-            const Row r = load_row(t, idx);
-            const RowX x = load_rowx<F>(t, idx);
-            const bool f = feasible<F>(r, x, p, px) && (!aa || aa_ok(t, p.flags, idx));
-            const uint32_t tot = node_total<F>(r, x, p, px, c, nf.mt, ymt, nf.ma, yma, nullptr);
-            tv[j] = f ? tot + 1 : 0;
-        }
-    }
-    uint64_t *out = G == 1 ? lists + (size_t)b.v * sh.RS + (size_t)b.k * GLp
-                           : clists + (((size_t)b.vs * sh.kw + b.k) * G + b.g) * L;
-    block_topl<BS, E>(tv, L, out, [&](int j) { return pack_key(tv[j], base + j * kWave); });
-}
-
-template <int BS, int E, uint32_t F>
-__global__ __launch_bounds__(BS) void k_la_select(DevTable t, const DPod *__restrict__ pods,
-                                                  const DPodX *__restrict__ podx, DevCfg c,
-                                                  uint32_t s0, uint32_t P, LaShard sh,
-                                                  uint32_t G, uint32_t L, uint32_t chunk,
-                                                  uint32_t GLp, uint64_t *__restrict__ lists,
-                                                  uint64_t *__restrict__ clists,
-                                                  const uint4 *__restrict__ npart, uint32_t K,
-                                                  NormInfo *__restrict__ norm_out,
-                                                  const uint32_t *__restrict__ pidx,
-                                                  const uint32_t *__restrict__ pcount) {
-    la_select_block<BS, E, F>(blockIdx.x, t, pods, podx, c, s0, P, sh, G, L, chunk, GLp, lists, clists,
-                              npart, K, norm_out, pidx, pcount);
-}
-
-// Grid: shards × pods.  Reduces a pod's G chunk lists (M = G*L keys, chunk-major: equal totals
-// sit in node-index order) to its top-L in the final [W][K][GLp] lists the resolver reads, so the
-// resolver scans L keys per pod instead of G*L.
-template <int E2>
-__device__ __forceinline__ void la_merge_block(uint32_t bid, const uint64_t *__restrict__ clists, uint32_t M,
-                                               uint32_t L, const LaShard &sh, uint32_t GLp,
-                                               uint64_t *__restrict__ lists) {
-    const uint32_t vs = bid / sh.kw, k = bid % sh.kw;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const uint64_t *in = clists + ((size_t)vs * sh.kw + k) * M;
-    uint64_t e[E2];
-    uint32_t tv[E2];
-#pragma unroll
-    for (int j = 0; j < E2; ++j) {
-        const uint32_t pos = (uint32_t)w * E2 * kWave + (uint32_t)j * kWave + lane;
-        e[j] = pos < M ? in[pos] : 0ull;
-        tv[j] = (uint32_t)(e[j] >> 32);
-    }
-    block_topl<256, E2>(tv, L, lists + (size_t)(sh.v0 + vs) * sh.RS + (size_t)k * GLp,
-                        [&](int j) { return e[j]; });
-}
-
-template <int E2>
-__global__ __launch_bounds__(256) void k_la_merge(const uint64_t *__restrict__ clists, uint32_t M,
-                                                  uint32_t L, LaShard sh, uint32_t GLp,
-                                                  uint64_t *__restrict__ lists) {
-    la_merge_block<E2>(blockIdx.x, clists, M, L, sh, GLp, lists);
-}
-
-// Entry m (0 <= m < EPL) of resolver lane `lane` for window pod `pod`.  Lists are laid out
-// [shard][pod][GLp] (GLp = 64 * 2^lr entries per pod and shard: the all-gathered layout of the
-// sharded engine); entries of shards >= W read as empty.
-__device__ __forceinline__ uint64_t list_ent(const uint64_t *__restrict__ lists, uint32_t pod,
-                                             uint32_t GLp, uint32_t lr, const LaShard &sh, int m,
-                                             int lane) {
-    const uint32_t q = (uint32_t)m >> lr;
-    if (q >= sh.W) return 0ull;
-    return lists[(size_t)q * sh.RS + (size_t)pod * GLp + (uint32_t)lane +
-                 64u * ((uint32_t)m & ((1u << lr) - 1u))];
-}
-
-// One wave resolves the window sequentially (spec S7 order).  Dirty (modified-in-window) node
-// rows live in the lanes' registers (slot = lane); a dynamic-LDS bitmap marks dirty nodes.
-// Per pod, off the critical path: the window's pod records sit one per lane (read by readlane),
-// the next pod's list entries are prefetched, and every lane prefetches the row of its best clean
-// candidate so that a newly dirtied winner's row is already in a register when the argmax lands.
-// Results are kept one per lane (lane i = pod i) and stored once per window.
-// Diagnostic build only (DIAG = true, QS_DIAG=1 at run time): shader-clock stamps per segment.
-__device__ __forceinline__ uint64_t diag_stamp() {
-    uint64_t t;
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-    __builtin_amdgcn_sched_barrier(0);
-    return t;
-}
-#define QS_STAMP(k)                                  \
-    if (DIAG) {                                      \
-        const uint64_t t_ = diag_stamp();            \
-        dsum[k] += t_ - tprev;                       \
-        tprev = t_;                                  \
-    }
-
-template <uint32_t F, int EPL, bool DIAG>
-__global__ __launch_bounds__(64) void k_la_resolve(DevTable t, const DPod *__restrict__ pods,
-                                                   DevCfg c, uint32_t s0, uint32_t P, uint32_t K,
-                                                   uint32_t GLp, uint32_t lr, LaShard sh,
-                                                   const uint64_t *__restrict__ lists,
-                                                   int32_t *__restrict__ out_node,
-                                                   uint64_t *__restrict__ out_key,
-                                                   uint64_t *__restrict__ stamps,
-                                                   uint64_t *__restrict__ diag) {
-    uint64_t dsum[6] = {0, 0, 0, 0, 0, 0};
-    uint64_t tprev = 0;
-    extern __shared__ __attribute__((aligned(16))) uint32_t dirty[];
-    const int lane = threadIdx.x;
-    const uint32_t nwords = (t.n + 31) / 32;
-    for (uint32_t i = lane; i < nwords; i += 64) dirty[i] = 0;
-    const uint32_t kend = min(K, P - s0);
-    // staging area for a newly dirtied row (after the bitmap; 16-byte aligned)
-    Row *stage = (Row *)(dirty + ((nwords + 3) & ~3u));
-    RowX *stagex = (RowX *)(stage + 1);
-    DPod pn = pods[s0];  // uniform: scalar loads, prefetched one pod ahead
-    const DPodX px{};
-    Row dr = empty_row();
-    RowX dx{};
-    uint32_t didx = 0xFFFFFFFFu;
-    uint32_t nd = 0;
-    uint64_t res_key = 0, res_stamp = 0;
-    // Software pipeline (three pods in flight):
-    //   pod i:   clean candidate = top-1 of the lane's entries, or top-2 when top-1 is the previous
-    //            pod's winner (both rows loaded one pod earlier: no memory or LDS on the path);
-    //   pod i+1: top-2 clean entries against the current dirty set (LDS bitmap) + their row loads;
-    //   pod i+2: list entries loaded.
-    uint64_t ent1[EPL], ent2[EPL];
-#pragma unroll
-    for (int m = 0; m < EPL; ++m) ent1[m] = list_ent(lists, 0, GLp, lr, sh, m, lane);
-#pragma unroll
-    for (int m = 0; m < EPL; ++m) ent2[m] = kend > 1 ? list_ent(lists, 1, GLp, lr, sh, m, lane) : 0ull;
-    __syncthreads();
-    // top-2 clean entries of a pod's list against the dirty bitmap
-    auto top2 = [&](const uint64_t (&e)[EPL], uint64_t &c1, uint64_t &c2) {
-        uint32_t word[EPL];
-#pragma unroll
-        for (int m = 0; m < EPL; ++m) {
-            const uint32_t nidx = e[m] ? key_node(e[m]) : 0u;
-            word[m] = dirty[nidx >> 5] >> (nidx & 31);
-        }
-        c1 = 0;
-        c2 = 0;
-#pragma unroll
-        for (int m = 0; m < EPL; ++m) {
-            const uint64_t x = (word[m] & 1u) ? 0ull : e[m];
-            const bool gt1 = x > c1;
-            c2 = gt1 ? c1 : (x > c2 ? x : c2);
-            c1 = gt1 ? x : c1;
-        }
-    };
-    uint64_t c1, c2;
-    top2(ent1, c1, c2);
-    Row r1 = load_row(t, c1 ? key_node(c1) : 0u), r2 = load_row(t, c2 ? key_node(c2) : 0u);
-    RowX x1 = load_rowx<F>(t, c1 ? key_node(c1) : 0u), x2 = load_rowx<F>(t, c2 ? key_node(c2) : 0u);
-    uint32_t wprev = 0xFFFFFFFFu;
-    if (DIAG) tprev = diag_stamp();
-    for (uint32_t i = 0; i < kend; ++i) {
-        const DPod p = pn;
-        if (i + 1 < kend) pn = pods[s0 + i + 1];
-        // this pod's clean candidate: the previous winner is the only node dirtied since top2()
-        const bool use2 = c1 && key_node(c1) == wprev;
-        const uint64_t cand = use2 ? c2 : c1;
-        const Row crow = sel_row(use2, r2, r1);
-        const RowX cx = sel_rowx(use2, x2, x1);
-        QS_STAMP(0)
-        // next pod: top-2 clean entries and their rows; the pod after: its list entries
-        if (i + 1 < kend) {
-            top2(ent2, c1, c2);
-            r1 = load_row(t, c1 ? key_node(c1) : 0u);
-            r2 = load_row(t, c2 ? key_node(c2) : 0u);
-            x1 = load_rowx<F>(t, c1 ? key_node(c1) : 0u);
-            x2 = load_rowx<F>(t, c2 ? key_node(c2) : 0u);
-        }
-        if (i + 2 < kend) {
-#pragma unroll
-            for (int m = 0; m < EPL; ++m) ent2[m] = list_ent(lists, i + 2, GLp, lr, sh, m, lane);
-        }
-        QS_STAMP(1)
-        // fresh keys of the dirty slots
-        const bool f = feasible<F>(dr, dx, p, px);
-        const uint32_t tot = node_total<F>(dr, dx, p, px, c, 0, 0.0, 0, 0.0, nullptr);
-        const uint64_t fk = ((uint32_t)lane < nd && f) ? pack_key(tot + 1, didx) : 0ull;
-        const uint64_t best = fk > cand ? fk : cand;
-        QS_STAMP(2)
-        const uint64_t ks = wave_max_u64(best);
-        QS_STAMP(3)
-        if (ks) {
-            const uint32_t win = key_node(ks);
-            const bool own = (uint32_t)lane < nd && didx == win;
-            if (__ballot(own)) {
-                if (own) reserve(dr, dx, p, +1);
-            } else {
-                // the winner is a clean node: its row was prefetched by the lane whose cand == ks;
-                // hand it to slot lane nd through LDS (same wave: LDS operations stay in order)
-                const int src = (int)__builtin_ctzll(__ballot(cand == ks));
-                if (lane == src) { *stage = crow; if (F & kFeatExt) *stagex = cx; }
-                const Row nr = *stage;
-                RowX nx{};
-                if (F & kFeatExt) nx = *stagex;
-                if ((uint32_t)lane == nd) {
-                    dr = nr;
-                    dx = nx;
-                    reserve(dr, dx, p, +1);
-                    didx = win;
-                    dirty[win >> 5] |= 1u << (win & 31);
-                }
-                ++nd;
-            }
-        }
-        wprev = ks ? key_node(ks) : 0xFFFFFFFFu;
-        QS_STAMP(4)
-        if ((uint32_t)lane == i) {
-            res_key = ks;
-            if (stamps) res_stamp = __builtin_amdgcn_s_memrealtime();
-        }
-    }
-    if (DIAG && lane == 0) {
-        for (int k = 0; k < 5; ++k) atomicAdd((unsigned long long *)&diag[k], (unsigned long long)dsum[k]);
-        atomicAdd((unsigned long long *)&diag[5], (unsigned long long)kend);
-    }
-    if ((uint32_t)lane < kend) {
-        const uint32_t s = s0 + lane;
-        out_node[s] = res_key ? (int32_t)key_node(res_key) : -1;
-        if (out_key) out_key[s] = res_key;
-        if (stamps) stamps[s] = res_stamp;
-    }
-    if ((uint32_t)lane < nd) { store_dyn(t, didx, dr); store_dynx<F>(t, didx, dx); }
-}
-
-// Single-wave resolver for normalizing profiles (TaintToleration / NodeAffinity on).  Keys carry
-// per-pod normalized scores, so a list is only valid while the pod's selection-time maxima (nf)
-// still hold.  The feasible set only shrinks during a stream, and only dirty nodes changed, so a
-// maximum still holds whenever fewer of its holders than nf.ct / nf.ca are dirty AND infeasible
-// now; otherwise (rare: few holders left) the wave rescans every node at the current state for
-// the exact maxima and keys (`nfall` counts those pods).  Supports overlapped windows (dprev/dcur)
-// like k_la_resolve4.  Four waves run the walk redundantly (identical lane state, LDS writes of
-// identical values, one barrier per pod) so that an exact rescan is spread over all four SIMDs;
-// only wave 0 writes results.
-constexpr uint32_t kResNormWaves = 4;
-template <uint32_t F, int EPL>
-__global__ __launch_bounds__(64 * kResNormWaves) void k_la_resolve_norm(
-    DevTable t, const DPod *__restrict__ pods, const DPodX *__restrict__ podx, DevCfg c,
-    uint32_t s0, uint32_t P, uint32_t K, uint32_t GLp, uint32_t lr, LaShard sh,
-    const uint64_t *__restrict__ lists, const NormInfo *__restrict__ norm,
-    int32_t *__restrict__ out_node, uint64_t *__restrict__ out_key, uint64_t *__restrict__ stamps,
-    const uint32_t *__restrict__ dprev, uint32_t *__restrict__ dcur, unsigned long long *nfall,
-    const uint32_t *__restrict__ rec) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    __shared__ uint32_t red_m[2 * kResNormWaves];  // per-wave rescan maxima (taint, affinity)
-    __shared__ uint64_t red_k[kResNormWaves];      // per-wave rescan best keys
-    const int lane = threadIdx.x & 63;
-    const uint32_t wid = threadIdx.x >> 6;
-    // Resume mode (rec != nullptr, after the four-wave resolver of the same window): nothing to do
-    // unless it stopped at pod rec[0]; then continue from there with its slots (rec[1] nodes at
-    // rec[4..], rows already stored, won mask rec[2..3]) as the initial dirty set.
-    uint32_t pbase = 0;
-    uint64_t won0 = 0;
-    const uint32_t *init = dprev;
-    if (rec) {
-        const uint32_t stop = rec[0];
-        if (stop == 0xFFFFFFFFu) return;
-        if (threadIdx.x == 0 && nfall) atomicAdd(nfall + 1, 1ull);  // resumed windows (QS_NORM_DIAG)
-        pbase = stop;
-        s0 += stop;
-        K -= stop;
-        won0 = (uint64_t)rec[2] | ((uint64_t)rec[3] << 32);
-        init = rec + 3;  // init[1 + j] = rec[4 + j]; the count is rec[1]
-    }
-    const uint32_t n = t.n, nwords = (n + 31) / 32;
-    uint32_t *dirty = lds;
-    Row *srow = (Row *)(lds + ((nwords + 3) & ~3u));  // [64] slot rows, staged for a rescan
-    RowX *sx = (RowX *)(srow + 64);                    // [64]
-    Row *stage = (Row *)(sx + 64);                     // newly dirtied row hand-off
-    RowX *stagex = (RowX *)(stage + 1);
-    uint32_t *sidx = (uint32_t *)(stagex + 1);         // [64] slot -> node, staged for a rescan
-    for (uint32_t i = lane; i < nwords; i += 64) dirty[i] = 0;
-    const uint32_t kend = min(K, P - s0);
-    const uint32_t nd0 = rec ? rec[1] : (dprev ? dprev[0] : 0u);
-    __syncthreads();
-    Row dr = empty_row();
-    RowX dx{};
-    uint32_t didx = 0xFFFFFFFFu;
-    if ((uint32_t)lane < nd0) {
-        didx = init[1 + lane];
-        dr = load_row(t, didx);
-        dx = load_rowx<F>(t, didx);
-        atomicOr(&dirty[didx >> 5], 1u << (didx & 31));
-    }
-    uint32_t nd = nd0;
-    bool won = (uint32_t)lane < nd0 && ((won0 >> lane) & 1ull);
-    uint64_t res_key = 0, res_stamp = 0;
-    __syncthreads();
-    auto top2 = [&](const uint64_t(&e)[EPL], uint64_t &c1, uint64_t &c2) {
-        uint32_t word[EPL];
-#pragma unroll
-        for (int m = 0; m < EPL; ++m) {
-            const uint32_t nidx = e[m] ? key_node(e[m]) : 0u;
-            word[m] = dirty[nidx >> 5] >> (nidx & 31);
-        }
-        c1 = c2 = 0;
-#pragma unroll
-        for (int m = 0; m < EPL; ++m) {
-            const uint64_t x = (word[m] & 1u) ? 0ull : e[m];
-            const bool gt1 = x > c1;
-            c2 = gt1 ? c1 : (x > c2 ? x : c2);
-            c1 = gt1 ? x : c1;
-        }
-    };
-    uint64_t ent1[EPL], ent2[EPL];
-#pragma unroll
-    for (int m = 0; m < EPL; ++m) ent1[m] = list_ent(lists, pbase, GLp, lr, sh, m, lane);
-#pragma unroll
-    for (int m = 0; m < EPL; ++m) ent2[m] = kend > 1 ? list_ent(lists, pbase + 1, GLp, lr, sh, m, lane) : 0ull;
-    uint64_t c1, c2;
-    top2(ent1, c1, c2);
-    Row r1 = load_row(t, c1 ? key_node(c1) : 0u), r2 = load_row(t, c2 ? key_node(c2) : 0u);
-    RowX x1 = load_rowx<F>(t, c1 ? key_node(c1) : 0u), x2 = load_rowx<F>(t, c2 ? key_node(c2) : 0u);
-    uint32_t wprev = 0xFFFFFFFFu;
-    // pod records + normalization facts, one pod ahead, through the vector path (scalar copies
-    // of the 44-dword extension record spilled the SGPRs)
-    DPod pn = load_vgpr(pods + s0);
-    DPodX pxn = load_vgpr(podx + s0);
-    NormInfo nfn = load_vgpr(norm + pbase);
-    for (uint32_t i = 0; i < kend; ++i) {
-        const DPod p = pn;
-        const DPodX px = pxn;
-        const NormInfo nf = nfn;
-        if (i + 1 < kend) {
-            pn = load_vgpr(pods + s0 + i + 1);
-            pxn = load_vgpr(podx + s0 + i + 1);
-            nfn = load_vgpr(norm + pbase + i + 1);
-        }
-        const bool use2 = c1 && key_node(c1) == wprev;
-        const uint64_t cand = use2 ? c2 : c1;
-        const Row crow = sel_row(use2, r2, r1);
-        const RowX cx = sel_rowx(use2, x2, x1);
-        if (i + 1 < kend) {  // next pod's candidates and rows; the pod after: its list entries
-            top2(ent2, c1, c2);
-            r1 = load_row(t, c1 ? key_node(c1) : 0u);
-            r2 = load_row(t, c2 ? key_node(c2) : 0u);
-            x1 = load_rowx<F>(t, c1 ? key_node(c1) : 0u);
-            x2 = load_rowx<F>(t, c2 ? key_node(c2) : 0u);
-        }
-        if (i + 2 < kend) {
-#pragma unroll
-            for (int m = 0; m < EPL; ++m) ent2[m] = list_ent(lists, pbase + i + 2, GLp, lr, sh, m, lane);
-        }
-        const double ymt = rcp_exact(nf.mt), yma = rcp_exact(nf.ma);
-        const bool act = (uint32_t)lane < nd;
-        const bool f = feasible<F>(dr, dx, p, px);
-        const uint32_t tot = node_total<F>(dr, dx, p, px, c, nf.mt, ymt, nf.ma, yma, nullptr);
-        const uint64_t fk = (act && f) ? pack_key(tot + 1, didx) : 0ull;
-        // do the selection-time maxima still hold?  (holders lost = dirty, infeasible now)
-        bool unsafe = false;
-        if (F & kFeatTaint) {
-            const uint32_t lost = (uint32_t)__popcll(__ballot(act && !f && taint_raw(dx, px) == nf.mt));
-            unsafe |= nf.mt > 0 && lost >= nf.ct;
-        }
-        if (F & kFeatAffinity) {
-            const uint32_t lost = (uint32_t)__popcll(__ballot(act && !f && affinity_raw(dx, p, px) == nf.ma));
-            unsafe |= nf.ma > 0 && lost >= nf.ca;
-        }
-        uint64_t ks;
-        if (!unsafe) {
-            ks = wave_max_u64(fk > cand ? fk : cand);
-        } else {
-            // exact rescan at the current state: slot rows from LDS, every other row from HBM
-            if (act) { srow[lane] = dr; sx[lane] = dx; sidx[lane] = didx; }
-            // both passes keep U rows per lane in flight (one wave, dependent loads otherwise):
-            // every row is loaded unconditionally first, and only then are the few dirty ones
-            // (held by a slot, stale in HBM) replaced from LDS, so no branch or search loop sits
-            // between the loads and forces them to complete one by one
-            constexpr uint32_t U = 8;
-            auto rows_at = [&](uint32_t b0, Row (&r)[U], RowX (&x)[U]) {
-#pragma unroll
-                for (uint32_t u = 0; u < U; ++u) {
-                    const uint32_t idx = b0 + 64 * u < n ? b0 + 64 * u : 0u;
-                    r[u] = load_row(t, idx);
-                    x[u] = load_rowx<F>(t, idx);
-                }
-#pragma unroll
-                for (uint32_t u = 0; u < U; ++u) {
-                    const uint32_t idx = b0 + 64 * u;
-                    if (idx < n && ((dirty[idx >> 5] >> (idx & 31)) & 1u)) {
-                        uint32_t j = 0;
-                        while (j < nd && sidx[j] != idx) ++j;  // dirty => held by a slot
-                        r[u] = srow[j];
-                        x[u] = sx[j];
-                    }
-                }
-            };
-            uint32_t mt = 0, ma = 0;
-            for (uint32_t b0 = wid * 64 * U + lane; b0 < n; b0 += kResNormWaves * 64 * U) {
-                Row r[U];
-                RowX x[U];
-                rows_at(b0, r, x);
-#pragma unroll
-                for (uint32_t u = 0; u < U; ++u) {
-                    if (b0 + 64 * u < n && feasible<F>(r[u], x[u], p, px)) {
-                        const uint32_t a = taint_raw(x[u], px), b2 = affinity_raw(x[u], p, px);
-                        mt = a > mt ? a : mt;
-                        ma = b2 > ma ? b2 : ma;
-                    }
-                }
-            }
-            mt = (F & kFeatTaint) ? wave_max_u32(mt) : 0u;
-            ma = (F & kFeatAffinity) ? wave_max_u32(ma) : 0u;
-            if (lane == 0) { red_m[2 * wid] = mt; red_m[2 * wid + 1] = ma; }
-            __syncthreads();
-#pragma unroll
-            for (uint32_t w = 0; w < kResNormWaves; ++w) {
-                mt = red_m[2 * w] > mt ? red_m[2 * w] : mt;
-                ma = red_m[2 * w + 1] > ma ? red_m[2 * w + 1] : ma;
-            }
-            const double ymt2 = rcp_exact(mt), yma2 = rcp_exact(ma);
-            uint64_t best = 0;
-            for (uint32_t b0 = wid * 64 * U + lane; b0 < n; b0 += kResNormWaves * 64 * U) {
-                Row r[U];
-                RowX x[U];
-                rows_at(b0, r, x);
-#pragma unroll
-                for (uint32_t u = 0; u < U; ++u) {
-                    const uint32_t idx = b0 + 64 * u;
-                    const uint32_t tv = node_total<F>(r[u], x[u], p, px, c, mt, ymt2, ma, yma2, nullptr);
-                    const uint64_t key = (idx < n && feasible<F>(r[u], x[u], p, px)) ? pack_key(tv + 1, idx) : 0ull;
-                    best = key > best ? key : best;
-                }
-            }
-            ks = wave_max_u64(best);
-            if (lane == 0) red_k[wid] = ks;
-            __syncthreads();
-#pragma unroll
-            for (uint32_t w = 0; w < kResNormWaves; ++w) ks = red_k[w] > ks ? red_k[w] : ks;
-            if (threadIdx.x == 0 && nfall) atomicAdd(nfall, 1ull);
-        }
-        __syncthreads();  // every wave has read this pod's dirty bits before any marks the winner
-        if (ks) {
-            const uint32_t win = key_node(ks);
-            const uint64_t own = __ballot(act && didx == win);
-            if (own) {
-                if (lane == __builtin_ctzll(own)) { reserve(dr, dx, p, +1); won = true; }
-            } else {
-                // clean winner: its row was prefetched by a lane whose candidate it is (after a
-                // rescan it may be nobody's candidate: then lane 0 loads it)
-                const uint64_t srcm = __ballot(cand == ks);
-                if (srcm) {
-                    if (lane == __builtin_ctzll(srcm)) { *stage = crow; *stagex = cx; }
-                } else if (lane == 0) {
-                    *stage = load_row(t, win);
-                    *stagex = load_rowx<F>(t, win);
-                }
-                const Row nr = *stage;
-                const RowX nx = *stagex;
-                if ((uint32_t)lane == nd) {
-                    dr = nr;
-                    dx = nx;
-                    reserve(dr, dx, p, +1);
-                    didx = win;
-                    won = true;
-                    dirty[win >> 5] |= 1u << (win & 31);
-                }
-                ++nd;
-            }
-        }
-        wprev = ks ? key_node(ks) : 0xFFFFFFFFu;
-        if ((uint32_t)lane == i) {
-            res_key = ks;
-            if (stamps) res_stamp = __builtin_amdgcn_s_memrealtime();
-        }
-        __syncthreads();  // no wave overwrites stage / the rescan partials while another reads them
-    }
-    if (wid != 0) return;
-    if ((uint32_t)lane < kend) {
-        const uint32_t s = s0 + lane;
-        out_node[s] = res_key ? (int32_t)key_node(res_key) : -1;
-        if (out_key) out_key[s] = res_key;
-        if (stamps) stamps[s] = res_stamp;
-    }
-    if ((uint32_t)lane < nd) { store_dyn(t, didx, dr); store_dynx<F>(t, didx, dx); }
-    if (dcur) {
-        const uint64_t wm = __ballot(won && (uint32_t)lane < nd);
-        if (won && (uint32_t)lane < nd) dcur[1 + __popcll(wm & ((1ull << lane) - 1ull))] = didx;
-        if (lane == 0) dcur[0] = (uint32_t)__popcll(wm);
-    }
-}
-
-// ---------------------------------------------------------------------------------------------
-// Four-wave pipelined resolver (one wave per SIMD).  Pod i's dirty-slot keys never wait for an
-// evaluation: they were computed during pod i-1 for both outcomes —
-//   wave A: A_l = key_{i+1}(slot_l)              (slot l not the winner of pod i)
-//   wave B: B_l = key_{i+1}(slot_l + pod i)      (slot l wins pod i)
-//   wave C: C_l = key_{i+1}(cand_l(i) + pod i)   (lane l's clean candidate wins pod i: new slot),
-//           plus the top-2 clean list entries of pod i+1 and their rows (loaded one pod ahead);
-//   wave D: picks pod i's keys from A/B/C with pod i-1's winner, argmax, publishes the winner.
-// One LDS exchange + one s_barrier per pod.  Slot rows are replicated in waves A and B; a new
-// slot's row comes from wave C's staging copy of its candidate row.
-struct alignas(16) ResPub {
-    uint64_t ks;     // packed key of the winner (0 = unschedulable)
-    uint32_t w;      // winner node
-    int32_t slot;    // existing dirty slot that won, or -1
-    int32_t src;     // lane whose clean candidate won (new slot)
-    uint32_t nd_old; // lane of the new slot
-    uint32_t pad[2];
-};
-// One 32-byte LDS read of the published winner (two ds_read_b128 issued together; reading the
-// fields lazily under branches serialised four LDS round trips).
-__device__ __forceinline__ ResPub read_pub(const ResPub *p) {
-    const uint4 a = reinterpret_cast<const uint4 *>(p)[0];
-    const uint4 b = reinterpret_cast<const uint4 *>(p)[1];
-    ResPub r;
-    r.ks = ((uint64_t)a.y << 32) | a.x;
-    r.w = a.z;
-    r.slot = (int32_t)a.w;
-    r.src = (int32_t)b.x;
-    r.nd_old = b.y;
-    r.pad[0] = r.pad[1] = 0;
-    return r;
-}
-
-template <uint32_t F, int EPL, bool DIAG, bool K32>
-__device__ __forceinline__ void la_resolve4_block(uint32_t *lds, const DevTable &t, const DPod *__restrict__ pods,
-                                                  const DevCfg &c, uint32_t s0, uint32_t P,
-                                                  uint32_t K, uint32_t GLp, uint32_t lr,
-                                                  const LaShard &sh,
-                                                  const uint64_t *__restrict__ lists,
-                                                  int32_t *__restrict__ out_node,
-                                                  uint64_t *__restrict__ out_key,
-                                                  uint64_t *__restrict__ stamps,
-                                                  uint64_t *__restrict__ diag,
-                                                  const uint32_t *__restrict__ dprev,
-                                                  uint32_t *__restrict__ dcur,
-                                                  const DPodX *__restrict__ podx = nullptr,
-                                                  const NormInfo *__restrict__ norm = nullptr,
-                                                  uint32_t *__restrict__ rec = nullptr) {
-    constexpr bool NORM = (F & kFeatNorm) != 0;
-    const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t t_start = DIAG ? diag_stamp() : 0ull;
-    uint64_t t_loop = 0;
-    const uint32_t nwords = (t.n + 31) / 32;
-    uint32_t *dirty = lds;
-    char *base = (char *)(lds + ((nwords + 3) & ~3u));
-    uint64_t(*keyA)[64] = (uint64_t(*)[64])base; base += 2 * 64 * 8;
-    uint64_t(*keyB)[64] = (uint64_t(*)[64])base; base += 2 * 64 * 8;
-    uint64_t(*keyC)[64] = (uint64_t(*)[64])base; base += 2 * 64 * 8;
-    uint64_t(*C1)[64] = (uint64_t(*)[64])base; base += 2 * 64 * 8;
-    uint64_t(*C2)[64] = (uint64_t(*)[64])base; base += 2 * 64 * 8;
-    Row(*stage)[64] = (Row(*)[64])base; base += 2 * 64 * sizeof(Row);
-    int4(*stagex)[64] = (int4(*)[64])base; base += 2 * 64 * sizeof(int4);
-    ResPub *pub = (ResPub *)base; base += 2 * sizeof(ResPub);
-    uint32_t *slotnode = (uint32_t *)base; base += 64 * 4;
-    DPod *wpods = (DPod *)base; base += 64 * sizeof(DPod);  // the window's pod records (K <= 64)
-    // normalizing profiles only (the host sizes the LDS accordingly): pod extensions, the
-    // selection-time maxima and their reciprocals, C's lost-holder flags, full staged RowX
-    DPodX *wpodx = (DPodX *)base; base += 64 * sizeof(DPodX);
-    NormInfo *wnorm = (NormInfo *)base; base += 64 * sizeof(NormInfo);
-    double2 *wrcp = (double2 *)base; base += 64 * sizeof(double2);
-    uint32_t(*flagC)[64] = (uint32_t(*)[64])base; base += 2 * 64 * 4;
-    RowX(*stagexN)[64] = (RowX(*)[64])base;
-
-    for (uint32_t i = threadIdx.x; i < nwords; i += 256) dirty[i] = 0;
-    if (threadIdx.x == 0) pub[1] = ResPub{0, 0xFFFFFFFFu, -1, -1, 0, {0, 0}};
-    const uint32_t kend = min(K, P - s0);
-    if (threadIdx.x < kend) wpods[threadIdx.x] = pods[s0 + threadIdx.x];
-    if (NORM) {
-        constexpr uint32_t q = sizeof(DPodX) / 16;
-        for (uint32_t j = threadIdx.x; j < kend * q; j += 256)
-            reinterpret_cast<uint4 *>(wpodx)[j] = reinterpret_cast<const uint4 *>(podx + s0)[j];
-        if (threadIdx.x < kend) {
-            const NormInfo nf = norm[threadIdx.x];
-            wnorm[threadIdx.x] = nf;
-            wrcp[threadIdx.x] = make_double2(rcp_exact(nf.mt), rcp_exact(nf.ma));
-        }
-    }
-    const DPodX px{};
-    // Overlapped windows (dprev != nullptr): this window's lists were selected against the table
-    // as it stood BEFORE the previous window, so the nodes that window dirtied (dprev[1..nd0])
-    // start as dirty slots: their list entries are stale and their rows are re-read here.
-    const uint32_t nd0 = dprev ? dprev[0] : 0u;
-    __syncthreads();
-    if (threadIdx.x < nd0) {
-        const uint32_t nn = dprev[1 + threadIdx.x];
-        atomicOr(&dirty[nn >> 5], 1u << (nn & 31));
-    }
-    __syncthreads();
-    if (kend == 0) return;
-    uint64_t dsum = 0, tprev = 0, dpart = 0, dwait = 0;
-#define QS_DIAG_BEGIN() if (DIAG) tprev = diag_stamp();
-#define QS_DIAG_END() if (DIAG) { const uint64_t t_ = diag_stamp(); dsum += t_ - tprev; }
-
-    // Each role runs its own loop; every wave executes one s_barrier per pod (+1 prologue), so
-    // the barriers pair up.  Roles never share registers, which keeps waitcnt placement local.
-    if (wv == 0) {
-        // ---- D: pod i's winner from the precomputed keys ---------------------------------------
-        uint32_t nd = nd0, didx = (uint32_t)lane < nd0 ? dprev[1 + lane] : 0xFFFFFFFFu;
-        bool won = false;  // slot won a pod of THIS window (it belongs to the next window's dprev)
-        uint64_t res_key = 0, res_stamp = 0;
-        uint32_t kdone = kend;  // normalizing profiles: the pod a stop hands to the resume kernel
-        ResPub pv{0, 0xFFFFFFFFu, -1, -1, 0, {0, 0}};  // D produced it: kept in registers
-        __syncthreads();  // prologue barrier (wave C publishes pod 0's candidates)
-        if (DIAG && lane == 0) atomicAdd((unsigned long long *)&diag[8], (unsigned long long)(diag_stamp() - t_start));
-        for (uint32_t i = 0; i < kend; ++i) {
-            QS_DIAG_BEGIN()
-            const int par = i & 1, pp = par ^ 1;
-            // every LDS read of the step is independent of this step: one batch, one wait
-            const uint64_t a = keyA[pp][lane], b = keyB[pp][lane], cl = keyC[pp][lane];
-            const uint64_t e1 = C1[pp][lane], e2 = EPL > 1 ? C2[pp][lane] : 0ull;
-            const bool pnew = pv.ks != 0 && pv.slot < 0;
-            uint64_t sc = (lane == pv.slot) ? b : a;
-            uint32_t fl = 0;  // NORM: lost-holder flags of this slot (bit 0 taint, bit 1 affinity)
-            if (NORM) {
-                fl = (uint32_t)sc & 3u;
-                sc &= ~3ull;
-            }
-            uint64_t fk = ((uint32_t)lane < nd && sc) ? (sc | (uint64_t)(0xFFFFFFFFu - didx)) : 0ull;
-            if (pnew) {
-                const uint64_t cw = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(cl >> 32), pv.src) << 32) |
-                                    (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)cl, pv.src);
-                if ((uint32_t)lane == pv.nd_old) fk = cw;
-                if (NORM) {
-                    const uint32_t fc = (uint32_t)__builtin_amdgcn_readlane((int)flagC[pp][lane], pv.src);
-                    if ((uint32_t)lane == pv.nd_old) fl = fc;
-                }
-            }
-            if (NORM) {
-                // do the selection-time maxima still hold for pod i?  A maximum is lost only when
-                // every node attaining it is dirty and infeasible now; then the resume kernel
-                // (k_la_resolve_norm) takes over from pod i with an exact rescan
-                const NormInfo nf = wnorm[i];
-                bool unsafe = false;
-                if (F & kFeatTaint)
-                    unsafe |= nf.mt > 0 && (uint32_t)__popcll(__ballot((uint32_t)lane < nd && (fl & 1u))) >= nf.ct;
-                if (F & kFeatAffinity)
-                    unsafe |= nf.ma > 0 && (uint32_t)__popcll(__ballot((uint32_t)lane < nd && (fl & 2u))) >= nf.ca;
-                if (unsafe) {
-                    if (lane == 0) pub[par] = ResPub{0, 0xFFFFFFFFu, -2, -1, nd, {0, 0}};  // STOP
-                    kdone = i;
-                    __syncthreads();
-                    break;
-                }
-            }
-            const uint64_t cand = (pv.ks != 0 && e1 != 0 && key_node(e1) == pv.w) ? e2 : e1;
-            const uint64_t best = fk > cand ? fk : cand;
-            uint64_t ks;
-            if (K32) {  // (score+1) < 2^10 and n <= 2^22: one 32-bit reduction
-                const uint32_t tv = (uint32_t)(best >> 32);
-                const uint32_t k32 = tv ? (tv << 22) | (0x3FFFFFu - key_node(best)) : 0u;
-                const uint32_t m = wave_max_u32(k32);
-                ks = m ? (((uint64_t)(m >> 22) << 32) | (uint64_t)(0xFFFFFFFFu - (0x3FFFFFu - (m & 0x3FFFFFu)))) : 0ull;
-            } else {
-                ks = wave_max_u64(best);
-            }
-            ResPub np{ks, ks ? key_node(ks) : 0xFFFFFFFFu, -1, -1, nd, {0, 0}};
-            if (ks) {
-                const uint64_t own = __ballot((uint32_t)lane < nd && didx == np.w);
-                if (own) {
-                    np.slot = (int32_t)__builtin_ctzll(own);
-                    won |= lane == np.slot;
-                } else {
-                    np.src = (int32_t)__builtin_ctzll(__ballot(cand == ks));
-                    if ((uint32_t)lane == nd) { didx = np.w; won = true; }
-                    ++nd;
-                }
-            }
-            pv = np;
-            if (lane == 0) pub[par] = np;
-            if ((uint32_t)lane == i) {
-                res_key = ks;
-                if (stamps) res_stamp = __builtin_amdgcn_s_memrealtime();
-            }
-            QS_DIAG_END()
-            __syncthreads();
-        }
-        if (DIAG) t_loop = diag_stamp();
-        if ((uint32_t)lane < kdone) {
-            const uint32_t s = s0 + lane;
-            out_node[s] = res_key ? (int32_t)key_node(res_key) : -1;
-            if (out_key) out_key[s] = res_key;
-            if (stamps) stamps[s] = res_stamp;
-        }
-        if ((uint32_t)lane < nd) slotnode[lane] = didx;
-        if (kdone < kend) {
-            // stopped: hand the window state to the resume kernel — rec = {first pod left, slots,
-            // won mask lo/hi, slot nodes}; it writes dcur when it finishes the window
-            const uint64_t wm = __ballot(won && (uint32_t)lane < nd);
-            if (lane == 0) {
-                rec[0] = kdone;
-                rec[1] = nd;
-                rec[2] = (uint32_t)wm;
-                rec[3] = (uint32_t)(wm >> 32);
-            }
-            if ((uint32_t)lane < nd) rec[4 + lane] = didx;
-        } else {
-            if (rec && lane == 0) rec[0] = 0xFFFFFFFFu;
-            if (dcur) {  // nodes dirtied in this window, for the next (overlapped) window
-                const uint64_t wm = __ballot(won && (uint32_t)lane < nd);
-                if (won && (uint32_t)lane < nd) dcur[1 + __popcll(wm & ((1ull << lane) - 1ull))] = didx;
-                if (lane == 0) dcur[0] = (uint32_t)__popcll(wm);
-            }
-        }
-    } else if (wv <= 2) {
-        // ---- A / B: apply pod i-1 to the slot copy, then the next pod's keys --------------------
-        Row S = empty_row();
-        RowX SX{};
-        uint32_t nd = nd0;
-        if ((uint32_t)lane < nd0) {
-            const uint32_t nn = dprev[1 + lane];
-            S = load_row(t, nn);
-            SX = load_rowx<F>(t, nn);
-        }
-        // score half of a slot key for window pod k (+ NORM lost-holder flags in bits 0-1)
-        // NORM: pod k's extension record, maxima and reciprocals, read from LDS one step ahead
-        struct PodN {
-            DPodX x;
-            NormInfo nf;
-            double2 yr;
-        };
-        auto podn = [&](uint32_t k) -> PodN {
-            PodN r{};
-            if (NORM && k < kend) r = PodN{wpodx[k], wnorm[k], wrcp[k]};
-            return r;
-        };
-        auto slot_key = [&](const Row &r, const RowX &x, uint32_t k, const PodN &pn) -> uint64_t {
-            const DPod &q = wpods[k];
-            const bool act = (uint32_t)lane < nd;
-            if (NORM) {
-                const DPodX &qx = pn.x;
-                const NormInfo nf = pn.nf;
-                const double2 yr = pn.yr;
-                const bool f = feasible<F>(r, x, q, qx);
-                const uint32_t tot = node_total<F>(r, x, q, qx, c, nf.mt, yr.x, nf.ma, yr.y, nullptr);
-                uint32_t fl = 0;
-                if (act && !f) {
-                    if (F & kFeatTaint) fl |= taint_raw(x, qx) == nf.mt ? 1u : 0u;
-                    if (F & kFeatAffinity) fl |= affinity_raw(x, q, qx) == nf.ma ? 2u : 0u;
-                }
-                return ((act && f) ? ((uint64_t)(tot + 1) << 32) : 0ull) | fl;
-            }
-            const bool f = feasible<F>(r, x, q, px);
-            const uint32_t tot = node_total<F>(r, x, q, px, c, 0, 0.0, 0, 0.0, nullptr);
-            return (act && f) ? ((uint64_t)(tot + 1) << 32) : 0ull;
-        };
-        if (wv == 1 && nd0 > 0) keyA[1][lane] = slot_key(S, SX, 0, podn(0));  // pod 0, inherited slots
-        PodN pnx = podn(1);  // pod i+1's record at step i
-        auto apply = [&](const ResPub &pv, int pp, const DPod &pprev) {
-            if (pv.ks == 0) return;
-            if (pv.slot >= 0) {
-                if (lane == pv.slot) reserve(S, SX, pprev, +1);
-            } else {
-                if ((uint32_t)lane == pv.nd_old) {
-                    S = stage[pp][pv.src];
-                    if (NORM) {
-                        SX = stagexN[pp][pv.src];
-                    } else if (F & kFeatExt) {
-                        const int4 e = stagex[pp][pv.src];
-                        SX.ae0 = e.x; SX.re0 = e.y; SX.ae1 = e.z; SX.re1 = e.w;
-                    }
-                    reserve(S, SX, pprev, +1);
-                }
-                ++nd;
-            }
-        };
-        __syncthreads();
-        bool stopped = false;
-        for (uint32_t i = 0; i < kend; ++i) {
-            QS_DIAG_BEGIN()
-            const int par = i & 1, pp = par ^ 1;
-            const ResPub pv = read_pub(&pub[pp]);
-            if (NORM && pv.slot == -2) { stopped = true; break; }  // D stopped at pod i-1
-            if (i > 0) apply(pv, pp, wpods[i - 1]);
-            if (DIAG) { const uint64_t t_ = diag_stamp(); dpart += t_ - tprev; }
-            if (i + 1 < kend) {
-                const PodN pcur = pnx;
-                if (NORM) pnx = podn(i + 2);  // next step's record: its LDS reads overlap this score
-                Row s2 = S;
-                RowX x2s = SX;
-                if (wv == 2) reserve(s2, x2s, wpods[i], +1);
-                // score half only: wave D owns the slot -> node map and fills the index half
-                (wv == 1 ? keyA : keyB)[par][lane] = slot_key(s2, x2s, i + 1, pcur);
-            }
-            QS_DIAG_END()
-            __syncthreads();
-        }
-        // (a stop at the last pod publishes STOP, which apply() ignores: ks == 0)
-        if (wv == 1 && !stopped) apply(read_pub(&pub[(kend - 1) & 1]), (kend - 1) & 1, wpods[kend - 1]);
-        __syncthreads();  // slotnode written by wave D
-        if (wv == 1 && (uint32_t)lane < nd) {
-            const uint32_t node = slotnode[lane];
-            store_dyn(t, node, S);
-            store_dynx<F>(t, node, SX);
-        }
-    } else {
-        // ---- C: candidate rows, C keys, next pod's top-2 ------------------------------------
-        auto top2 = [&](const uint64_t(&e)[EPL], uint64_t &a, uint64_t &b) {
-            uint32_t word[EPL];
-#pragma unroll
-            for (int m = 0; m < EPL; ++m) {
-                const uint32_t nidx = e[m] ? key_node(e[m]) : 0u;
-                word[m] = dirty[nidx >> 5] >> (nidx & 31);
-            }
-            a = 0;
-            b = 0;
-#pragma unroll
-            for (int m = 0; m < EPL; ++m) {
-                const uint64_t x = (word[m] & 1u) ? 0ull : e[m];
-                const bool gt = x > a;
-                b = gt ? a : (x > b ? x : b);
-                a = gt ? x : a;
-            }
-        };
-        auto load_ent = [&](uint64_t(&e)[EPL], uint32_t pod) {
-#pragma unroll
-            for (int m = 0; m < EPL; ++m) e[m] = pod < kend ? list_ent(lists, pod, GLp, lr, sh, m, lane) : 0ull;
-        };
-        uint64_t c1, c2;
-        uint64_t eX[EPL], eY[EPL];  // ping-pong: entries consumed two pods after their load
-        {
-            uint64_t e0[EPL];
-            load_ent(e0, 0);
-            top2(e0, c1, c2);
-        }
-        load_ent(eX, 1);
-        load_ent(eY, 2);
-        // EPL == 1 (merged lists): a lane holds one entry, so its second candidate is always empty
-        constexpr bool TWO = EPL > 1;
-        C1[1][lane] = c1;
-        if (TWO) C2[1][lane] = c2;
-        Row r1 = load_row(t, c1 ? key_node(c1) : 0u), r2 = TWO ? load_row(t, c2 ? key_node(c2) : 0u) : empty_row();
-        RowX x1 = load_rowx<F>(t, c1 ? key_node(c1) : 0u), x2 = TWO ? load_rowx<F>(t, c2 ? key_node(c2) : 0u) : RowX{};
-        __syncthreads();
-        auto step = [&](uint32_t i, uint64_t(&en)[EPL]) -> bool {
-            QS_DIAG_BEGIN()
-            const int par = i & 1, pp = par ^ 1;
-            const ResPub pv = read_pub(&pub[pp]);
-            if (NORM && pv.slot == -2) return false;  // D stopped at pod i-1
-            if (lane == 0 && pv.ks != 0 && pv.slot < 0)
-                __hip_atomic_fetch_or(&dirty[pv.w >> 5], 1u << (pv.w & 31), __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_WORKGROUP);  // ds_or: no round trip
-            const bool use2 = pv.ks != 0 && c1 != 0 && key_node(c1) == pv.w;
-            const uint64_t cc = use2 ? c2 : c1;
-            uint64_t tw0 = 0;
-            if (DIAG) tw0 = diag_stamp();
-            const Row crow = sel_row(use2, r2, r1);
-            const RowX cx = sel_rowx(use2, x2, x1);
-            stage[par][lane] = crow;
-            if (NORM) stagexN[par][lane] = cx;
-            else if (F & kFeatExt) stagex[par][lane] = make_int4(cx.ae0, cx.re0, cx.ae1, cx.re1);
-            if (DIAG) { const uint64_t t_ = diag_stamp(); dwait += t_ - tw0; }
-            if (i + 1 < kend) {
-                const DPod p = wpods[i], pn1 = wpods[i + 1];
-                top2(en, c1, c2);  // pod i+1 against the dirty set through pod i-1
-                C1[par][lane] = c1;
-                if (TWO) C2[par][lane] = c2;
-                r1 = load_row(t, c1 ? key_node(c1) : 0u);
-                x1 = load_rowx<F>(t, c1 ? key_node(c1) : 0u);
-                if (TWO) {
-                    r2 = load_row(t, c2 ? key_node(c2) : 0u);
-                    x2 = load_rowx<F>(t, c2 ? key_node(c2) : 0u);
-                }
-                load_ent(en, i + 3);
-                if (DIAG) { const uint64_t t_ = diag_stamp(); dpart += t_ - tprev; }
-                Row cr = crow;
-                RowX crx = cx;
-                reserve(cr, crx, p, +1);
-                if (NORM) {
-                    const DPodX &qx = wpodx[i + 1];
-                    const NormInfo nf = wnorm[i + 1];
-                    const double2 yr = wrcp[i + 1];
-                    const bool f = feasible<F>(cr, crx, pn1, qx);
-                    const uint32_t tot = node_total<F>(cr, crx, pn1, qx, c, nf.mt, yr.x, nf.ma, yr.y, nullptr);
-                    keyC[par][lane] = (cc != 0 && f) ? pack_key(tot + 1, key_node(cc)) : 0ull;
-                    uint32_t fl = 0;
-                    if (!f) {
-                        if (F & kFeatTaint) fl |= taint_raw(crx, qx) == nf.mt ? 1u : 0u;
-                        if (F & kFeatAffinity) fl |= affinity_raw(crx, pn1, qx) == nf.ma ? 2u : 0u;
-                    }
-                    flagC[par][lane] = fl;
-                } else {
-                    const bool f = feasible<F>(cr, crx, pn1, px);
-                    const uint32_t tot = node_total<F>(cr, crx, pn1, px, c, 0, 0.0, 0, 0.0, nullptr);
-                    keyC[par][lane] = (cc != 0 && f) ? pack_key(tot + 1, key_node(cc)) : 0ull;
-                }
-            }
-            QS_DIAG_END()
-            __syncthreads();
-            return true;
-        };
-        uint32_t i = 0;
-        for (; i + 1 < kend; i += 2) {
-            if (!step(i, eX) || !step(i + 1, eY)) { i = kend; break; }
-        }
-        if (i < kend) step(i, eX);
-        __syncthreads();
-    }
-    if (DIAG && lane == 0) {
-        atomicAdd((unsigned long long *)&diag[wv], (unsigned long long)dsum);
-        if (wv == 0) atomicAdd((unsigned long long *)&diag[5], (unsigned long long)kend);
-        if (wv == 1) atomicAdd((unsigned long long *)&diag[6], (unsigned long long)dpart);
-        if (wv == 3) atomicAdd((unsigned long long *)&diag[7], (unsigned long long)dpart);
-        if (wv == 3) atomicAdd((unsigned long long *)&diag[4], (unsigned long long)dwait);
-        if (wv == 0) atomicAdd((unsigned long long *)&diag[9], (unsigned long long)(diag_stamp() - t_loop));
-    }
-    if (wv == 0) __syncthreads();  // pairs with the post-loop barrier of waves A/B and C
-#undef QS_DIAG_BEGIN
-#undef QS_DIAG_END
-}
-
-template <uint32_t F, int EPL, bool DIAG, bool K32>
-__global__ __launch_bounds__(256) void k_la_resolve4(DevTable t, const DPod *__restrict__ pods,
-                                                     DevCfg c, uint32_t s0, uint32_t P,
-                                                     uint32_t K, uint32_t GLp, uint32_t lr,
-                                                     LaShard sh,
-                                                     const uint64_t *__restrict__ lists,
-                                                     int32_t *__restrict__ out_node,
-                                                     uint64_t *__restrict__ out_key,
-                                                     uint64_t *__restrict__ stamps,
-                                                     uint64_t *__restrict__ diag,
-                                                     const uint32_t *__restrict__ dprev,
-                                                     uint32_t *__restrict__ dcur,
-                                                     const DPodX *__restrict__ podx,
-                                                     const NormInfo *__restrict__ norm,
-                                                     uint32_t *__restrict__ rec) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    la_resolve4_block<F, EPL, DIAG, K32>(lds, t, pods, c, s0, P, K, GLp, lr, sh, lists, out_node, out_key,
-                                         stamps, diag, dprev, dcur, podx, norm, rec);
-}
-
-// =============================================================================================
-// BATCHED mode (spec S11): per batch of B <= 64 pods, k_la_select + k_la_merge give each pod its
-// 64 best keys against the batch-start table; k_batch_claim walks the batch in queue order, each
-// pod claiming its best key whose node (and, for zone anti-affinity, whose (app, zone)) no earlier
-// pod of the batch claimed, then applies every claim (Reserve + anti-affinity state) and builds
-// the next batch: the pods that found no free candidate first, then fresh pods from the stream.
-// ctrl = {pods in the batch, stream cursor}.
-// =============================================================================================
 __global__ void k_batch_init(uint32_t *ctrl, uint32_t *bidx, uint32_t P, uint32_t B) {
     const uint32_t nb = min(P, B);
     if (threadIdx.x < nb) bidx[threadIdx.x] = threadIdx.x;
     if (threadIdx.x == 0) { ctrl[0] = nb; ctrl[1] = nb; }
-}
-
-// Descending bitonic sort of one 64-bit key per lane across the wave (21 compare-exchange steps).
-__device__ __forceinline__ uint64_t wave_sort_desc(uint64_t v, int lane) {
-#pragma unroll
-    for (int k = 2; k <= 64; k <<= 1) {
-#pragma unroll
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, j);
-            const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), j);
-            const uint64_t o = ((uint64_t)hi << 32) | lo;
-            const bool keep_max = ((lane & j) == 0) == ((lane & k) == 0);
-            v = keep_max ? (v > o ? v : o) : (v < o ? v : o);
-        }
-    }
-    return v;
-}
-
-#ifdef QS_CLAIM_DIAG
-__device__ uint64_t g_claim_diag[5];
-#define CLAIM_STAMP0() uint64_t cds[4] = {0, 0, 0, 0}; uint64_t ctp = diag_stamp();
-#define CLAIM_STAMP(q) { const uint64_t t_ = diag_stamp(); cds[q] += t_ - ctp; ctp = t_; }
-#else
-#define CLAIM_STAMP0()
-#define CLAIM_STAMP(q)
-#endif
-constexpr int kClaimWaves = 16;
-
-__global__ __launch_bounds__(64 * kClaimWaves) void k_batch_claim(
-    DevTable t, const DPod *__restrict__ pods, const uint64_t *__restrict__ lists, uint32_t GLp,
-    uint32_t *ctrl, uint32_t *bidx, uint32_t P, uint32_t B, int32_t *__restrict__ out_node,
-    uint64_t *__restrict__ out_key) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    CLAIM_STAMP0();
-    const uint32_t nwords = (t.n + 31) / 32;
-    uint32_t *claimed = lds;                                   // node bitmap
-    uint32_t *claimed_az = lds + ((nwords + 3) & ~3u);         // (app, zone) bitmap
-    uint32_t *pend = claimed_az + kMaxApps * kMaxZones / 32;   // carried pods (<= 64)
-    uint64_t *lkey = (uint64_t *)(pend + 64);                  // [64 pods][64] keys, best first
-    uint32_t *lzone = (uint32_t *)(lkey + 64 * 64);            // [64 pods][64] their zones
-    uint32_t *lpod = lzone + 64 * 64;                          // [64] stream positions, [64] flags
-    const uint32_t nb = ctrl[0], cursor = ctrl[1];
-    for (uint32_t i = tid; i < nwords; i += 64 * kClaimWaves) claimed[i] = 0;
-    for (uint32_t i = tid; i < kMaxApps * kMaxZones / 32; i += 64 * kClaimWaves) claimed_az[i] = 0;
-    // Staging, all waves: each pod's list sorted best-first (so that a pod's claim is the first
-    // still-available lane: one ballot instead of a 64-bit max reduction in the sequential loop)
-    // and, for zone-anti-affinity pods, the zones of its candidates.
-    // Wave wv takes pods wv + 16q (q < 4): all loads of a round are issued before any is used and
-    // the four sorts interleave.
-    {
-        constexpr int Q = 64 / kClaimWaves;
-        uint64_t ev[Q];
-        uint32_t fv[Q];
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            const uint32_t i = (uint32_t)wv + kClaimWaves * q;
-            ev[q] = i < nb ? lists[(size_t)i * GLp + lane] : 0ull;
-            fv[q] = i < nb ? bidx[i] : 0u;
-        }
-        uint32_t sv[Q];
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            sv[q] = fv[q];
-            fv[q] = (uint32_t)wv + kClaimWaves * q < nb ? pods[sv[q]].flags : 0u;
-        }
-#pragma unroll
-        for (int q = 0; q < Q; ++q) ev[q] = wave_sort_desc(ev[q], lane);
-        uint32_t zv[Q];
-#pragma unroll
-        for (int q = 0; q < Q; ++q)
-            zv[q] = (ev[q] && pod_aa(fv[q]) == 2u) ? (uint32_t)t.zone[key_node(ev[q])] : 0u;
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            const uint32_t i = (uint32_t)wv + kClaimWaves * q;
-            if (i < nb) {
-                lkey[i * 64 + lane] = ev[q];
-                lzone[i * 64 + lane] = zv[q];
-                if (lane == 0) { lpod[i] = sv[q]; lpod[64 + i] = fv[q]; }
-            }
-        }
-    }
-    __syncthreads();
-    if (wv != 0) return;
-    CLAIM_STAMP(0);  // the claim walk and the apply step are one wave's work
-    int32_t my_node = -2;  // lane i: batch pod i's outcome (-2 carried, -1 unschedulable)
-    uint64_t my_key = 0;
-    uint32_t npend = 0;
-    // lane i holds batch pod i's stream position and flags (read with readlane in the walk)
-    const uint32_t my_s = (uint32_t)lane < nb ? lpod[lane] : 0u;
-    const uint32_t my_flags = (uint32_t)lane < nb ? lpod[64 + lane] : 0u;
-    CLAIM_STAMP(1);
-    // Software-pipelined walk.  Entering iteration i: pod i's entries (e, z) and its exact
-    // availability mask am (claims of pods < i), pod i+1's entries (e1, z1).  Pod i+1's bitmap
-    // words are read before pod i's claim is written (they see the claims of pods < i) and then
-    // patched with pod i's claim (node w; (app, zone) when both are zone-anti-affinity pods), so
-    // the LDS round trip overlaps pod i's scalar chain instead of following it.
-    auto lane_node = [](uint64_t v, bool ok) { return (ok && v) ? key_node(v) : 0u; };
-    uint64_t e = lkey[lane];
-    uint32_t z = lzone[lane] & (kMaxZones - 1);
-    uint32_t fl = (uint32_t)__builtin_amdgcn_readlane((int)my_flags, 0);
-    uint64_t am;
-    {
-        const uint32_t node = lane_node(e, true), azb = pod_app(fl) * kMaxZones + z;
-        const uint32_t taken = ((claimed[node >> 5] >> (node & 31)) |
-                                (pod_aa(fl) == 2u ? claimed_az[azb >> 5] >> (azb & 31) : 0u)) & 1u;
-        am = __ballot(e != 0ull && taken == 0u);
-    }
-    uint64_t e1 = lkey[min(1u, 63u) * 64 + lane];
-    uint32_t z1 = lzone[min(1u, 63u) * 64 + lane] & (kMaxZones - 1);
-    for (uint32_t i = 0; i < nb; ++i) {
-        const uint32_t aa = pod_aa(fl), app = pod_app(fl);
-        const bool has1 = i + 1 < nb;
-        const uint32_t fl1 = (uint32_t)__builtin_amdgcn_readlane((int)my_flags, (int)min(i + 1, 63u));
-        const uint32_t aa1 = pod_aa(fl1), app1 = pod_app(fl1);
-        // pod i+1: bitmap words (claims of pods < i) and pod i+2's entries, all in flight now
-        const uint32_t node1 = lane_node(e1, has1), azb1 = app1 * kMaxZones + z1;
-        const uint32_t cw1 = claimed[node1 >> 5], aw1 = claimed_az[azb1 >> 5];
-        const uint32_t j2 = min(i + 2, 63u);
-        const uint64_t e2 = lkey[j2 * 64 + lane];
-        const uint32_t z2 = lzone[j2 * 64 + lane] & (kMaxZones - 1);
-        // pod i
-        uint32_t w = 0xFFFFFFFFu, zw = 0xFFFFFFFFu;
-        if (am) {
-            const int src = __builtin_ctzll(am);
-            const uint64_t best = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(e >> 32), src) << 32) |
-                                  (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)e, src);
-            w = key_node(best);
-            zw = (uint32_t)__builtin_amdgcn_readlane((int)z, src);
-            const uint32_t b2 = app * kMaxZones + zw;
-            if (lane == 0) {
-                __hip_atomic_fetch_or(&claimed[w >> 5], 1u << (w & 31), __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (aa == 2u)
-                    __hip_atomic_fetch_or(&claimed_az[b2 >> 5], 1u << (b2 & 31), __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-            if ((uint32_t)lane == i) { my_node = (int32_t)w; my_key = best; }
-        } else if (__ballot(e != 0ull)) {
-            if (lane == 0) pend[npend] = (uint32_t)__builtin_amdgcn_readlane((int)my_s, (int)i);
-            ++npend;  // every candidate taken by an earlier pod: carried to the next batch
-        } else if ((uint32_t)lane == i) {
-            my_node = -1;  // no feasible node at all (spec S7: unschedulable)
-        }
-        // pod i+1's exact mask: bitmap words patched with pod i's claim
-        const bool az_hit = aa1 == 2u && aa == 2u && app1 == app && z1 == zw;
-        const uint32_t taken1 = ((cw1 >> (node1 & 31)) | (aa1 == 2u ? aw1 >> (azb1 & 31) : 0u)) & 1u;
-        am = __ballot(has1 && e1 != 0ull && taken1 == 0u && node1 != w && !az_hit);
-        e = e1;
-        z = z1;
-        fl = fl1;
-        e1 = e2;
-        z1 = z2;
-    }
-    CLAIM_STAMP(2);
-    // apply every claim (distinct nodes; counts of one (app, zone) may be shared: atomics)
-    if ((uint32_t)lane < nb && my_node != -2) {
-        const uint32_t s = my_s;
-        if (my_node >= 0) {
-            const DPod p = pods[s];
-            const uint32_t w = (uint32_t)my_node;
-            Row r = load_row(t, w);
-            RowX x = load_rowx<kFeatExt>(t, w);
-            reserve(r, x, p, +1);
-            store_dyn(t, w, r);
-            store_dynx<kFeatExt>(t, w, x);
-            if (t.apps) {
-                const uint32_t app = pod_app(p.flags);
-                atomicOr(&t.apps[(size_t)(app >> 5) * t.cap + w], 1u << (app & 31));
-                atomicAdd(&t.zcount[app * kMaxZones + (uint32_t)t.zone[w]], 1);
-            }
-        }
-        out_node[s] = my_node;
-        if (out_key) out_key[s] = my_key;
-    }
-    // next batch: carried pods first (queue order), then fresh pods from the stream.  bidx is
-    // rewritten only after every lane has read its entry above (single wave, program order).
-    const uint32_t take = min(B - npend, P - cursor);
-    if ((uint32_t)lane < npend) bidx[lane] = pend[lane];
-    else if ((uint32_t)lane < npend + take) bidx[lane] = cursor + (uint32_t)lane - npend;
-    if (lane == 0) { ctrl[0] = npend + take; ctrl[1] = cursor + take; }
-    CLAIM_STAMP(3);
-#ifdef QS_CLAIM_DIAG
-    if (lane == 0) {
-        for (int q = 0; q < 4; ++q) atomicAdd((unsigned long long *)&g_claim_diag[q], (unsigned long long)cds[q]);
-        const unsigned long long nbt = atomicAdd((unsigned long long *)&g_claim_diag[4], 1ull);
-        if (npend + take == 0)
-            printf("claim diag: batches %llu  stage %llu  setup %llu  walk %llu  apply %llu (clocks, totals)\n",
-                   nbt + 1, (unsigned long long)g_claim_diag[0], (unsigned long long)g_claim_diag[1],
-                   (unsigned long long)g_claim_diag[2], (unsigned long long)g_claim_diag[3]);
-    }
-#endif
 }
 
 hipError_t launch_batch_init(uint32_t *ctrl, uint32_t *bidx, uint32_t P, uint32_t B, hipStream_t stream) {
@@ -1671,25 +27,22 @@ hipError_t launch_batch_init(uint32_t *ctrl, uint32_t *bidx, uint32_t P, uint32_
     return hipGetLastError();
 }
 
-// Raises the claim kernel's dynamic-LDS limit to the CU's 160 KB; called once, outside capture.
 hipError_t batch_claim_prepare() {
-    static const hipError_t attr = hipFuncSetAttribute((const void *)k_batch_claim,
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    return attr;
+    QS_RET(batch_claim_prepare_f<kFeatExt>());
+    return wide_batch_claim_prepare();
 }
 
 size_t batch_claim_lds(uint32_t n) {
     return ((((size_t)n + 31) / 32 + 3) & ~(size_t)3) * 4 + kMaxApps * kMaxZones / 8 + 64 * 4 + 64 * 64 * (8 + 4) + 128 * 4;
 }
 
-hipError_t launch_batch_claim(const DevTable &t, const DPod *pods, const uint64_t *lists, uint32_t *ctrl,
+hipError_t launch_batch_claim(const DevTable &t, const void *pods, const uint64_t *lists, uint32_t *ctrl,
                               uint32_t *bidx, uint32_t P, uint32_t B, int32_t *on, uint64_t *ok,
                               hipStream_t stream) {
     const size_t lds = batch_claim_lds(t.n);
     if (lds > 160 * 1024) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_batch_claim, dim3(1), dim3(64 * kClaimWaves), lds, stream, t, pods, lists, 64u, ctrl, bidx, P, B,
-                       on, ok);
-    return hipGetLastError();
+    if (t.wrows) return wide_batch_claim(t, pods, lists, ctrl, bidx, P, B, on, ok, lds, stream);
+    return batch_claim_f<kFeatExt>(t, pods, lists, ctrl, bidx, P, B, on, ok, lds, stream);
 }
 
 // =============================================================================================
@@ -1697,72 +50,40 @@ hipError_t launch_batch_claim(const DevTable &t, const DPod *pods, const uint64_
 // =============================================================================================
 __global__ void k_set_row(DevTable t, uint32_t i, HostRow v, uint32_t feat) {
     (void)feat;
+    t.masks[i] = DMask{v.th, v.ts, v.lb0, v.lb1};
+    if (t.zone) t.zone[i] = v.zone;
+    if (t.wrows) {  // wide layout: memory columns in f64 bytes
+        DRowW w;
+        w.ac = v.ac; w.rc = v.rc; w.zc = v.zc; w.np = v.np;
+        w.am = v.wam; w.rm = v.wrm; w.zm = v.wzm; w.ym = v.ym;
+        w.yc = v.yc; w.mp = v.mp; w.pad = 0;
+        w.ae0 = v.ae0; w.re0 = v.re0; w.ae1 = v.ae1; w.re1 = v.re1;
+        t.wrows[i] = w;
+        return;
+    }
     DRow r;
     r.ac = v.ac; r.am = v.am; r.rc = v.rc; r.rm = v.rm; r.zc = v.zc; r.zm = v.zm;
     r.np = v.np; r.mp = v.mp; r.yc = v.yc; r.ym = v.ym;
     r.ae0 = v.ae0; r.re0 = v.re0; r.ae1 = v.ae1; r.re1 = v.re1;
     t.rows[i] = r;
-    t.masks[i] = DMask{v.th, v.ts, v.lb0, v.lb1};
     if (t.soa.c[0]) {
         const int32_t f[kSCols] = {v.ac, v.am, v.rc, v.rm, v.zc, v.zm, v.np, v.mp, v.ae0, v.re0, v.ae1, v.re1};
 #pragma unroll
         for (int k = 0; k < kSCols; ++k) t.soa.c[k][i] = f[k];
     }
-    if (t.zone) t.zone[i] = v.zone;
 }
 
 // =============================================================================================
-// launchers
+// dispatchers (qs_launch.hpp)
 // =============================================================================================
-#define QS_RET(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return e_; } while (0)
-
-template <int NPT, int BS, uint32_t F>
-static hipError_t persistent_t(const DevTable &t, const DPod *pods, const DPodX *podx, uint32_t P,
-                               const DevCfg &c, int32_t *on, uint64_t *ok, uint64_t *st,
-                               hipStream_t stream) {
-    hipLaunchKernelGGL((k_persistent<NPT, BS, F>), dim3(1), dim3(BS), 0, stream, t, pods, podx, P,
-                       c, on, ok, st);
-    return hipGetLastError();
-}
-
-// Largest node count per feature set for the register-resident rows (1024 threads, 4 waves/SIMD;
-// the largest NPT of each set spills a few dwords to scratch: correct, slower — the LOOKAHEAD
-// engine is the fast path at these sizes).
-template <uint32_t F>
-static constexpr uint32_t persistent_cap() {
-    return F == 0 ? 6144u : (F == kFeatExt ? 5120u : 2048u);
-}
-
-template <uint32_t F>
-static hipError_t persistent_f(const DevTable &t, const DPod *pods, const DPodX *podx, uint32_t P,
-                               const DevCfg &c, int32_t *on, uint64_t *ok, uint64_t *st,
-                               hipStream_t stream) {
-    const uint32_t n = t.n;
-    if (n > persistent_cap<F>()) return hipErrorInvalidValue;
-    if (n <= 64) return persistent_t<1, 64, F>(t, pods, podx, P, c, on, ok, st, stream);
-    if (n <= 128) return persistent_t<1, 128, F>(t, pods, podx, P, c, on, ok, st, stream);
-    if (n <= 256) return persistent_t<1, 256, F>(t, pods, podx, P, c, on, ok, st, stream);
-    if (n <= 512) return persistent_t<1, 512, F>(t, pods, podx, P, c, on, ok, st, stream);
-    if (n <= 1024) return persistent_t<1, 1024, F>(t, pods, podx, P, c, on, ok, st, stream);
-    if (n <= 2048) return persistent_t<2, 1024, F>(t, pods, podx, P, c, on, ok, st, stream);
-    if constexpr (persistent_cap<F>() > 2048) {
-        if (n <= 3072) return persistent_t<3, 1024, F>(t, pods, podx, P, c, on, ok, st, stream);
-        if (n <= 4096) return persistent_t<4, 1024, F>(t, pods, podx, P, c, on, ok, st, stream);
-        if (n <= 5120) return persistent_t<5, 1024, F>(t, pods, podx, P, c, on, ok, st, stream);
-    }
-    if constexpr (persistent_cap<F>() > 5120) {
-        if (n <= 6144) return persistent_t<6, 1024, F>(t, pods, podx, P, c, on, ok, st, stream);
-    }
-    return hipErrorInvalidValue;
-}
-
 static uint32_t feat_class(uint32_t feat) {
     return feat == 0 ? 0u : (feat == kFeatExt ? kFeatExt : (kFeatExt | kFeatTaint | kFeatAffinity));
 }
 
-hipError_t launch_persistent(const DevTable &t, const DPod *pods, const DPodX *podx, uint32_t P,
+hipError_t launch_persistent(const DevTable &t, const void *pods, const DPodX *podx, uint32_t P,
                              const DevCfg &c, int32_t *on, uint64_t *ok, uint64_t *st,
                              hipStream_t stream) {
+    if (t.wrows) return wide_persistent(t, pods, podx, P, c, on, ok, st, stream);
     switch (feat_class(c.feat)) {
         case 0: return persistent_f<0>(t, pods, podx, P, c, on, ok, st, stream);
         case kFeatExt: return persistent_f<kFeatExt>(t, pods, podx, P, c, on, ok, st, stream);
@@ -1773,6 +94,7 @@ hipError_t launch_persistent(const DevTable &t, const DPod *pods, const DPodX *p
 }
 
 uint32_t persistent_max_nodes(uint32_t feat) {
+    if (feat & kFeatWide) return wide_persistent_max_nodes(feat);
     switch (feat_class(feat)) {
         case 0: return persistent_cap<0>();
         case kFeatExt: return persistent_cap<kFeatExt>();
@@ -1780,58 +102,17 @@ uint32_t persistent_max_nodes(uint32_t feat) {
     }
 }
 
-template <uint32_t F>
-static hipError_t scan_pod_f(const DevTable &t, const DPod *pods, const DPodX *podx, uint32_t s,
-                             const DevCfg &c, void *scratch, int32_t *on, uint64_t *ok,
-                             uint64_t *st, uint8_t *feas, int32_t *score, int32_t *total,
-                             int part, hipStream_t stream) {
-    ScanScratch *sc = (ScanScratch *)scratch;
-    const bool soa = !(F & kFeatNorm) && t.soa.c[0];
-    // one partial key per block; a grid of <= 2048 blocks (8 four-wave blocks per CU) strides
-    const uint32_t units = soa ? (t.n + 3) / 4 : t.n;
-    uint32_t blocks = min(kScanBlocksMax, max(1u, (units + 255) / 256));
-    if (soa) {
-        // SoA scan: exactly one resident wave of blocks (CUs x blocks per CU at this kernel's
-        // occupancy), so no CU runs a second, partial round of blocks at the end of the scan
-        static const uint32_t resident = [] {
-            int dev = 0, cus = 0, per = 0;
-            if (hipGetDevice(&dev) != hipSuccess ||
-                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)k_scan_soa<F>, 256, 0) != hipSuccess)
-                return kScanBlocksMax;
-            const char *env = getenv("QS_SCAN_BLOCKS");
-            if (env && atoi(env) > 0) return (uint32_t)atoi(env);
-            return (uint32_t)std::max(1, std::min((int)kScanBlocksMax, cus * per));
-        }();
-        blocks = min(blocks, min(kScanBlocksMax, resident));
-    }
-    if (part & 1) {
-        if (soa) {
-            hipLaunchKernelGGL((k_scan_soa<F>), dim3(blocks), dim3(256), 0, stream, t, pods, s, c, sc,
-                               feas, score, total);
-        } else {
-            if (F & kFeatNorm)
-                hipLaunchKernelGGL((k_scan_norm<F>), dim3(blocks), dim3(256), 0, stream, t, pods, podx, s, sc);
-            hipLaunchKernelGGL((k_scan_key<F>), dim3(blocks), dim3(256), 0, stream, t, pods, podx, s, c, sc,
-                               feas, score, total);
-        }
-    }
-    if (part & 2)
-        hipLaunchKernelGGL((k_scan_commit<F>), dim3(1), dim3(256), 0, stream, t, pods, s, blocks, sc,
-                           on, ok, st);
-    return hipGetLastError();
-}
-
 hipError_t launch_rows_to_soa(const DevTable &t, hipStream_t stream) {
-    if (!t.soa.c[0] || t.n == 0) return hipSuccess;
+    if (!t.soa.c[0] || t.n == 0 || !t.rows) return hipSuccess;
     hipLaunchKernelGGL(k_rows_to_soa, dim3((t.n + 255) / 256), dim3(256), 0, stream, t);
     return hipGetLastError();
 }
 
-hipError_t launch_scan_pod(const DevTable &t, const DPod *pods, const DPodX *podx, uint32_t s,
+hipError_t launch_scan_pod(const DevTable &t, const void *pods, const DPodX *podx, uint32_t s,
                            const DevCfg &c, void *scratch, int32_t *on, uint64_t *ok, uint64_t *st,
                            uint8_t *feas, int32_t *score, int32_t *total, int part,
                            hipStream_t stream) {
+    if (t.wrows) return wide_scan_pod(t, pods, podx, s, c, scratch, on, ok, st, feas, score, total, part, stream);
     switch (feat_class(c.feat)) {
         case 0: return scan_pod_f<0>(t, pods, podx, s, c, scratch, on, ok, st, feas, score, total, part, stream);
         case kFeatExt: return scan_pod_f<kFeatExt>(t, pods, podx, s, c, scratch, on, ok, st, feas, score, total, part, stream);
@@ -1842,109 +123,15 @@ hipError_t launch_scan_pod(const DevTable &t, const DPod *pods, const DPodX *pod
 
 size_t scan_scratch_bytes() { return sizeof(ScanScratch); }
 
-template <uint32_t F>
-static hipError_t la_window_f(const DevTable &t, const DPod *pods, const DPodX *podx, uint32_t s0,
-                              uint32_t P, const DevCfg &c, const LaGeom &geo, const LaBufs &bf,
-                              int32_t *on, uint64_t *ok, uint64_t *st, uint64_t *diag,
-                              hipStream_t stream, int part) {
-    const uint32_t K = geo.K, G = geo.G, L = geo.L, GLp = geo.eplr * 64;
-    const uint32_t kw = min(K, P - s0);
-    LaShard sh{geo.W, geo.v0, kw, 0u, (uint64_t)K * GLp};
-    const dim3 grid(geo.nv * kw * G);
-    if ((part & 4) && (F & kFeatNorm)) {
-        switch (geo.E) {
-#define QS_NRM(EE) case EE: hipLaunchKernelGGL((k_la_norm<256, EE, F>), grid, dim3(256), 0, stream, t, pods, podx, s0, P, sh, G, K, geo.chunk, bf.npart); break;
-            QS_NRM(1) QS_NRM(2) QS_NRM(3) QS_NRM(4) QS_NRM(5) QS_NRM(6) QS_NRM(8) QS_NRM(10) QS_NRM(12) QS_NRM(16)
-#undef QS_NRM
-            default: return hipErrorInvalidValue;
-        }
-        QS_RET(hipGetLastError());
-    }
-    if (part & 1) {
-        switch (geo.E) {
-#define QS_SEL(EE) case EE: hipLaunchKernelGGL((k_la_select<256, EE, F>), grid, dim3(256), 0, stream, t, pods, podx, c, s0, P, sh, G, L, geo.chunk, GLp, bf.lists, bf.clists, bf.npart, K, bf.norm, bf.pidx, bf.pcount); break;
-            QS_SEL(1) QS_SEL(2) QS_SEL(3) QS_SEL(4) QS_SEL(5) QS_SEL(6) QS_SEL(8) QS_SEL(10) QS_SEL(12) QS_SEL(16)
-#undef QS_SEL
-            default: return hipErrorInvalidValue;
-        }
-        QS_RET(hipGetLastError());
-        if (G > 1) {
-            const uint32_t M = G * L, e2 = (M + 255) / 256;
-            const dim3 mgrid(geo.nv * kw);
-            switch (e2) {
-#define QS_MRG(EE) case EE: hipLaunchKernelGGL((k_la_merge<EE>), mgrid, dim3(256), 0, stream, bf.clists, M, L, sh, GLp, bf.lists); break;
-                QS_MRG(1) QS_MRG(2) QS_MRG(3) QS_MRG(4) QS_MRG(5) QS_MRG(6) QS_MRG(7) QS_MRG(8)
-#undef QS_MRG
-                default: return hipErrorInvalidValue;
-            }
-            QS_RET(hipGetLastError());
-        }
-    }
-    if (part & 2) {
-        const size_t bm = (((t.n + 31) / 32 + 3) & ~3u) * 4;
-        if constexpr ((F & kFeatNorm) != 0) {
-            const size_t ldsn = bm + 64 * (sizeof(Row) + sizeof(RowX)) + sizeof(Row) + sizeof(RowX) + 64 * 4;
-            if (geo.waves == 4) {
-                // four-wave resolver with the maxima test; on a lost maximum it stops and the
-                // single-wave kernel resumes the window from that pod (rescan included)
-                if (geo.epl != 1 || !bf.rec) return hipErrorInvalidValue;
-                const size_t lds4n = bm + 5 * 2 * 64 * 8 + 2 * 64 * (sizeof(Row) + sizeof(int4)) + 2 * sizeof(ResPub) +
-                                     64 * 4 + 64 * sizeof(DPod) + 64 * sizeof(DPodX) + 64 * sizeof(NormInfo) +
-                                     64 * sizeof(double2) + 2 * 64 * 4 + 2 * 64 * sizeof(RowX);
-                if (diag)
-                    hipLaunchKernelGGL((k_la_resolve4<F, 1, true, false>), dim3(1), dim3(256), lds4n, stream, t, pods, c, s0, P,
-                                       K, GLp, geo.lr, sh, bf.lists, on, ok, st, diag, bf.dprev, bf.dcur, podx, bf.norm, bf.rec);
-                else if (geo.k32)
-                    hipLaunchKernelGGL((k_la_resolve4<F, 1, false, true>), dim3(1), dim3(256), lds4n, stream, t, pods, c, s0, P,
-                                       K, GLp, geo.lr, sh, bf.lists, on, ok, st, diag, bf.dprev, bf.dcur, podx, bf.norm, bf.rec);
-                else
-                    hipLaunchKernelGGL((k_la_resolve4<F, 1, false, false>), dim3(1), dim3(256), lds4n, stream, t, pods, c, s0, P,
-                                       K, GLp, geo.lr, sh, bf.lists, on, ok, st, diag, bf.dprev, bf.dcur, podx, bf.norm, bf.rec);
-                QS_RET(hipGetLastError());
-                hipLaunchKernelGGL((k_la_resolve_norm<F, 1>), dim3(1), dim3(64 * kResNormWaves), ldsn, stream, t, pods, podx, c, s0, P, K, GLp,
-                                   geo.lr, sh, bf.lists, bf.norm, on, ok, st, bf.dprev, bf.dcur, bf.nfall, bf.rec);
-                return hipGetLastError();
-            }
-            switch (geo.epl) {
-#define QS_RESN(EP) case EP: hipLaunchKernelGGL((k_la_resolve_norm<F, EP>), dim3(1), dim3(64 * kResNormWaves), ldsn, stream, t, pods, podx, c, s0, P, K, GLp, geo.lr, sh, bf.lists, bf.norm, on, ok, st, bf.dprev, bf.dcur, bf.nfall, nullptr); break;
-                QS_RESN(1) QS_RESN(2) QS_RESN(4) QS_RESN(8) QS_RESN(16)
-#undef QS_RESN
-                default: return hipErrorInvalidValue;
-            }
-            return hipGetLastError();
-        }
-        const uint64_t *lists = bf.lists;
-        const uint32_t *dprev = bf.dprev;
-        uint32_t *dcur = bf.dcur;
-        const size_t lds = bm + sizeof(Row) + sizeof(RowX);
-        const size_t lds4 = bm + 5 * 2 * 64 * 8 + 2 * 64 * (sizeof(Row) + sizeof(int4)) + 2 * sizeof(ResPub) + 64 * 4 + 64 * sizeof(DPod);
-        switch (geo.epl) {
-#define QS_RES(EP) case EP: \
-            if (geo.waves == 1) { \
-                if (diag) hipLaunchKernelGGL((k_la_resolve<F, EP, true>), dim3(1), dim3(64), lds, stream, t, pods, c, s0, P, K, GLp, geo.lr, sh, lists, on, ok, st, diag); \
-                else hipLaunchKernelGGL((k_la_resolve<F, EP, false>), dim3(1), dim3(64), lds, stream, t, pods, c, s0, P, K, GLp, geo.lr, sh, lists, on, ok, st, diag); \
-            } else { \
-                if (diag) hipLaunchKernelGGL((k_la_resolve4<F, EP, true, false>), dim3(1), dim3(256), lds4, stream, t, pods, c, s0, P, K, GLp, geo.lr, sh, lists, on, ok, st, diag, dprev, dcur, nullptr, nullptr, nullptr); \
-                else if (geo.k32) hipLaunchKernelGGL((k_la_resolve4<F, EP, false, true>), dim3(1), dim3(256), lds4, stream, t, pods, c, s0, P, K, GLp, geo.lr, sh, lists, on, ok, st, diag, dprev, dcur, nullptr, nullptr, nullptr); \
-                else hipLaunchKernelGGL((k_la_resolve4<F, EP, false, false>), dim3(1), dim3(256), lds4, stream, t, pods, c, s0, P, K, GLp, geo.lr, sh, lists, on, ok, st, diag, dprev, dcur, nullptr, nullptr, nullptr); \
-            } break;
-            QS_RES(1) QS_RES(2) QS_RES(4) QS_RES(8) QS_RES(16)
-#undef QS_RES
-            default: return hipErrorInvalidValue;
-        }
-    }
-    return hipGetLastError();
-}
-
-hipError_t launch_la_window(const DevTable &t, const DPod *pods, const DPodX *podx, uint32_t s0,
+hipError_t launch_la_window(const DevTable &t, const void *pods, const DPodX *podx, uint32_t s0,
                             uint32_t P, const DevCfg &c, const LaGeom &geo, const LaBufs &bf,
                             int32_t *on, uint64_t *ok, uint64_t *st, uint64_t *diag,
                             hipStream_t stream, int part) {
     if (bf.dprev && geo.waves == 1 && !(c.feat & kFeatNorm)) return hipErrorInvalidValue;
-    if (c.feat & kFeatNorm) {
-        if (diag && geo.waves != 4) return hipErrorInvalidValue;
+    if ((c.feat & kFeatNorm) && diag && geo.waves != 4) return hipErrorInvalidValue;
+    if (t.wrows) return wide_la_window(t, pods, podx, s0, P, c, geo, bf, on, ok, st, diag, stream, part);
+    if (c.feat & kFeatNorm)
         return la_window_f<kFeatExt | kFeatTaint | kFeatAffinity>(t, pods, podx, s0, P, c, geo, bf, on, ok, st, diag, stream, part);
-    }
     if (c.feat & kFeatExt) return la_window_f<kFeatExt>(t, pods, podx, s0, P, c, geo, bf, on, ok, st, diag, stream, part);
     return la_window_f<0>(t, pods, podx, s0, P, c, geo, bf, on, ok, st, diag, stream, part);
 }

@@ -1,0 +1,51 @@
+// qs_kernels_wide.hip — the wide-layout translation unit: instantiations of the
+// kernels of qs_kernels.hpp for tables whose memory quantities need f64 byte columns (odd-Ki
+// allocatable, decimal requests — anything the compact 2^u-byte int32 layout cannot hold below
+// 2^24).  Two feature classes: Fit + Balanced (+ extended resources), and the normalizing profile
+// (TaintToleration / NodeAffinity); extended-resource columns are always on (a zero request skips
+// them, spec S4).
+#include "qs_kernels.hpp"
+
+namespace qs {
+
+namespace {
+constexpr uint32_t kWideFit = kFeatWide | kFeatExt;
+constexpr uint32_t kWideNorm = kFeatWide | kFeatExt | kFeatTaint | kFeatAffinity;
+}  // namespace
+
+hipError_t wide_persistent(const DevTable &t, const void *pods, const DPodX *podx, uint32_t P,
+                           const DevCfg &c, int32_t *on, uint64_t *ok, uint64_t *st, hipStream_t stream) {
+    if (c.feat & kFeatNorm) return persistent_f<kWideNorm>(t, pods, podx, P, c, on, ok, st, stream);
+    return persistent_f<kWideFit>(t, pods, podx, P, c, on, ok, st, stream);
+}
+
+uint32_t wide_persistent_max_nodes(uint32_t feat) {
+    return (feat & kFeatNorm) ? persistent_cap<kWideNorm>() : persistent_cap<kWideFit>();
+}
+
+hipError_t wide_scan_pod(const DevTable &t, const void *pods, const DPodX *podx, uint32_t s,
+                         const DevCfg &c, void *scratch, int32_t *on, uint64_t *ok, uint64_t *st,
+                         uint8_t *feas, int32_t *score, int32_t *total, int part, hipStream_t stream) {
+    if (c.feat & kFeatNorm)
+        return scan_pod_f<kWideNorm>(t, pods, podx, s, c, scratch, on, ok, st, feas, score, total, part, stream);
+    return scan_pod_f<kWideFit>(t, pods, podx, s, c, scratch, on, ok, st, feas, score, total, part, stream);
+}
+
+hipError_t wide_la_window(const DevTable &t, const void *pods, const DPodX *podx, uint32_t s0,
+                          uint32_t P, const DevCfg &c, const LaGeom &geo, const LaBufs &bf,
+                          int32_t *on, uint64_t *ok, uint64_t *st, uint64_t *diag,
+                          hipStream_t stream, int part) {
+    if (c.feat & kFeatNorm)
+        return la_window_f<kWideNorm>(t, pods, podx, s0, P, c, geo, bf, on, ok, st, diag, stream, part);
+    return la_window_f<kWideFit>(t, pods, podx, s0, P, c, geo, bf, on, ok, st, diag, stream, part);
+}
+
+hipError_t wide_batch_claim_prepare() { return batch_claim_prepare_f<kWideFit>(); }
+
+hipError_t wide_batch_claim(const DevTable &t, const void *pods, const uint64_t *lists, uint32_t *ctrl,
+                            uint32_t *bidx, uint32_t P, uint32_t B, int32_t *on, uint64_t *ok,
+                            size_t lds, hipStream_t stream) {
+    return batch_claim_f<kWideFit>(t, pods, lists, ctrl, bidx, P, B, on, ok, lds, stream);
+}
+
+}  // namespace qs

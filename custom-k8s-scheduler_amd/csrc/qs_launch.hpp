@@ -8,16 +8,17 @@ namespace qs {
 
 struct DevTable;
 struct DevCfg;
-struct DPod;
-struct DPodX;
+struct DPodX;  // pod records are DPod (compact layout) or DPodW (wide layout): passed as void*
 
-// One compacted node row, passed by value to k_set_row.
+// One node row for k_set_row (by value).  Compact layout: the int32 fields; wide layout
+// (DevTable::wrows): wam / wrm / wzm carry memory in f64 bytes and am / rm / zm are unused.
 struct HostRow {
     int32_t ac, am, rc, rm, zc, zm, np, mp;
     double yc, ym;
     int32_t ae0, re0, ae1, re1;
     uint64_t th, ts, lb0, lb1;
     int32_t zone, pad;
+    double wam, wrm, wzm;
 };
 
 // Lookahead geometry: window K pods, list length L (= K), G node chunks of `chunk` nodes per pod,
@@ -39,12 +40,12 @@ struct LaShard {
     uint64_t RS;
 };
 
-hipError_t launch_persistent(const DevTable &t, const DPod *pods, const DPodX *podx, uint32_t P,
+hipError_t launch_persistent(const DevTable &t, const void *pods, const DPodX *podx, uint32_t P,
                              const DevCfg &c, int32_t *out_node, uint64_t *out_key,
                              uint64_t *stamps, hipStream_t stream);
 uint32_t persistent_max_nodes(uint32_t feat);
 
-hipError_t launch_scan_pod(const DevTable &t, const DPod *pods, const DPodX *podx, uint32_t s,
+hipError_t launch_scan_pod(const DevTable &t, const void *pods, const DPodX *podx, uint32_t s,
                            const DevCfg &c, void *scratch, int32_t *out_node, uint64_t *out_key,
                            uint64_t *stamps, uint8_t *feas, int32_t *score, int32_t *total,
                            int part, hipStream_t stream);  // part: 1 keys (+norm), 2 commit
@@ -71,7 +72,7 @@ struct LaBufs {
     // normalizing profiles, four-wave resolver: the stop record it hands to the resume kernel
     uint32_t *rec = nullptr;
 };
-hipError_t launch_la_window(const DevTable &t, const DPod *pods, const DPodX *podx, uint32_t s0,
+hipError_t launch_la_window(const DevTable &t, const void *pods, const DPodX *podx, uint32_t s0,
                             uint32_t P, const DevCfg &c, const LaGeom &geo, const LaBufs &bufs,
                             int32_t *out_node, uint64_t *out_key, uint64_t *stamps, uint64_t *diag,
                             hipStream_t stream, int part);  // part: 4 norm, 1 select(+merge), 2 resolve
@@ -82,7 +83,7 @@ hipError_t launch_la_window(const DevTable &t, const DPod *pods, const DPodX *po
 hipError_t launch_batch_init(uint32_t *ctrl, uint32_t *bidx, uint32_t P, uint32_t B, hipStream_t stream);
 size_t batch_claim_lds(uint32_t n);
 hipError_t batch_claim_prepare();  // dynamic LDS of the claim kernel (<= 160 KB)
-hipError_t launch_batch_claim(const DevTable &t, const DPod *pods, const uint64_t *lists, uint32_t *ctrl,
+hipError_t launch_batch_claim(const DevTable &t, const void *pods, const uint64_t *lists, uint32_t *ctrl,
                               uint32_t *bidx, uint32_t P, uint32_t B, int32_t *out_node,
                               uint64_t *out_key, hipStream_t stream);
 

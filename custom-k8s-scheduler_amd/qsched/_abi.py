@@ -29,6 +29,7 @@ QS_QOS_BESTEFFORT, QS_QOS_BURSTABLE, QS_QOS_GUARANTEED = 0, 1, 2
 QS_MODE_EXACT, QS_MODE_BATCHED = 0, 1
 ENGINES = {"auto": 0, "persistent": 1, "scan": 2, "lookahead": 3, "batched": 4}
 ENGINE_NAMES = {v: k for k, v in ENGINES.items()}
+LAYOUT_NAMES = {0: "compact", 1: "wide"}
 
 
 class QschedLibraryMissing(RuntimeError):
@@ -89,7 +90,9 @@ class QsStats(ctypes.Structure):
                 ("wall_s", ctypes.c_double), ("h2d_s", ctypes.c_double), ("d2h_s", ctypes.c_double),
                 ("p50_cycle_us", ctypes.c_double), ("p99_cycle_us", ctypes.c_double),
                 ("max_cycle_us", ctypes.c_double), ("engine_used", ctypes.c_int32),
-                ("reserved", ctypes.c_int32 * 7), ("kernel_s", ctypes.c_double * 4),
+                ("table_layout", ctypes.c_int32), ("resumed_windows", ctypes.c_uint64),
+                ("device_faults", ctypes.c_uint64),
+                ("reserved", ctypes.c_int32 * 2), ("kernel_s", ctypes.c_double * 4),
                 ("kernel_launches", ctypes.c_uint64 * 4)]
 
     KERNELS = ("persistent", "scan", "select", "resolve")
@@ -98,6 +101,7 @@ class QsStats(ctypes.Structure):
         d = {f: getattr(self, f) for f, _ in self._fields_
              if f not in ("reserved", "kernel_s", "kernel_launches")}
         d["engine_used"] = ENGINE_NAMES.get(self.engine_used, self.engine_used)
+        d["table_layout"] = LAYOUT_NAMES.get(self.table_layout, self.table_layout)
         d["kernels"] = {k: {"s": self.kernel_s[i], "launches": int(self.kernel_launches[i])}
                         for i, k in enumerate(self.KERNELS) if self.kernel_launches[i]}
         return d

@@ -158,7 +158,12 @@ typedef struct qs_stats {
     double h2d_s, d2h_s;            /* host<->device copies around it (qs_schedule_stream) */
     double p50_cycle_us, p99_cycle_us, max_cycle_us; /* per-pod decision interval (record_timestamps) */
     int32_t engine_used;
-    int32_t reserved[7];
+    int32_t table_layout;           /* device layout that ran: 0 compact (int32 columns, memory in
+                                       2^u-byte units < 2^24), 1 wide (f64 memory columns in bytes) */
+    uint64_t resumed_windows;       /* normalizing LOOKAHEAD: windows stopped for an exact rescan */
+    uint64_t device_faults;         /* QS_EDEVICE results of this context so far (each one drops
+                                       the device table; the next call rebuilds it from the mirror) */
+    int32_t reserved[2];
     /* per-kernel device time (config.profile_kernels = 1; HIP events on the library's stream):
      * [0] persistent, [1] scan (all per-pod kernels), [2] lookahead select, [3] lookahead resolve */
     double kernel_s[4];

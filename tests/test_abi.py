@@ -48,6 +48,20 @@ def test_no_symbols_leak_torch():
     assert all(n.startswith("qs_") for n in text_syms), text_syms
 
 
+def test_every_registered_kernel_has_device_code():
+    """Each kernel the host side registers (by mangled name) has a kernel descriptor (<name>.kd)
+    in the embedded gfx950 code object.  Guards against host/device name drift, e.g. a kernel
+    signature that mangles an unnamed type ($_N is numbered per compilation pass)."""
+    import subprocess
+    strs = set(subprocess.run(["strings", "-n", "8", _abi.LIB_PATH], capture_output=True,
+                              text=True).stdout.split())
+    kernels = {s for s in strs if re.fullmatch(r"_ZN2qs\d+k_\w+", s.replace("$", "_"))}
+    assert len(kernels) > 100
+    assert not any("$_" in k for k in kernels)
+    missing = [k for k in kernels if k + ".kd" not in strs]
+    assert not missing, missing[:3]
+
+
 def test_config_default():
     lib = qsched.load()
     c = _abi.QsConfig()

@@ -77,14 +77,23 @@ def test_config4_full_lookahead(oracle, serial):
     assert g[3]["engine_used"] == "lookahead"
 
 
+@pytest.mark.parametrize("waves", ["4", "1"])
 @pytest.mark.parametrize("K", [1, 5, 32, 64])
-def test_config4_lookahead_windows(oracle, K):
+def test_config4_lookahead_windows(oracle, K, waves, monkeypatch):
     """Tight cluster (many nodes fill up): exercises the normalize-maximum safety test and the
-    exact rescan fallback."""
+    exact rescan fallback.  The rescan path must actually run (stats.truncations), and with the
+    four-wave resolver (overlapped windows, K <= 32) so must the stop / resume hand-off
+    (stats.resumed_windows); QS_NORM_WAVES=1 pins the single-wave kernel for comparison."""
+    monkeypatch.setenv("QS_NORM_WAVES", waves)
     nodes, pods = synth_generate(4, 400, 14000)
     g = run_gpu(nodes, pods, CFG4, "lookahead", lookahead=K)
     o = run_oracle(oracle, nodes, pods, CFG4)
     assert_same(g[:2], o[:2], g[2], o[2])
+    assert g[3]["truncations"] > 0
+    if waves == "4" and K <= 32:
+        assert g[3]["resumed_windows"] > 0
+    else:
+        assert g[3]["resumed_windows"] == 0
 
 
 def test_config2_full_lookahead(oracle):

@@ -1,0 +1,183 @@
+"""The wide device layout ("compacts to the int32 layout only after verifying
+alignment and range, and otherwise uses the int64 kernel"; VERDICT r1 missing #1).
+
+Kubelet reports allocatable memory in Ki, and pods request decimal quantities ("100M" = 10^8 B =
+2^8 * 5^8).  Neither fits the compact layout (memory in 2^u-byte units below 2^24), so such tables
+run on f64 byte columns.  Every engine must load and schedule them bit-exact against
+the oracle, and the compact layout must stay the fast path when it applies.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+from qsched import Scheduler, pods_from_struct, synth_generate  # noqa: E402
+
+from oracle import oracle as O  # noqa: E402
+
+MIB, GIB, KI = 1 << 20, 1 << 30, 1 << 10
+ENGINES = ["persistent", "scan", "lookahead"]
+
+
+def ki_cluster(n, p, seed=7, features=False):
+    """Config-2/4 shaped cluster with odd-Ki node memory (64-768 GiB) and decimal pod requests."""
+    nodes, pods = synth_generate(4 if features else 2, n, p, seed=seed)
+    rng = np.random.default_rng(seed)
+    nodes["alloc_mem"][:] = (rng.integers(64 << 20, 768 << 20, n) | 1) * KI
+    op = pods_from_struct(pods)
+    dec = rng.choice([100 * 10**6, 512 * 10**6, 10**9, 3 * 10**9], p)
+    has = op["req_mem"] > 0
+    pods["req_mem"] = np.where(has, dec, 0)
+    pods["nz_mem"] = np.where(has, dec, O.DEF_MEM)
+    return nodes, pods
+
+
+def run(nodes, pods, cfg):
+    with Scheduler(cfg) as s:
+        s.load_nodes(nodes)
+        st = s.prepare(pods)
+        stats = st.run()
+        pl, keys = st.results()
+        st.free()
+        final = s.read_nodes()
+    return pl, keys, final, stats
+
+
+def oracle_run(nodes, pods, cfg=None):
+    on = {k: v.copy() for k, v in nodes.items()}
+    pl, keys, _ = O.schedule(on, pods_from_struct(pods), cfg or {}, nthreads=16)
+    return pl, keys, on
+
+
+def assert_exact(g, o):
+    pl, keys, final = g[:3]
+    bad = np.nonzero(pl != o[0])[0]
+    assert bad.size == 0, f"{bad.size} placements differ; first {bad[0]}: gpu {pl[bad[0]]} oracle {o[0][bad[0]]}"
+    assert np.array_equal(keys, o[1])
+    for k in o[2]:
+        assert np.array_equal(final[k], o[2][k]), k
+
+
+@pytest.mark.parametrize("engine", ENGINES + ["lookahead_serial", "vshards"])
+def test_odd_ki_nodes_decimal_pods_5000(engine):
+    """VERDICT r1 done-criterion: 5,000 nodes with odd-Ki memory, pods requesting 100M / 512M."""
+    nodes, pods = ki_cluster(5000, 20000)
+    cfg = {"engine": "lookahead" if engine in ("lookahead_serial", "vshards") else engine}
+    if engine == "lookahead_serial":
+        cfg["lookahead_serial"] = 1
+    if engine == "vshards":
+        cfg["virtual_shards"] = 4
+    g = run(nodes, pods, cfg)
+    assert g[3]["table_layout"] == "wide"
+    assert_exact(g, oracle_run(nodes, pods))
+
+
+@pytest.mark.parametrize("engine", ENGINES)
+def test_wide_config4_profile(engine):
+    """All four plugins + amd.com/gpu on the wide layout (normalizing LOOKAHEAD incl. stop/resume)."""
+    nodes, pods = ki_cluster(600, 12000, seed=11, features=True)
+    cfg = dict(enable_taint=1, enable_affinity=1)
+    g = run(nodes, pods, dict(cfg, engine=engine))
+    assert g[3]["table_layout"] == "wide"
+    assert_exact(g, oracle_run(nodes, pods, cfg))
+
+
+def test_wide_full_config2_shape():
+    """5,000 x 100,000 on the wide layout (the headline shape), every placement bit-exact."""
+    nodes, pods = ki_cluster(5000, 100000, seed=3)
+    g = run(nodes, pods, {})
+    assert g[3]["table_layout"] == "wide" and g[3]["engine_used"] == "lookahead"
+    assert_exact(g, oracle_run(nodes, pods))
+
+
+def test_wide_batched():
+    nodes, pods = ki_cluster(800, 10000, seed=5)
+    with Scheduler({}) as s:
+        s.load_nodes(nodes)
+        st = s.prepare(pods)
+        stats = st.run(mode="batched")
+        pl, keys = st.results()
+        st.free()
+        final = s.read_nodes()
+    assert stats["table_layout"] == "wide"
+    on = {k: v.copy() for k, v in nodes.items()}
+    opl, okeys, _ = O.schedule_batched(on, pods_from_struct(pods), nthreads=16)
+    assert np.array_equal(pl, opl) and np.array_equal(keys, okeys)
+    for k in ("req_cpu", "req_mem", "nz_cpu", "nz_mem", "pods"):
+        assert np.array_equal(final[k], on[k]), k
+
+
+def test_compact_stays_the_fast_path():
+    nodes, pods = synth_generate(2, 2000, 5000)
+    g = run(nodes, pods, {})
+    assert g[3]["table_layout"] == "compact"
+    assert_exact(g, oracle_run(nodes, pods))
+
+
+def test_compact_table_goes_wide_for_a_decimal_stream():
+    """A MiB-aligned table stays compact until a stream brings 100M requests; the second stream
+    runs on the wide layout and continues from the first stream's placements exactly."""
+    nodes, pods = synth_generate(2, 1500, 8000)
+    op = pods_from_struct(pods)
+    with Scheduler({}) as s:
+        s.load_nodes(nodes)
+        st = s.prepare(pods[:4000])
+        st1 = st.run()
+        pl1, k1 = st.results()
+        st.free()
+        p2 = pods[4000:].copy()
+        has = p2["req_mem"] > 0
+        p2["req_mem"] = np.where(has, 100 * 10**6, 0)
+        p2["nz_mem"] = np.where(has, 100 * 10**6, O.DEF_MEM)
+        st = s.prepare(p2)
+        st2 = st.run()
+        pl2, k2 = st.results()
+        st.free()
+        final = s.read_nodes()
+    assert st1["table_layout"] == "compact" and st2["table_layout"] == "wide"
+    on = {k: v.copy() for k, v in nodes.items()}
+    o1, ok1, _ = O.schedule(on, {k: v[:4000] for k, v in op.items()}, nthreads=16)
+    o2, ok2, _ = O.schedule(on, pods_from_struct(p2), nthreads=16)
+    assert np.array_equal(pl1, o1) and np.array_equal(k1, ok1)
+    assert np.array_equal(pl2, o2) and np.array_equal(k2, ok2)
+    for k in on:
+        assert np.array_equal(final[k], on[k]), k
+
+
+@pytest.mark.parametrize("layout", ["rows", "soa"])
+def test_wide_score_pod_reserve(layout):
+    """qs_score_pod / qs_reserve / qs_unreserve on the wide layout (framework path)."""
+    nodes, pods = ki_cluster(700, 12, seed=9)
+    cfg = {"scan_soa_min_nodes": 1 if layout == "soa" else -1}
+    op = pods_from_struct(pods)
+    ref = {k: v.copy() for k, v in nodes.items()}
+    wins = []
+    with Scheduler(cfg) as s:
+        s.load_nodes(nodes)
+        for j in range(12):
+            got = s.score_pod(pods[j])
+            keys, sc = O.score_pod(ref, op, j)
+            feas = keys != 0
+            assert np.array_equal(got["feasible"], feas)
+            assert np.array_equal(got["total"], np.where(feas, (keys >> np.uint64(32)).astype(np.int64) - 1, -1))
+            np.testing.assert_array_equal(got["scores"][feas], sc[feas])
+            best = got["best"]
+            wins.append(best)
+            s.reserve(best, pods[j])
+            O.lib().or_reserve(O.ctypes.byref(O._mk_nodes(ref)), O.ctypes.byref(O._mk_pods(op)), j, best, 1)
+        final = s.read_nodes()
+        for k in ref:
+            assert np.array_equal(final[k], ref[k]), k
+        for j in reversed(range(12)):  # Unreserve rolls every Reserve back exactly
+            s.unreserve(wins[j], pods[j])
+        back = s.read_nodes()
+        for k in nodes:
+            assert np.array_equal(back[k], nodes[k]), k
+
+
+def test_memory_above_2p46_is_rejected():
+    nodes, pods = synth_generate(2, 10, 1)
+    nodes["alloc_mem"][3] = 1 << 47
+    with Scheduler({}) as s:
+        with pytest.raises(Exception, match="alloc_mem"):
+            s.load_nodes(nodes)
