@@ -13,6 +13,11 @@ Workloads (BASELINE.json configs):
 A *step* = restore the empty cluster on the device (qs_table_restore, a D2D copy) + run the whole
 exact stream (qs_stream_run): inputs resident in HBM, every pod scheduled, placements left in HBM.
 Timed: K steps bracketed by barrier + device sync on both sides; MAX over ranks.
+
+``--gpus N`` (N > 1) without a launcher environment re-launches this script under
+``torch.distributed.run`` (one rank per GPU, 127.0.0.1 rendezvous) as a child process before any
+GPU call, and exits with its status; ``--dry-run`` prints that launch plan and exits.  Under a
+launcher, WORLD_SIZE must equal --gpus.
 """
 import argparse
 import json
@@ -26,7 +31,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "custom-k8s-scheduler_amd"))
 
-import qsched  # noqa: E402
+import qsched  # noqa: E402  (ctypes binding: the library is loaded on first use, not at import)
 
 WORKLOADS = {
     # name: (generator config, nodes, pods, description)
@@ -48,7 +53,7 @@ KERNEL_NAMES = {"resolve": "k_la_resolve4", "select": "k_la_select", "persistent
                 "scan": "k_scan_key"}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -61,36 +66,67 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-config3", action="store_true", help="skip the N=1 config-3 reference point")
     ap.add_argument("--no-scan", action="store_true", help="skip the HBM-resident scan roofline leg")
-    return ap.parse_args()
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the end-to-end, framework-path and wide-layout legs")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="print the launch plan (torchrun argv for --gpus N > 1) and exit, no GPU touched")
+    return ap.parse_args(argv)
+
+
+def launch_plan(a, argv, env=None):
+    """How this invocation runs: {"mode": "torchrun", "argv": [...]} when --gpus N > 1 and no
+    launcher environment is present (re-launch as N ranks), {"mode": "in-process", ...} otherwise.
+    Raises SystemExit when a launcher's WORLD_SIZE disagrees with --gpus."""
+    env = os.environ if env is None else env
+    world = env.get("WORLD_SIZE")
+    if world is None:
+        if a.gpus > 1:
+            import socket
+            with socket.socket() as sk:  # a free local port for the rendezvous
+                sk.bind(("127.0.0.1", 0))
+                port = sk.getsockname()[1]
+            cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                   f"--nproc-per-node={a.gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+                   os.path.abspath(__file__)] + [x for x in argv if x != "--dry-run"]
+            return {"mode": "torchrun", "argv": cmd, "world": a.gpus}
+        return {"mode": "in-process", "world": 1}
+    if int(world) != a.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} from the launcher but --gpus {a.gpus}")
+    return {"mode": "in-process", "world": int(world)}
 
 
 class Ctx:
     """Process-group plumbing: rank/world from the torchrun env, RCCL id broadcast, barriers."""
 
-    def __init__(self):
+    def __init__(self, backend=None):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        # "nccl" (= RCCL) on the GPU box; "gloo" rehearses the plumbing on CPU (tests/test_bench_launch.py)
+        self.backend = backend or os.environ.get("QS_BENCH_BACKEND", "nccl")
+        self.dev = f"cuda:{self.local}" if self.backend == "nccl" else "cpu"
         self.dist = None
         if self.world > 1:
             import torch
             import torch.distributed as dist
 
-            torch.cuda.set_device(self.local)
-            dist.init_process_group("nccl", init_method="env://")
+            if self.backend == "nccl":
+                torch.cuda.set_device(self.local)
+            dist.init_process_group(self.backend, init_method="env://")
             self.dist = dist
 
     def barrier(self):
         if self.dist is not None:
             import torch
             self.dist.barrier()
-            torch.cuda.synchronize()
+            if self.backend == "nccl":
+                torch.cuda.synchronize()
 
     def max(self, v):
         if self.dist is None:
             return v
         import torch
-        t = torch.tensor([v], dtype=torch.float64, device=f"cuda:{self.local}")
+        t = torch.tensor([v], dtype=torch.float64, device=self.dev)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
@@ -98,7 +134,7 @@ class Ctx:
         """(rank, world, RCCL unique id) for qs_open_shard; the id is made on rank 0."""
         import torch
         uid = qsched.dist_unique_id() if self.rank == 0 else bytes(128)
-        t = torch.tensor(list(uid), dtype=torch.uint8, device=f"cuda:{self.local}")
+        t = torch.tensor(list(uid), dtype=torch.uint8, device=self.dev)
         self.dist.broadcast(t, 0)
         return (self.rank, self.world, bytes(t.cpu().numpy().tolist()))
 
@@ -159,6 +195,24 @@ def pmc_traffic(kernel_prefix):
     return None
 
 
+def host_info():
+    """The box the CPU arms ran on (north_star: "core count stated")."""
+    model = None
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = None
+    return {"cpu_model": model, "nproc": os.cpu_count(), "usable_cpus": usable,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+
+
 def cpu_baseline(nodes, pods, n_nodes, n_pods, sample, threads=1, gpu_placement=None):
     """Oracle (C restatement) on the same stream: 1 thread, or the node-parallel OpenMP arm
     (SURVEY §8(d) arm 2: upstream's Parallelizer runs 16 workers).  sample = 0 runs the whole
@@ -176,6 +230,7 @@ def cpu_baseline(nodes, pods, n_nodes, n_pods, sample, threads=1, gpu_placement=
     what = (f"the whole {n_pods:,}-pod stream" if whole else
             f"first {sample} of the {n_pods:,} pods (QoS-sorted within the sample)")
     out = {"value": round(sample / dt, 1), "unit": "pods/s", "cores": threads, "kind": "port",
+           "host": host_info(),
            "sample": f"{what} onto the empty {n_nodes:,}-node cluster, oracle/qs_oracle.c {how}, "
                      f"{dt:.2f} s",
            "evals_per_s": round(sample * n_nodes / dt, 1)}
@@ -193,8 +248,8 @@ def measure(cx, a, workload, steps, warmup, with_diag=True):
     cfg = dict({"engine": a.engine, "lookahead": a.lookahead}, **PROFILE.get(workload, {}))
     s = open_sched(cx, cfg, sharded)
     s.load_nodes(nodes)
+    st = s.prepare(pods)  # (may re-lay the table out for the pods' quantities: snapshot after)
     s.save_table()
-    st = s.prepare(pods)
 
     mode = MODE.get(workload, "exact")
 
@@ -217,6 +272,7 @@ def measure(cx, a, workload, steps, warmup, with_diag=True):
     ranks_work = cx.world if (cx.world > 1 and not sharded) else 1  # replicas multiply the work
     value = n_pods * steps * ranks_work / elapsed
     out = {"value": value, "ms_per_step": elapsed / steps * 1e3, "engine": last["engine_used"],
+           "table_layout": last["table_layout"],
            "unschedulable_frac": float((placement < 0).mean()), "n_nodes": n_nodes,
            "placement": placement.copy(),
            "n_pods": n_pods, "desc": desc, "sharded": sharded, "nodes": nodes, "pods": pods,
@@ -236,15 +292,22 @@ def scan_roofline(cx, a, n_nodes=1 << 24, n_pods=32):
     cfg = {"engine": "scan"}
     s = qsched.Scheduler(cfg, device=cx.local)
     s.load_nodes(nodes)
-    s.save_table()
     st = s.prepare(pods)
+    s.save_table()
     st.run()  # warm-up
     walls = []
     for _ in range(3):
         s.restore_table()
         walls.append(st.run()["wall_s"])
+    placement, _ = st.results()  # the last run started from the restored (empty) table
     st.free()
     s.close()
+    from oracle import oracle as O
+    on = {k: v.copy() for k, v in nodes.items()}
+    t0 = time.perf_counter()
+    ref, _, _ = O.schedule(on, qsched.pods_from_struct(pods), nthreads=16)
+    oracle_s = time.perf_counter() - t0
+    del on
     sp = qsched.Scheduler(dict(cfg, profile_kernels=1), device=cx.local)
     sp.load_nodes(nodes)
     stp = sp.prepare(pods)
@@ -258,6 +321,8 @@ def scan_roofline(cx, a, n_nodes=1 << 24, n_pods=32):
     return {"workload": f"SCAN engine, {n_nodes:,} nodes (config-2 distribution, SoA columns) x "
                         f"{n_pods} pods: one full scoring scan + argmax + Reserve per pod",
             "pods_per_s": round(n_pods / wall, 1), "evals_per_s": round(n_pods * n_nodes / wall, 1),
+            "placements_match": bool(np.array_equal(placement, ref)),
+            "oracle_16t_s": round(oracle_s, 2),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": pmc_traffic("k_scan_soa"), "kernel": "k_scan_soa",
@@ -265,8 +330,111 @@ def scan_roofline(cx, a, n_nodes=1 << 24, n_pods=32):
                          "bytes_per_launch": n_nodes * B_NODE}}
 
 
+def ki_decimal_cluster(n, p, seed):
+    """Config-2 shaped cluster in real-world quantities: odd-Ki node allocatable (64-768 GiB, as
+    kubelet reports it) and decimal pod requests (100M, 512M, 1G, 3G).  Needs the wide layout."""
+    nodes, pods = qsched.synth_generate(2, n, p, seed=seed)
+    rng = np.random.default_rng(seed)
+    nodes["alloc_mem"][:] = (rng.integers(64 << 20, 768 << 20, n) | 1) * 1024
+    dec = rng.choice([100 * 10**6, 512 * 10**6, 10**9, 3 * 10**9], p)
+    has = pods["req_mem"] > 0
+    pods["req_mem"] = np.where(has, dec, 0)
+    pods["nz_mem"] = np.where(has, dec, 209715200)
+    return nodes, pods
+
+
+def wide_leg(cx, a, n_nodes=5000, n_pods=100000, steps=3):
+    """Config-2 shape on the wide layout (f64 memory columns), placements diffed
+    against the 16-thread oracle."""
+    nodes, pods = ki_decimal_cluster(n_nodes, n_pods, seed=0x5EED0002)
+    s = qsched.Scheduler({"engine": a.engine, "lookahead": a.lookahead}, device=cx.local)
+    s.load_nodes(nodes)
+    st = s.prepare(pods)
+    s.save_table()
+    stats = st.run()
+    walls = []
+    for _ in range(steps):
+        s.restore_table()
+        t0 = time.perf_counter()
+        st.run()
+        walls.append(time.perf_counter() - t0)
+    placement, _ = st.results()
+    st.free()
+    s.close()
+    from oracle import oracle as O
+    on = {k: v.copy() for k, v in nodes.items()}
+    ref, _, _ = O.schedule(on, qsched.pods_from_struct(pods), nthreads=16)
+    wall = min(walls)
+    return {"workload": f"{n_nodes:,} nodes (odd-Ki allocatable 64-768 GiB) x {n_pods:,} pods "
+                        "(decimal requests 100M/512M/1G/3G): exact stream on the wide layout",
+            "table_layout": stats["table_layout"], "engine": stats["engine_used"],
+            "value": round(n_pods / wall, 1), "unit": "pods/s", "ms_per_step": round(wall * 1e3, 3),
+            "placements_match": bool(np.array_equal(placement, ref))}
+
+
+def e2e_leg(cx, nodes, pods, gpu_placement):
+    """qs_schedule_stream end to end on a freshly loaded table (SURVEY.md §8(d) GPU timing): host
+    precompute (QoSSort, compaction) + H2D of the pod records + device run (incl. building the
+    stream's HIP graph) + D2H of placements, with the phases reported separately."""
+    out = []
+    for _ in range(2):
+        s = qsched.Scheduler({}, device=cx.local)
+        s.load_nodes(nodes)
+        t0 = time.perf_counter()
+        placement, stats = s.schedule(pods, with_stats=True)
+        e2e = time.perf_counter() - t0
+        s.close()
+        out.append((e2e, stats, placement))
+    e2e, stats, placement = min(out, key=lambda x: x[0])
+    n = len(placement)
+    return {"what": "qs_schedule_stream wall on a freshly loaded table: prepare (QoSSort + compaction "
+                    "+ H2D) + run (graph build + device stream) + D2H of placements",
+            "pods_per_s": round(n / e2e, 1), "e2e_ms": round(e2e * 1e3, 3),
+            "prepare_h2d_ms": round(stats["h2d_s"] * 1e3, 3), "device_run_ms": round(stats["wall_s"] * 1e3, 3),
+            "d2h_ms": round(stats["d2h_s"] * 1e3, 3),
+            "placements_match": bool(np.array_equal(placement, gpu_placement))}
+
+
+def framework_leg(cx, n_nodes=5000, n_pods=2000):
+    """The framework-embedded path (SURVEY.md §3.4, §5 p99 definition): per pod one qs_score_pod
+    (PreFilter..NormalizeScore over all nodes, per-node feasible / plugin scores / totals copied
+    back for Filter/Score lookups) + one qs_reserve of the chosen node, host wall per pod through
+    the Python ctypes binding.  Arrival order; placements diffed against the oracle."""
+    nodes, pods = qsched.synth_generate(2, n_nodes, n_pods)
+    s = qsched.Scheduler({}, device=cx.local)
+    s.load_nodes(nodes)
+    lat = np.empty(n_pods)
+    placement = np.empty(n_pods, np.int32)
+    for j in range(n_pods):
+        t0 = time.perf_counter()
+        best = s.score_pod(pods[j])["best"]
+        if best >= 0:
+            s.reserve(best, pods[j])
+        lat[j] = time.perf_counter() - t0
+        placement[j] = best
+    s.close()
+    from oracle import oracle as O
+    on = {k: v.copy() for k, v in nodes.items()}
+    ref, _, _ = O.schedule(on, qsched.pods_from_struct(pods), {"qos_sort": 0}, nthreads=16)
+    us = lat * 1e6
+    return {"workload": f"{n_nodes:,} nodes x {n_pods:,} pods, qs_score_pod + qs_reserve per pod "
+                        "(Python ctypes caller, arrival order)",
+            "p50_us": round(float(np.percentile(us, 50)), 2), "p99_us": round(float(np.percentile(us, 99)), 2),
+            "mean_us": round(float(us.mean()), 2), "pods_per_s": round(n_pods / lat.sum(), 1),
+            "placements_match": bool(np.array_equal(placement, ref))}
+
+
 def main():
-    a = parse()
+    argv = sys.argv[1:]
+    a = parse(argv)
+    plan = launch_plan(a, argv)
+    if a.dry_run:
+        print(json.dumps(plan), flush=True)
+        return 0
+    if plan["mode"] == "torchrun":
+        # one rank per GPU; this parent never touches the GPU (no exec after GPU init)
+        import subprocess
+        return subprocess.run(plan["argv"]).returncode
     cx = Ctx()
     workload = a.workload if a.workload != "auto" else ("config2" if cx.world == 1 else "config3")
     m = measure(cx, a, workload, a.steps, a.warmup)
@@ -277,6 +445,11 @@ def main():
         c5 = measure(cx, a, "config5", 3, 1, with_diag=False)
     if cx.world == 1 and not a.no_scan:
         scan = scan_roofline(cx, a)
+    e2e = fw = wide = None
+    if cx.world == 1 and workload == "config2" and not a.no_extra:
+        e2e = e2e_leg(cx, m["nodes"], m["pods"], m["placement"])
+        fw = framework_leg(cx)
+        wide = wide_leg(cx, a)
     if cx.rank == 0:
         rl = roofline(m["kp"], m["n_nodes"], m["n_pods"], m["wall_fallback"])
         if m["sharded"]:
@@ -292,7 +465,7 @@ def main():
             "warmup": a.warmup, "ms_per_step": round(m["ms_per_step"], 3), "higher_is_better": True,
             "scaling": scaling, "vs_baseline": None, "dtype": "int32+f64",
             "data": f"synthetic (spec/synth.md generator, config {WORKLOADS[workload][0]})",
-            "config": {"workload": m["desc"], "engine": m["engine"],
+            "config": {"workload": m["desc"], "engine": m["engine"], "table_layout": m["table_layout"],
                        "lookahead": a.lookahead or 32, "parallelism": par},
             "evals_per_s": round(m["value"] * m["n_nodes"], 1),
             "p50_pod_latency_us": round(m["p50"], 4), "p99_pod_latency_us": round(m["p99"], 4),
@@ -320,6 +493,10 @@ def main():
                                       "unschedulable_frac": round(c5["unschedulable_frac"], 5)}
         if scan is not None:
             out["scan"] = scan
+        if e2e is not None:
+            out["end_to_end"] = e2e
+            out["framework_path"] = fw
+            out["wide_layout"] = wide
         if cx.world == 1 and not a.no_cpu:
             out["cpu_baseline"] = cpu_baseline(m["nodes"], m["pods"], m["n_nodes"], m["n_pods"],
                                                a.cpu_sample, gpu_placement=m["placement"])
@@ -329,7 +506,8 @@ def main():
         print(json.dumps(out), flush=True)
     if cx.dist is not None:
         cx.dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -1150,7 +1150,11 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                 // prepared stream): ~3 launches + 4 event operations per window would otherwise
                 // be issued one host call at a time.  Not used for diagnostic runs.
                 static const char *genv = getenv("QS_GRAPH");
-                const bool use_graph = !kt.on && !diag_on && !(genv && genv[0] == '0');
+                // Multi-rank contexts enqueue directly: RCCL collectives inside a captured graph
+                // across ranks have not been observed on this pool yet; QS_GRAPH=1
+                // forces capture for them.
+                const bool graph_ok = !c->comm || (genv && genv[0] == '1');
+                const bool use_graph = graph_ok && !kt.on && !diag_on && !(genv && genv[0] == '0');
                 if (use_graph) {
                     std::vector<uint8_t> key;
                     auto put = [&](const void *p, size_t nb) {

@@ -1,0 +1,94 @@
+"""bench.py's multi-GPU launch, host only (ADVICE r1 --gpus):
+* ``--gpus N`` without a launcher re-launches under torch.distributed.run with N ranks on a
+  127.0.0.1 rendezvous (checked through ``--dry-run``, which never touches a GPU);
+* a launcher's WORLD_SIZE that disagrees with --gpus is an error, not a silent 1-GPU run;
+* world size 2 over gloo: the rank plumbing bench.py uses on the GPU box (process group, RCCL id
+  broadcast from rank 0, max over ranks, barrier) up to the first HIP call, which reports a
+  status (no device here) instead of crashing or hanging.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def dry(args, env_extra=None):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, BENCH, "--dry-run"] + args, capture_output=True, text=True,
+                          env=env, timeout=120)
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_gpus_n_relaunches_under_torchrun(n):
+    r = dry(["--gpus", str(n), "--steps", "3", "--warmup", "1"])
+    assert r.returncode == 0, r.stderr
+    plan = json.loads(r.stdout.strip().splitlines()[-1])
+    assert plan["mode"] == "torchrun" and plan["world"] == n
+    argv = plan["argv"]
+    assert argv[1:3] == ["-m", "torch.distributed.run"]
+    assert f"--nproc-per-node={n}" in argv and "--master-addr=127.0.0.1" in argv and "--nnodes=1" in argv
+    i = argv.index(BENCH)
+    assert argv[i + 1:] == ["--gpus", str(n), "--steps", "3", "--warmup", "1"]  # no --dry-run, no loop
+
+
+def test_single_gpu_runs_in_process():
+    r = dry([])
+    assert json.loads(r.stdout.strip().splitlines()[-1]) == {"mode": "in-process", "world": 1}
+
+
+def test_launcher_world_size_must_match():
+    r = dry(["--gpus", "4"], {"WORLD_SIZE": "2"})
+    assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr
+    r = dry(["--gpus", "2"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 0 and json.loads(r.stdout.strip().splitlines()[-1])["mode"] == "in-process"
+
+
+def _rank(rank, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE="2",
+                      LOCAL_RANK=str(rank))
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "custom-k8s-scheduler_amd")]
+    import bench
+    import qsched
+
+    # no RCCL unique id without a GPU: a fixed stand-in id exercises the broadcast from rank 0
+    qsched.dist_unique_id = lambda: bytes(range(128))
+    cx = bench.Ctx(backend="gloo")
+    r, w, uid = cx.shard()
+    top = cx.max(float(rank) + 0.5)
+    cx.barrier()
+    status = None
+    try:
+        bench.open_sched(cx, {"engine": "lookahead"}, True)  # qs_open_shard: first HIP call
+    except qsched.QschedError as e:
+        status = e.status
+    cx.dist.destroy_process_group()
+    q.put((rank, r, w, uid, top, status))
+
+
+def test_world2_gloo_rank_plumbing():
+    import torch.multiprocessing as mp
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank, args=(r, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for rank, (r, r_, w, uid, top, status) in enumerate(res):
+        assert r == rank and r_ == rank and w == 2
+        assert uid == bytes(range(128))  # rank 1 received rank 0's id
+        assert top == 1.5                # max over ranks
+        assert status == 2               # QS_EDEVICE: no HIP device in this container
