@@ -1038,6 +1038,13 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                 if (c->dc.feat & kFeatTaint) wmax += c->cfg.w_taint;       // every plugin scores <= 100
                 if (c->dc.feat & kFeatAffinity) wmax += c->cfg.w_affinity;
                 geo.k32 = (100 * wmax + 1 < 1024 && n <= (1u << 22)) ? 1u : 0u;
+                // speculative batch resolver for the non-normalizing profiles on
+                // unsharded lists: opt-in with QS_SPEC=1 (measured slower than the four-wave
+                // pipelined resolver so far)
+                const char *spec_env = getenv("QS_SPEC");
+                geo.spec = (!norm && geo.W == 1 && geo.epl == 1 && geo.waves == 4 &&
+                            (spec_env && spec_env[0] == '1') && spec_resolver_fits(n)) ? 1u : 0u;
+                if (geo.spec) HIPCHK(spec_prepare());
                 if (geo.G == 0) fail(QS_EINVAL, "no lookahead geometry for this table size");
                 const size_t rank_entries = (size_t)geo.K * 64 * geo.eplr;  // [K][GLp] per shard
                 const size_t lwords = geo.W * rank_entries;                 // one window's lists
@@ -1201,7 +1208,12 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                     HIPCHK(hipMemcpyAsync(h, diag, 128, hipMemcpyDeviceToHost, c->stream));
                     HIPCHK(hipStreamSynchronize(c->stream));
                     const double np = h[5] ? (double)h[5] : 1.0;
-                    fprintf(stderr, geo.waves == 1 ? "QS_DIAG resolve cycles/pod: cand %.0f issue %.0f fresh %.0f wmax %.0f commit %.0f (pods %llu, G=%u E=%u epl=%u)\n"
+                    if (geo.spec)
+                        fprintf(stderr, "QS_DIAG spec cycles/batch: phase1 %.0f phase2 %.0f phase3 %.0f; batches %llu (%.2f pods/batch, dirty wins %llu) pods %llu; prologue/window %.0f\n",
+                                h[0] / (double)(h[3] ? h[3] : 1), h[1] / (double)(h[3] ? h[3] : 1), h[2] / (double)(h[3] ? h[3] : 1),
+                                (unsigned long long)h[3], h[5] / (double)(h[3] ? h[3] : 1), (unsigned long long)h[4],
+                                (unsigned long long)h[5], h[8] / (double)nwin);
+                    else fprintf(stderr, geo.waves == 1 ? "QS_DIAG resolve cycles/pod: cand %.0f issue %.0f fresh %.0f wmax %.0f commit %.0f (pods %llu, G=%u E=%u epl=%u)\n"
                                                    : "QS_DIAG resolve4 busy cycles/pod: D %.0f A %.0f B %.0f C %.0f (C row wait %.0f) (pods %llu, G=%u E=%u epl=%u)\n",
                             h[0] / np, h[1] / np, h[2] / np, h[3] / np, h[4] / np,
                             (unsigned long long)h[5], geo.G, geo.E, geo.epl);

@@ -123,6 +123,16 @@ hipError_t launch_scan_pod(const DevTable &t, const void *pods, const DPodX *pod
 
 size_t scan_scratch_bytes() { return sizeof(ScanScratch); }
 
+bool spec_resolver_fits(uint32_t n) {
+    return std::max(spec_lds_bytes<kFeatExt>(n), spec_lds_bytes<kFeatExt | kFeatWide>(n)) <= 160 * 1024;
+}
+
+hipError_t spec_prepare() {
+    QS_RET(spec_prepare_f<0>());
+    QS_RET(spec_prepare_f<kFeatExt>());
+    return wide_spec_prepare();
+}
+
 hipError_t launch_la_window(const DevTable &t, const void *pods, const DPodX *podx, uint32_t s0,
                             uint32_t P, const DevCfg &c, const LaGeom &geo, const LaBufs &bf,
                             int32_t *on, uint64_t *ok, uint64_t *st, uint64_t *diag,

@@ -311,6 +311,34 @@ __device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t (*buf)[NW], i
     return s;
 }
 
+// Descending bitonic sort of one 64-bit key per lane across the wave (21 compare-exchange steps).
+__device__ __forceinline__ uint64_t wave_sort_desc(uint64_t v, int lane) {
+#pragma unroll
+    for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, j);
+            const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), j);
+            const uint64_t o = ((uint64_t)hi << 32) | lo;
+            const bool keep_max = ((lane & j) == 0) == ((lane & k) == 0);
+            v = keep_max ? (v > o ? v : o) : (v < o ? v : o);
+        }
+    }
+    return v;
+}
+
+// Sorts a pod's final list (out[0..L), L <= 64, zero-padded) best-first, so that the top clean
+// entries are its first clean lanes (k_la_resolve_spec).  Every thread of the block calls it.
+__device__ __forceinline__ void sort_list_desc(uint64_t *__restrict__ out, uint32_t L) {
+    __syncthreads();  // the block's stores of out[] are visible to wave 0
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        uint64_t v = (uint32_t)lane < L ? out[lane] : 0ull;
+        v = wave_sort_desc(v, lane);
+        if ((uint32_t)lane < L) out[lane] = v;
+    }
+}
+
 // Block-wide top-L of per-position values tv (0 = empty).  Position order is (wave, j, lane):
 // wave w owns positions [w*E*64, (w+1)*E*64), so when positions follow node-index order, ranks
 // come from ballots and one cross-wave prefix.  Writes the keys of the L largest values to
@@ -543,6 +571,7 @@ __device__ __forceinline__ void la_select_block(uint32_t bid, const DevTable &t,
     uint64_t *out = G == 1 ? lists + (size_t)b.v * sh.RS + (size_t)b.k * GLp
                            : clists + (((size_t)b.vs * sh.kw + b.k) * G + b.g) * L;
     block_topl<BS, E>(tv, L, out, [&](int j) { return pack_key(tv[j], base + j * kWave); });
+    if (G == 1) sort_list_desc(out, L);  // a final list (else k_la_merge sorts)
 }
 
 template <int BS, int E, uint32_t F>
@@ -578,8 +607,9 @@ __device__ __forceinline__ void la_merge_block(uint32_t bid, const uint64_t *__r
         e[j] = pos < M ? in[pos] : 0ull;
         tv[j] = (uint32_t)(e[j] >> 32);
     }
-    block_topl<256, E2>(tv, L, lists + (size_t)(sh.v0 + vs) * sh.RS + (size_t)k * GLp,
-                        [&](int j) { return e[j]; });
+    uint64_t *out = lists + (size_t)(sh.v0 + vs) * sh.RS + (size_t)k * GLp;
+    block_topl<256, E2>(tv, L, out, [&](int j) { return e[j]; });
+    sort_list_desc(out, L);
 }
 
 template <int E2, bool WIDE>
@@ -1455,6 +1485,327 @@ __global__ __launch_bounds__(256) void k_la_resolve4(DevTable t, const PodT<F> *
 }
 
 // =============================================================================================
+// Speculative batch resolver: Fit + Balanced (+ extended resources) profiles,
+// unsharded sorted lists.  The window is resolved in batches of up to four pods, one per wave
+// (wave w owns the window's pods p ≡ w (mod 4)).  Speculation: every pod of a batch takes its
+// best clean list entry (lists are sorted best-first, so: its first clean lane) that no earlier
+// pod of the batch took.  Each wave then scores its pod exactly against every dirty node (the
+// slots, replicated in every wave's lanes) and against the batch's earlier candidates reserved
+// with their pods.  The first pod whose best dirty key beats its candidate is resolved by that
+// key — exact, because every earlier pod of the batch did take its candidate — and ends the
+// batch; the pods before it commit their candidates as new slots.  Two barriers per batch; in
+// config 2 about 84 % of the pods take their clean candidate, i.e. ~3 pods per batch.
+// =============================================================================================
+constexpr uint32_t kSpecM = 4;  // pods per batch = waves
+constexpr uint32_t kSpecRing = 4;  // list ring slots per wave (pod ordinals in flight)
+// Candidate record: its list key and where its row sits in the row ring.
+struct alignas(16) SpecCand {
+    uint64_t key;
+    uint32_t ring;  // row ring index ((wave * kSpecRing + slot) * 64 + lane)
+    uint32_t pad;
+};
+// Dynamic LDS: dirty bitmap | row ring [4][4][64] R | ext ring [4][4][64] int4 (kFeatExt) |
+// key ring [4][4][64] u64 | cand [2][4][4] | resk [4] u64 | ccount [2][4] u32 | pods [64].
+template <uint32_t F>
+constexpr size_t spec_lds_bytes(uint32_t n) {
+    constexpr size_t ring = (size_t)kSpecM * kSpecRing * 64;
+    return (((size_t)(n + 31) / 32 + 3) & ~(size_t)3) * 4 + ring * sizeof(RowT<F>) +
+           ((F & kFeatExt) ? ring * sizeof(int4) : 0) + ring * 8 + 2 * kSpecM * kSpecM * sizeof(SpecCand) +
+           8 * kSpecM + 4 * 2 * kSpecM + 64 * sizeof(PodT<F>);
+}
+
+template <uint32_t F, bool K32, bool DIAG>
+__global__ __launch_bounds__(64 * kSpecM) void k_la_resolve_spec(
+    DevTable t, const PodT<F> *__restrict__ pods, DevCfg c, uint32_t s0, uint32_t P, uint32_t K,
+    uint32_t GLp, const uint64_t *__restrict__ lists, int32_t *__restrict__ out_node,
+    uint64_t *__restrict__ out_key, uint64_t *__restrict__ stamps, const uint32_t *__restrict__ dprev,
+    uint32_t *__restrict__ dcur, uint64_t *__restrict__ diag) {
+    uint64_t dph[3] = {0, 0, 0}, dnb = 0, dfail = 0, tprev = 0;
+    const uint64_t t_start = DIAG ? diag_stamp() : 0ull;
+    using R = RowT<F>;
+    using PD = PodT<F>;
+    constexpr bool EXT = (F & kFeatExt) != 0;
+    constexpr uint32_t kRing = kSpecM * kSpecRing * 64;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const int lane = threadIdx.x & 63;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t n = t.n, nwords = (n + 31) / 32;
+    uint32_t *dirty = lds;
+    char *base = (char *)(lds + ((nwords + 3) & ~3u));
+    R *rring = (R *)base;  // rows of the wave's pods' list entries, by pod ordinal mod 4
+    base += kRing * sizeof(R);
+    int4 *xring = (int4 *)base;  // their extended-resource columns
+    if (EXT) base += kRing * sizeof(int4);
+    uint64_t *kring = (uint64_t *)base;  // their list keys
+    base += kRing * 8;
+    SpecCand(*cand)[kSpecM][kSpecM] = (SpecCand(*)[kSpecM][kSpecM])base;  // [step parity][wave][rank]
+    base += 2 * kSpecM * kSpecM * sizeof(SpecCand);
+    uint64_t *resk = (uint64_t *)base;  // [batch position] best dirty key
+    base += 8 * kSpecM;
+    uint32_t *ccount = (uint32_t *)base;  // [step parity][wave] clean candidates found (<= 4)
+    base += 4 * 2 * kSpecM;
+    PD *wpods = (PD *)base;  // the window's pod records (K <= 64)
+    const DPodX px{};
+    const uint32_t kend = min(K, P - s0);
+    auto ridx = [&](uint32_t w, uint32_t ord, uint32_t l) { return (w * kSpecRing + (ord & (kSpecRing - 1))) * 64 + l; };
+    auto fetch_key = [&](uint32_t ord) -> uint64_t {
+        const uint32_t j = wv + kSpecM * ord;
+        return j < kend ? lists[(size_t)j * GLp + lane] : 0ull;
+    };
+    for (uint32_t i = threadIdx.x; i < nwords; i += 64 * kSpecM) dirty[i] = 0;
+    if (threadIdx.x < kend) wpods[threadIdx.x] = pods[s0 + threadIdx.x];
+    // slots (dirty nodes, one per lane), replicated bit for bit in every wave: the nodes the
+    // previous (overlapped) window dirtied first
+    const uint32_t nd0 = dprev ? dprev[0] : 0u;
+    uint32_t nd = nd0;
+    uint32_t sidx = (uint32_t)lane < nd0 ? dprev[1 + lane] : 0xFFFFFFFFu;
+    R S = empty_row<F>();
+    RowX SX{};
+    if ((uint32_t)lane < nd0) {
+        S = load_row<F>(t, sidx);
+        SX = load_rowx<F>(t, sidx);
+    }
+    bool won = false;  // slot won a pod of THIS window (handed to the next window's dprev)
+    // This wave's pods j = wv + 4m (ordinal m).  Keys and rows of their list entries live in LDS
+    // rings; every step re-issues, unconditionally, the key load of ordinal m+3 (kT) and the row
+    // loads of ordinal m+2 (T) and stores the previous step's ones: no load is waited for in the
+    // step that issues it, and no loaded register is carried conditionally.
+    {
+        uint64_t k0 = fetch_key(0), k1 = fetch_key(1), k2 = fetch_key(2);
+        kring[ridx(wv, 0, lane)] = k0;
+        kring[ridx(wv, 1, lane)] = k1;
+        kring[ridx(wv, 2, lane)] = k2;
+        const uint32_t a0 = k0 ? key_node(k0) : 0u, a1 = k1 ? key_node(k1) : 0u;
+        const R ra = load_row<F>(t, a0), rb = load_row<F>(t, a1);
+        const RowX xa = load_rowx<F>(t, a0), xb = load_rowx<F>(t, a1);
+        rring[ridx(wv, 0, lane)] = ra;
+        rring[ridx(wv, 1, lane)] = rb;
+        if (EXT) {
+            xring[ridx(wv, 0, lane)] = make_int4(xa.ae0, xa.re0, xa.ae1, xa.re1);
+            xring[ridx(wv, 1, lane)] = make_int4(xb.ae0, xb.re0, xb.ae1, xb.re1);
+        }
+    }
+    uint32_t mo = 0, oT = 2, oK = 3;
+    uint64_t kT = fetch_key(3);
+    R T;
+    RowX TX;
+    {
+        const uint64_t k2 = kring[ridx(wv, 2, lane)];
+        const uint32_t a2 = k2 ? key_node(k2) : 0u;
+        T = load_row<F>(t, a2);
+        TX = load_rowx<F>(t, a2);
+    }
+    __syncthreads();
+    if (threadIdx.x < nd0) atomicOr(&dirty[sidx >> 5], 1u << (sidx & 31));
+    uint64_t res_key = 0, res_stamp = 0;  // wave 0, lane k: window pod k's result
+    uint32_t newd[kSpecM] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};  // last batch's new slots
+    uint32_t i = 0;
+    int par = 0;
+    __syncthreads();
+    if (DIAG) {
+        tprev = diag_stamp();
+        if (threadIdx.x == 0) atomicAdd((unsigned long long *)&diag[8], (unsigned long long)(tprev - t_start));
+    }
+    while (i < kend) {
+        const uint32_t bn = min(kSpecM, kend - i);
+        const uint32_t k_me = (wv - i) & (kSpecM - 1);  // my pod = i + k_me (ordinal mo)
+        // ---- ring upkeep: store last step's loads, issue this step's (ordinals mo+2, mo+3)
+        kring[ridx(wv, oK, lane)] = kT;
+        rring[ridx(wv, oT, lane)] = T;
+        if (EXT) xring[ridx(wv, oT, lane)] = make_int4(TX.ae0, TX.re0, TX.ae1, TX.re1);
+        oK = mo + 3;
+        oT = mo + 2;
+        kT = fetch_key(oK);
+        {
+            const uint64_t kk = kring[ridx(wv, oT, lane)];
+            const uint32_t a = kk ? key_node(kk) : 0u;
+            T = load_row<F>(t, a);
+            TX = load_rowx<F>(t, a);
+        }
+        // ---- phase 1: my pod's top-4 clean entries (dirty: bitmap + the last batch's new slots)
+        if (k_me < bn) {
+            const uint64_t e = kring[ridx(wv, mo, lane)];
+            const uint32_t node = e ? key_node(e) : 0u;
+            bool cl = e != 0 && !((dirty[node >> 5] >> (node & 31)) & 1u);
+#pragma unroll
+            for (uint32_t q = 0; q < kSpecM; ++q) cl &= node != newd[q];
+            const uint64_t B = __ballot(cl);
+            const uint32_t rank = (uint32_t)__popcll(B & ((1ull << lane) - 1ull));
+            if (cl && rank < kSpecM) cand[par][wv][rank] = SpecCand{e, ridx(wv, mo, lane), 0u};
+            if (lane == 0) ccount[par * kSpecM + wv] = min((uint32_t)__popcll(B), kSpecM);
+        }
+        if (DIAG) { const uint64_t t_ = diag_stamp(); dph[0] += t_ - tprev; tprev = t_; }
+        __syncthreads();
+        // ---- phase 2 (every wave): the batch's candidates in pod order, replayed identically
+        const uint32_t q = (uint32_t)lane & (kSpecM * kSpecM - 1);
+        const uint32_t qw = q / kSpecM, qr = q % kSpecM;
+        const SpecCand qc = cand[par][qw][qr];
+        const uint64_t qkey = qr < ccount[par * kSpecM + qw] ? qc.key : 0ull;
+        const uint32_t qnode = qkey ? key_node(qkey) : 0xFFFFFFFFu;
+        uint64_t ck[kSpecM];
+        uint32_t cring[kSpecM], cpos[kSpecM];
+        uint32_t ncand = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kSpecM; ++k) {
+            ck[k] = 0;
+            cring[k] = 0;
+            cpos[k] = 0xFFFFFFFFu;
+            if (k < bn) {
+                bool ok = lane < (int)(kSpecM * kSpecM) && qw == ((i + k) & (kSpecM - 1)) && qkey != 0;
+#pragma unroll
+                for (uint32_t t2 = 0; t2 < kSpecM; ++t2)
+                    ok &= !(t2 < k && ck[t2] != 0 && qnode == key_node(ck[t2]));
+                const uint64_t m = __ballot(ok);
+                if (m) {
+                    const int src = (int)__builtin_ctzll(m);
+                    ck[k] = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(qkey >> 32), src) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)qkey, src);
+                    cring[k] = (uint32_t)__builtin_amdgcn_readlane((int)qc.ring, src);
+                    cpos[k] = ncand++;
+                }
+            }
+        }
+        // candidate lanes nd + cpos[t]: candidate t's row reserved with pod t (every wave keeps
+        // them: the committed ones become slots in phase 3)
+        const int ct = lane - (int)nd;  // candidate ordinal of this lane
+        uint32_t tl = 0xFFFFFFFFu, tr = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kSpecM; ++k)
+            if (ct >= 0 && (uint32_t)ct == cpos[k]) { tl = k; tr = cring[k]; }
+        R Rc = empty_row<F>();
+        RowX Xc{};
+        if (tl != 0xFFFFFFFFu) {
+            Rc = rring[tr];
+            if (EXT) {
+                const int4 e = xring[tr];
+                Xc.ae0 = e.x; Xc.re0 = e.y; Xc.ae1 = e.z; Xc.re1 = e.w;
+            }
+            reserve(Rc, Xc, wpods[i + tl], +1);
+        }
+        if (k_me < bn) {
+            // my pod vs every dirty node: the slots, and the candidates of the batch's earlier pods
+            const PD p = wpods[i + k_me];
+            const bool act = (uint32_t)lane < nd || tl < k_me;
+            const R rr = sel_row((uint32_t)lane < nd, S, Rc);
+            const RowX xx = sel_rowx((uint32_t)lane < nd, SX, Xc);
+            uint32_t node = sidx;
+#pragma unroll
+            for (uint32_t k = 0; k < kSpecM; ++k)
+                if (tl == k) node = ck[k] ? key_node(ck[k]) : 0u;
+            const bool f = act && feasible<F>(rr, xx, p, px);
+            const uint32_t tot = node_total<F>(rr, xx, p, px, c, 0, 0.0, 0, 0.0, nullptr);
+            const uint64_t key = f ? pack_key(tot + 1, node) : 0ull;
+            uint64_t best;
+            if (K32) {  // (score+1) < 2^10 and n <= 2^22: one 32-bit reduction
+                const uint32_t tv = (uint32_t)(key >> 32);
+                const uint32_t k32 = tv ? (tv << 22) | (0x3FFFFFu - key_node(key)) : 0u;
+                const uint32_t m = wave_max_u32(k32);
+                best = m ? (((uint64_t)(m >> 22) << 32) | (uint64_t)(0xFFFFFFFFu - (0x3FFFFFu - (m & 0x3FFFFFu)))) : 0ull;
+            } else {
+                best = wave_max_u64(key);
+            }
+            if (lane == 0) resk[k_me] = best;
+        }
+        if (DIAG) { const uint64_t t_ = diag_stamp(); dph[1] += t_ - tprev; tprev = t_; }
+        __syncthreads();
+        // ---- phase 3 (every wave, identical): commit the batch up to its first dirty win
+        uint32_t committed = bn, fail = 0xFFFFFFFFu;
+        uint64_t fkey = 0;
+        uint64_t rk[kSpecM];
+#pragma unroll
+        for (uint32_t k = 0; k < kSpecM; ++k) {
+            rk[k] = 0;
+            if (k < bn && fail == 0xFFFFFFFFu) {
+                const uint64_t bd = resk[k];
+                if (bd > ck[k]) {  // a dirty node beats the clean candidate: pod k is exact, stop
+                    fail = k;
+                    fkey = bd;
+                    rk[k] = bd;
+                    committed = k + 1;
+                } else {
+                    rk[k] = ck[k];  // the candidate (0: unschedulable)
+                }
+            }
+        }
+        // new slots: the committed candidates (pods before the failing one)
+        uint32_t nadd = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kSpecM; ++k) {
+            const bool take = k < committed && k != fail && ck[k] != 0;
+            newd[k] = take ? key_node(ck[k]) : 0xFFFFFFFFu;
+            nadd += take ? 1u : 0u;
+        }
+        if (tl != 0xFFFFFFFFu && tl < committed && tl != fail) {
+            S = Rc;
+            SX = Xc;
+            sidx = key_node(ck[tl]);
+            won = true;
+        }
+        nd += nadd;  // committed candidates hold the lanes nd .. nd + nadd - 1 (cpos order)
+        if (fail != 0xFFFFFFFFu) {  // the failing pod's dirty winner takes it
+            const uint32_t w = key_node(fkey);
+            const uint64_t own = __ballot((uint32_t)lane < nd && sidx == w);
+            if (lane == (int)__builtin_ctzll(own)) {
+                reserve(S, SX, wpods[i + fail], +1);
+                won = true;
+            }
+        }
+        if (wv == 0) {
+            if (lane == 0) {
+#pragma unroll
+                for (uint32_t k = 0; k < kSpecM; ++k)
+                    if (newd[k] != 0xFFFFFFFFu) atomicOr(&dirty[newd[k] >> 5], 1u << (newd[k] & 31));
+            }
+            const uint64_t now = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
+#pragma unroll
+            for (uint32_t k = 0; k < kSpecM; ++k)
+                if (k < committed && (uint32_t)lane == i + k) { res_key = rk[k]; res_stamp = now; }
+        }
+        if (wv + kSpecM * mo < i + committed) ++mo;  // my pod committed
+        i += committed;
+        par ^= 1;
+        if (DIAG) {
+            const uint64_t t_ = diag_stamp();
+            dph[2] += t_ - tprev;
+            tprev = t_;
+            ++dnb;
+            dfail += fail != 0xFFFFFFFFu ? 1u : 0u;
+        }
+    }
+    if (DIAG && threadIdx.x == 0) {
+        for (int k = 0; k < 3; ++k) atomicAdd((unsigned long long *)&diag[k], (unsigned long long)dph[k]);
+        atomicAdd((unsigned long long *)&diag[3], (unsigned long long)dnb);
+        atomicAdd((unsigned long long *)&diag[4], (unsigned long long)dfail);
+        atomicAdd((unsigned long long *)&diag[5], (unsigned long long)kend);
+    }
+    if (wv != 0) return;
+    if ((uint32_t)lane < kend) {
+        const uint32_t s = s0 + lane;
+        out_node[s] = res_key ? (int32_t)key_node(res_key) : -1;
+        if (out_key) out_key[s] = res_key;
+        if (stamps) stamps[s] = res_stamp;
+    }
+    if (won && (uint32_t)lane < nd) { store_dyn<F>(t, sidx, S); store_dynx<F>(t, sidx, SX); }
+    if (dcur) {  // nodes dirtied in this window, for the next (overlapped) window
+        const uint64_t wm = __ballot(won && (uint32_t)lane < nd);
+        if (won && (uint32_t)lane < nd) dcur[1 + __popcll(wm & ((1ull << lane) - 1ull))] = sidx;
+        if (lane == 0) dcur[0] = (uint32_t)__popcll(wm);
+    }
+}
+
+template <uint32_t F>
+static hipError_t spec_prepare_f() {
+    // the rings take the dynamic LDS past the default 64 KB: raise the limit once, outside capture
+    static const hipError_t a1 = hipFuncSetAttribute((const void *)k_la_resolve_spec<F, true, false>,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    static const hipError_t a2 = hipFuncSetAttribute((const void *)k_la_resolve_spec<F, false, false>,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    static const hipError_t a3 = hipFuncSetAttribute((const void *)k_la_resolve_spec<F, true, true>,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    return a1 != hipSuccess ? a1 : a2 != hipSuccess ? a2 : a3;
+}
+
+// =============================================================================================
 // BATCHED mode (spec S11): per batch of B <= 64 pods, k_la_select + k_la_merge give each pod its
 // 64 best keys against the batch-start table; k_batch_claim walks the batch in queue order, each
 // pod claiming its best key whose node (and, for zone anti-affinity, whose (app, zone)) no earlier
@@ -1462,22 +1813,6 @@ __global__ __launch_bounds__(256) void k_la_resolve4(DevTable t, const PodT<F> *
 // the next batch: the pods that found no free candidate first, then fresh pods from the stream.
 // ctrl = {pods in the batch, stream cursor}.
 // =============================================================================================
-// Descending bitonic sort of one 64-bit key per lane across the wave (21 compare-exchange steps).
-__device__ __forceinline__ uint64_t wave_sort_desc(uint64_t v, int lane) {
-#pragma unroll
-    for (int k = 2; k <= 64; k <<= 1) {
-#pragma unroll
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, j);
-            const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), j);
-            const uint64_t o = ((uint64_t)hi << 32) | lo;
-            const bool keep_max = ((lane & j) == 0) == ((lane & k) == 0);
-            v = keep_max ? (v > o ? v : o) : (v < o ? v : o);
-        }
-    }
-    return v;
-}
-
 #ifdef QS_CLAIM_DIAG
 static __device__ uint64_t g_claim_diag[5];
 #define CLAIM_STAMP0() uint64_t cds[4] = {0, 0, 0, 0}; uint64_t ctp = diag_stamp();
@@ -1825,6 +2160,20 @@ static hipError_t la_window_f(const DevTable &t, const void *pods_, const DPodX 
         const uint64_t *lists = bf.lists;
         const uint32_t *dprev = bf.dprev;
         uint32_t *dcur = bf.dcur;
+        if (geo.spec) {  // speculative batch resolver (unsharded sorted lists)
+            if (geo.epl != 1 || geo.W != 1) return hipErrorInvalidValue;
+            const size_t ldss = spec_lds_bytes<F>(t.n);
+            if (diag && geo.k32)
+                hipLaunchKernelGGL((k_la_resolve_spec<F, true, true>), dim3(1), dim3(64 * kSpecM), ldss, stream, t, pods, c, s0, P,
+                                   K, GLp, lists, on, ok, st, dprev, dcur, diag);
+            else if (geo.k32)
+                hipLaunchKernelGGL((k_la_resolve_spec<F, true, false>), dim3(1), dim3(64 * kSpecM), ldss, stream, t, pods, c, s0, P,
+                                   K, GLp, lists, on, ok, st, dprev, dcur, nullptr);
+            else
+                hipLaunchKernelGGL((k_la_resolve_spec<F, false, false>), dim3(1), dim3(64 * kSpecM), ldss, stream, t, pods, c, s0, P,
+                                   K, GLp, lists, on, ok, st, dprev, dcur, nullptr);
+            return hipGetLastError();
+        }
         const size_t lds = bm + sizeof(RowT<F>) + sizeof(RowX);
         const size_t lds4 = bm + 5 * 2 * 64 * 8 + 2 * 64 * (sizeof(RowT<F>) + sizeof(int4)) + 2 * sizeof(ResPub) + 64 * 4 + 64 * sizeof(PodT<F>);
         switch (geo.epl) {
@@ -1876,6 +2225,7 @@ hipError_t wide_la_window(const DevTable &t, const void *pods, const DPodX *podx
                           int32_t *on, uint64_t *ok, uint64_t *st, uint64_t *diag,
                           hipStream_t stream, int part);
 hipError_t wide_batch_claim_prepare();
+hipError_t wide_spec_prepare();
 hipError_t wide_batch_claim(const DevTable &t, const void *pods, const uint64_t *lists, uint32_t *ctrl,
                             uint32_t *bidx, uint32_t P, uint32_t B, int32_t *on, uint64_t *ok,
                             size_t lds, hipStream_t stream);

@@ -14,6 +14,12 @@ struct Rational {
     i128 num, den;  // value = num / den, den > 0
 };
 
+i128 checked_mul(i128 a, i128 b, const std::string &s) {
+    i128 r;
+    if (__builtin_mul_overflow(a, b, &r)) throw QuantityError("quantity: out of range in '" + s + "'");
+    return r;
+}
+
 Rational parse(const std::string &s) {
     size_t i = 0;
     bool neg = false;
@@ -59,12 +65,15 @@ Rational parse(const std::string &s) {
     } else {
         throw QuantityError("quantity: unknown suffix '" + suf + "' in '" + s + "'");
     }
-    Rational r{mant * mul, den * div};
+    // 30 digits (< 2^100) times a suffix factor up to 2^60 / 10^18 can leave the i128 range:
+    // checked, so an absurd quantity is a QuantityError rather than signed overflow
+    Rational r{checked_mul(mant, mul, s), checked_mul(den, div, s)};
     if (neg) r.num = -r.num;
     return r;
 }
 
 int64_t ceil_div(i128 num, i128 den) {
+    if (den <= 0) throw QuantityError("quantity: bad denominator");
     i128 q = num / den;
     if (num % den != 0 && num > 0) ++q;
     if (q > (i128)INT64_MAX || q < (i128)INT64_MIN) throw QuantityError("quantity: out of int64 range");
@@ -75,7 +84,7 @@ int64_t ceil_div(i128 num, i128 den) {
 
 int64_t parse_quantity_milli(const std::string &s) {
     const Rational r = parse(s);
-    return ceil_div(r.num * 1000, r.den);
+    return ceil_div(checked_mul(r.num, 1000, s), r.den);
 }
 
 int64_t value(const std::string &s) {

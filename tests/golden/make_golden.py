@@ -27,14 +27,23 @@ CASES = [
     ("config4_fitonly", 4, 300, 3000, {}),
     ("arrival_order", 2, 200, 2500, {"qos_sort": 0}),
     ("config2_tight", 2, 150, 5000, {}),
+    # batched mode (spec S11): 64-pod batches with hostname/zone anti-affinity (config 5 draws)
+    ("config5_batched", 5, 400, 8000, {"mode": "batched", "batch": 64}),
 ]
 DYN = ["req_cpu", "req_mem", "req_ext", "nz_cpu", "nz_mem", "pods"]
 
 
-def input_digest(nodes, pods):
+V1_SKIP = ("zone", "app", "anti_affinity")  # ABI-v2 columns, added after the first fixtures
+
+
+def input_digest(nodes, pods, full=False):
+    """SHA-256 over the generated columns; full=False skips the ABI-v2 columns (the digest the
+    first fixtures recorded), full=True covers every column."""
     h = hashlib.sha256()
     for d in (nodes, pods):
         for k in sorted(d):
+            if not full and k in V1_SKIP:
+                continue
             h.update(k.encode())
             h.update(np.ascontiguousarray(d[k]).tobytes())
     return h.hexdigest()
@@ -42,10 +51,16 @@ def input_digest(nodes, pods):
 
 def build(name, config, n, p, profile, check_python=True):
     nodes, pods = O.generate(config, n, p)
-    cfg = dict(O.DEFAULT_CONFIG, **profile)
+    prof = {k: v for k, v in profile.items() if k not in ("mode", "batch")}
+    cfg = dict(O.DEFAULT_CONFIG, **prof)
     digest = input_digest(nodes, pods)
     nc, _ = O.copy_cluster(nodes, pods)
-    pl, best, order = O.schedule(nc, pods, cfg)
+    if profile.get("mode") == "batched":
+        pl, best, nb = O.schedule_batched(nc, pods, batch=profile["batch"], cfg=cfg)
+        order = np.arange(p, dtype=np.uint32)  # batched mode keeps queue order per batch (S11)
+        check_python = False  # the pure-Python restatement covers the exact mode only
+    if profile.get("mode") != "batched":
+        pl, best, order = O.schedule(nc, pods, cfg)
     if check_python:
         npy, _ = O.copy_cluster(nodes, pods)
         pl2, best2 = O.py_schedule(npy, pods, cfg)
@@ -54,7 +69,10 @@ def build(name, config, n, p, profile, check_python=True):
     for k in DYN:
         out["final_" + k] = nc[k]
     meta = dict(name=name, config=config, nodes=n, pods=p, profile=profile, seed=0x5EED0000 + config,
-                input_sha256=digest, placed=int((pl >= 0).sum()))
+                input_sha256=digest, input_sha256_full=input_digest(nodes, pods, full=True),
+                placed=int((pl >= 0).sum()))
+    if profile.get("mode") == "batched":
+        meta["batches"] = nb
     return out, meta
 
 

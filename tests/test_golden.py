@@ -15,16 +15,24 @@ HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 INDEX = json.load(open(os.path.join(HERE, "index.json")))
 
 
-def _digest(nodes, pods):
+def _digest(nodes, pods, full=False):
     import hashlib
     h = hashlib.sha256()
     for d in (nodes, pods):
         for k in sorted(d):
-            if k in ("zone", "app", "anti_affinity"):  # ABI v2 columns, after the fixtures
+            if not full and k in ("zone", "app", "anti_affinity"):  # ABI-v2 columns (input_sha256_full)
                 continue
             h.update(k.encode())
             h.update(np.ascontiguousarray(d[k]).tobytes())
     return h.hexdigest()
+
+
+def _batched(meta):
+    return meta["profile"].get("mode") == "batched"
+
+
+def _profile(meta):
+    return {k: v for k, v in meta["profile"].items() if k not in ("mode", "batch")}
 
 
 def _load(meta):
@@ -38,13 +46,22 @@ def test_inputs_reproduce(meta):
     assert _digest(*O.py_generate(c, n, p)) == meta["input_sha256"]
     nodes, pods = qsched.synth_generate(c, n, p)
     assert _digest(nodes, qsched.pods_from_struct(pods)) == meta["input_sha256"]
+    # every column, the zone / app / anti-affinity ones included
+    assert _digest(*O.generate(c, n, p), full=True) == meta["input_sha256_full"]
+    assert _digest(nodes, qsched.pods_from_struct(pods), full=True) == meta["input_sha256_full"]
 
 
 @pytest.mark.parametrize("meta", INDEX, ids=[m["name"] for m in INDEX])
 def test_oracle_reproduces_outputs(meta):
     g = _load(meta)
     nodes, pods = O.generate(meta["config"], meta["nodes"], meta["pods"])
-    pl, best, order = O.schedule(nodes, pods, dict(O.DEFAULT_CONFIG, **meta["profile"]))
+    cfg = dict(O.DEFAULT_CONFIG, **_profile(meta))
+    if _batched(meta):
+        pl, best, nb = O.schedule_batched(nodes, pods, batch=meta["profile"]["batch"], cfg=cfg)
+        assert nb == meta["batches"]
+        order = g["order"]
+    else:
+        pl, best, order = O.schedule(nodes, pods, cfg)
     assert np.array_equal(pl, g["placement"])
     assert np.array_equal(best, g["best_key"])
     assert np.array_equal(order, g["order"])
@@ -53,8 +70,9 @@ def test_oracle_reproduces_outputs(meta):
 
 
 def _engines(meta):
-    norm = meta["profile"].get("enable_taint") or meta["profile"].get("enable_affinity")
-    return ["persistent", "scan"] if norm else ["persistent", "scan", "lookahead"]
+    if _batched(meta):
+        return ["batched"]
+    return ["persistent", "scan", "lookahead", "auto"]
 
 
 @pytest.mark.gpu
@@ -63,10 +81,16 @@ def test_gpu_reproduces_golden(meta):
     g = _load(meta)
     nodes, pods = qsched.synth_generate(meta["config"], meta["nodes"], meta["pods"])
     for eng in _engines(meta):
-        with qsched.Scheduler(dict(meta["profile"], engine=eng)) as s:
+        if eng == "batched":
+            prof, mode = dict(_profile(meta), batch_pods=meta["profile"]["batch"]), "batched"
+        else:
+            prof, mode = dict(_profile(meta), engine=eng), "exact"
+        with qsched.Scheduler(prof) as s:
             s.load_nodes(nodes)
             st = s.prepare(pods)
-            st.run()
+            stats = st.run(mode=mode)
+            if eng == "batched":
+                assert stats["batches"] == meta["batches"]
             pl, keys = st.results()
             st.free()
             fin = s.read_nodes()
