@@ -1041,10 +1041,15 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                 // speculative batch resolver for the non-normalizing profiles on
                 // unsharded lists: opt-in with QS_SPEC=1 (measured slower than the four-wave
                 // pipelined resolver so far)
-                const char *spec_env = getenv("QS_SPEC");
-                geo.spec = (!norm && geo.W == 1 && geo.epl == 1 && geo.waves == 4 &&
-                            (spec_env && spec_env[0] == '1') && spec_resolver_fits(n)) ? 1u : 0u;
-                if (geo.spec) HIPCHK(spec_prepare());
+                // QS_RESOLVER = four (default) | run | spec: the speculative resolvers are opt-in
+                // (measured at or below the four-wave pipeline so far)
+                const char *rv = getenv("QS_RESOLVER");
+                const bool plain = !norm && geo.W == 1 && geo.epl == 1 && geo.waves == 4;
+                geo.spec = 0;
+                if (plain && rv && !strcmp(rv, "spec") && spec_resolver_fits(n)) geo.spec = 1;
+                if (plain && rv && !strcmp(rv, "run") && geo.k32 && geo.K <= 32 && run_resolver_fits(n)) geo.spec = 2;
+                if (geo.spec == 1) HIPCHK(spec_prepare());
+                if (geo.spec == 2) HIPCHK(run_prepare());
                 if (geo.G == 0) fail(QS_EINVAL, "no lookahead geometry for this table size");
                 const size_t rank_entries = (size_t)geo.K * 64 * geo.eplr;  // [K][GLp] per shard
                 const size_t lwords = geo.W * rank_entries;                 // one window's lists
@@ -1208,7 +1213,15 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                     HIPCHK(hipMemcpyAsync(h, diag, 128, hipMemcpyDeviceToHost, c->stream));
                     HIPCHK(hipStreamSynchronize(c->stream));
                     const double np = h[5] ? (double)h[5] : 1.0;
-                    if (geo.spec)
+                    if (geo.spec == 2)
+                        fprintf(stderr, "QS_DIAG run cycles/round: picks %.0f score %.0f B2-wait %.0f verify %.0f; rounds %llu (%.2f pods/round, dirty wins %llu) pods %llu\n",
+                                h[0] / (double)(h[6] ? h[6] : 1), h[1] / (double)(h[6] ? h[6] : 1), h[2] / (double)(h[6] ? h[6] : 1),
+                                h[3] / (double)(h[6] ? h[6] : 1), (unsigned long long)h[6], h[5] / (double)(h[6] ? h[6] : 1),
+                                (unsigned long long)h[4], (unsigned long long)h[5]);
+                    if (geo.spec == 2)
+                        fprintf(stderr, "QS_DIAG run picks split (cumulative): loads %.0f chain %.0f rows %.0f\n",
+                                h[7] / (double)(h[6] ? h[6] : 1), h[8] / (double)(h[6] ? h[6] : 1), h[9] / (double)(h[6] ? h[6] : 1));
+                    else if (geo.spec)
                         fprintf(stderr, "QS_DIAG spec cycles/batch: phase1 %.0f phase2 %.0f phase3 %.0f; batches %llu (%.2f pods/batch, dirty wins %llu) pods %llu; prologue/window %.0f\n",
                                 h[0] / (double)(h[3] ? h[3] : 1), h[1] / (double)(h[3] ? h[3] : 1), h[2] / (double)(h[3] ? h[3] : 1),
                                 (unsigned long long)h[3], h[5] / (double)(h[3] ? h[3] : 1), (unsigned long long)h[4],

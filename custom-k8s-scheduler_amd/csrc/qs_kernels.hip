@@ -127,6 +127,16 @@ bool spec_resolver_fits(uint32_t n) {
     return std::max(spec_lds_bytes<kFeatExt>(n), spec_lds_bytes<kFeatExt | kFeatWide>(n)) <= 160 * 1024;
 }
 
+bool run_resolver_fits(uint32_t n) {
+    return std::max(run_lds_bytes<kFeatExt>(n), run_lds_bytes<kFeatExt | kFeatWide>(n)) <= 160 * 1024;
+}
+
+hipError_t run_prepare() {
+    QS_RET(run_prepare_f<0>());
+    QS_RET(run_prepare_f<kFeatExt>());
+    return wide_run_prepare();
+}
+
 hipError_t spec_prepare() {
     QS_RET(spec_prepare_f<0>());
     QS_RET(spec_prepare_f<kFeatExt>());

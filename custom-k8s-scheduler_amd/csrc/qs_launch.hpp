@@ -30,7 +30,9 @@ struct HostRow {
 // every shard has the same G/E/chunk and eplr = 2^lr entries per lane per pod; this process
 // selects shards [v0, v0 + nv) (nv = W for virtual shards in one process, 1 per rank with RCCL).
 // epl (total entries per resolver lane, power of two) >= W * eplr.
-// spec = 1: the speculative batch resolver (k_la_resolve_spec; non-normalizing profiles, W == 1).
+// spec = resolver variant for non-normalizing profiles on unsharded lists: 0 the four-wave
+// pipelined resolver, 1 the speculative batch resolver (k_la_resolve_spec), 2 the speculative-run
+// resolver (k_la_resolve_run: 32-bit keys, K <= 32).
 struct LaGeom {
     uint32_t K, L, G, E, chunk, epl, waves, k32;
     uint32_t W, v0, nv, eplr, lr;
@@ -77,6 +79,8 @@ struct LaBufs {
 // The speculative resolver keeps the dirty bitmap of the whole table in LDS (<= 64 KB here).
 bool spec_resolver_fits(uint32_t n);
 hipError_t spec_prepare();  // dynamic-LDS limit of the speculative resolver (call outside capture)
+bool run_resolver_fits(uint32_t n);
+hipError_t run_prepare();
 hipError_t launch_la_window(const DevTable &t, const void *pods, const DPodX *podx, uint32_t s0,
                             uint32_t P, const DevCfg &c, const LaGeom &geo, const LaBufs &bufs,
                             int32_t *out_node, uint64_t *out_key, uint64_t *stamps, uint64_t *diag,
