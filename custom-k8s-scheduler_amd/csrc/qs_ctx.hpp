@@ -127,6 +127,7 @@ struct qs_ctx {
     uint64_t device_faults = 0; // QS_EDEVICE results so far (each one drops the device table)
     qs_host::DevBuf diag;
     qs_host::DevBuf scratch, lists, clists, dio, npart, normi, nfall, nrec, bctrl, one_pod, one_podx, out_feas, out_score, out_total;
+    qs_host::DevBuf hand;  // window hand-off words: {epoch, ready, timeout flag} (u64 each)
     uint32_t cap = 0;
     // sharding (qs_open_shard): RCCL communicator of this rank, nullptr when unsharded
     int rank = 0, world = 1;

@@ -661,6 +661,7 @@ __global__ __launch_bounds__(64) void k_la_resolve(DevTable t, const PodT<F> *__
                                                    uint64_t *__restrict__ out_key,
                                                    uint64_t *__restrict__ stamps,
                                                    uint64_t *__restrict__ diag) {
+    wait_lists_ready(c, s0, K);
     uint64_t dsum[6] = {0, 0, 0, 0, 0, 0};
     uint64_t tprev = 0;
     extern __shared__ __attribute__((aligned(16))) uint32_t dirty[];
@@ -804,6 +805,7 @@ __global__ __launch_bounds__(64 * kResNormWaves) void k_la_resolve_norm(
     int32_t *__restrict__ out_node, uint64_t *__restrict__ out_key, uint64_t *__restrict__ stamps,
     const uint32_t *__restrict__ dprev, uint32_t *__restrict__ dcur, unsigned long long *nfall,
     const uint32_t *__restrict__ rec) {
+    if (!rec) wait_lists_ready(c, s0, K);  // resume mode follows the four-wave kernel on its stream
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     __shared__ uint32_t red_m[2 * kResNormWaves];  // per-wave rescan maxima (taint, affinity)
     __shared__ uint64_t red_k[kResNormWaves];      // per-wave rescan best keys
@@ -1479,6 +1481,7 @@ __global__ __launch_bounds__(256) void k_la_resolve4(DevTable t, const PodT<F> *
                                                      const DPodX *__restrict__ podx,
                                                      const NormInfo *__restrict__ norm,
                                                      uint32_t *__restrict__ rec) {
+    wait_lists_ready(c, s0, K);
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     la_resolve4_block<F, EPL, DIAG, K32>(lds, t, pods, c, s0, P, K, GLp, lr, sh, lists, out_node, out_key,
                                          stamps, diag, dprev, dcur, podx, norm, rec);
@@ -1520,6 +1523,7 @@ __global__ __launch_bounds__(64 * kSpecM) void k_la_resolve_spec(
     uint32_t GLp, const uint64_t *__restrict__ lists, int32_t *__restrict__ out_node,
     uint64_t *__restrict__ out_key, uint64_t *__restrict__ stamps, const uint32_t *__restrict__ dprev,
     uint32_t *__restrict__ dcur, uint64_t *__restrict__ diag) {
+    wait_lists_ready(c, s0, K);
     uint64_t dph[3] = {0, 0, 0}, dnb = 0, dfail = 0, tprev = 0;
     const uint64_t t_start = DIAG ? diag_stamp() : 0ull;
     using R = RowT<F>;
@@ -1869,6 +1873,7 @@ __global__ __launch_bounds__(64 * kRunWaves) void k_la_resolve_run(
     using PD = PodT<F>;
     using ST = RunStage<R>;
     constexpr bool EXT = (F & kFeatExt) != 0;
+    wait_lists_ready(c, s0, K);
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const int lane = threadIdx.x & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);

@@ -51,7 +51,7 @@ typedef enum qs_status {
     QS_OK = 0,
     QS_EINVAL = 1,   /* bad argument / input outside the device layout's range */
     QS_EDEVICE = 2,  /* HIP or RCCL failure (message in qs_last_error) */
-    QS_ETIMEOUT = 3, /* persistent-kernel spin bound hit */
+    QS_ETIMEOUT = 3, /* a resolver's in-kernel wait for its lookahead window's lists hit its ~2 s bound */
     QS_ENOMEM = 4,
     QS_ESTATE = 5 /* call out of order (e.g. no nodes loaded) */
 } qs_status;
