@@ -127,7 +127,9 @@ struct qs_ctx {
     uint64_t device_faults = 0; // QS_EDEVICE results so far (each one drops the device table)
     qs_host::DevBuf diag;
     qs_host::DevBuf scratch, lists, clists, dio, npart, normi, nfall, nrec, bctrl, one_pod, one_podx, out_feas, out_score, out_total;
-    qs_host::DevBuf hand;  // window hand-off words: {epoch, ready, timeout flag} (u64 each)
+    qs_host::DevBuf hand;  // window hand-off words: {unused, ready, timeout flag} (u64 each)
+    bool handoff_off = false;  // a hand-off timed out once: cross-stream events from then on
+    uint64_t run_seq = 0;      // lookahead runs of this context (the hand-off's epoch)
     uint32_t cap = 0;
     // sharding (qs_open_shard): RCCL communicator of this rank, nullptr when unsharded
     int rank = 0, world = 1;

@@ -91,24 +91,25 @@ struct DevCfg {
     uint32_t feat;               // kFeat* bits
     uint32_t ba_skip_be;         // balanced_skip_besteffort
     // Overlapped lookahead windows: the resolver of window w waits in-kernel for
-    // ready >= (epoch << 32 | w + 1), published by k_ready_set after window w's lists are complete,
-    // instead of a cross-stream event per window.  nullptr: no wait (the launch is ordered already).
+    // ready >= (epoch << 32 | w + 1), published by k_ready_set after window w's select chain,
+    // instead of a cross-stream event per window.  nullptr: no wait (the launch is ordered).
     const uint64_t *ready;
-    const uint64_t *epoch;
+    uint64_t epoch;  // the run's sequence number (host counter)
     uint32_t *werr;  // set to 1 when a wait times out (the run returns QS_ETIMEOUT)
 };
 
 // Resolver prologue: thread 0 spins (s_sleep) until window s0/K's lists are published, then every
-// thread proceeds.  Bounded: after ~2 s (s_memrealtime, 100 MHz) it records a timeout and returns.
+// thread proceeds.  Bounded: after 0.5 s (s_memrealtime, 100 MHz) it records a timeout; once one is
+// recorded no later resolver of the run waits (a profiler that serialises dispatches across streams
+// would otherwise cost the bound per window), and the run returns QS_ETIMEOUT.
 __device__ __forceinline__ void wait_lists_ready(const DevCfg &c, uint32_t s0, uint32_t K) {
     if (c.ready == nullptr) return;
-    if (threadIdx.x == 0) {
-        const uint64_t want = (__hip_atomic_load(c.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) << 32) |
-                              (uint64_t)(s0 / K + 1);
+    if (threadIdx.x == 0 && __hip_atomic_load(c.werr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+        const uint64_t want = (c.epoch << 32) | (uint64_t)(s0 / K + 1);
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         while (__hip_atomic_load(c.ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < want) {
             __builtin_amdgcn_s_sleep(1);
-            if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 50000000ull) {
                 __hip_atomic_store(c.werr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 break;
             }

@@ -489,7 +489,7 @@ qs_status guarded(qs_ctx *c, F &&f) {
         return QS_OK;
     } catch (const QsError &e) {
         c->err = e.msg;
-        if (e.st == QS_EDEVICE) {
+        if (e.st == QS_EDEVICE || e.st == QS_ETIMEOUT) {
             // failure recovery: the host mirror is authoritative — it is synced
             // after every stream, so it holds every placement the caller has been told about.
             // Drop the device table; the next call re-uploads it from the mirror.
@@ -1082,7 +1082,7 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                 // graph replay (and events), QS_HANDOFF=0 keeps events.
                 static const char *ho = getenv("QS_HANDOFF");
                 static const char *genv0 = getenv("QS_GRAPH");
-                const bool handoff_ok = overlap && !c->comm && !(ho && ho[0] == '0');
+                const bool handoff_ok = overlap && !c->comm && !c->handoff_off && !(ho && ho[0] == '0');
                 const bool graph_forced = genv0 && genv0[0] == '1';
                 const bool handoff = handoff_ok && !graph_forced;
                 if (!c->hand.p) {
@@ -1091,7 +1091,7 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                 }
                 uint64_t *hw = c->hand.as<uint64_t>();
                 c->dc.ready = handoff ? hw + 1 : nullptr;
-                c->dc.epoch = handoff ? hw : nullptr;
+                c->dc.epoch = handoff ? ++c->run_seq : 0;  // ready words of earlier runs compare lower
                 c->dc.werr = handoff ? reinterpret_cast<uint32_t *>(hw + 2) : nullptr;
                 uint64_t *L0 = c->lists.as<uint64_t>(), *C0 = c->clists.as<uint64_t>();
                 uint32_t *dio = c->dio.as<uint32_t>();
@@ -1130,7 +1130,7 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                     HIPCHK(launch_la_window(c->dt, dp, dx, w * geo.K, P, c->dc, geo, bf, on, ok, st, diag, ss, 1));
                     kt.end(2, ss);
                     if (c->comm) exchange_lists(c, bf.lists, rank_entries, ss);
-                    if (handoff) HIPCHK(launch_ready_set(hw + 1, hw, w, ss));
+                    if (handoff) HIPCHK(launch_ready_set(hw + 1, (c->dc.epoch << 32) | (w + 1), ss));
                 };
                 auto resolve = [&](uint32_t w) {
                     kt.begin(3, c->stream);
@@ -1156,10 +1156,7 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                         HIPCHK(hipEventCreateWithFlags(&eres[r], hipEventDisableTiming));
                     }
                     HIPCHK(hipEventCreateWithFlags(&est, hipEventDisableTiming));
-                    if (handoff) {
-                        HIPCHK(hipMemsetAsync(hw + 2, 0, 8, c->stream));
-                        HIPCHK(launch_epoch_bump(hw, c->stream));
-                    }
+                    if (handoff) HIPCHK(hipMemsetAsync(hw + 2, 0, 8, c->stream));
                     HIPCHK(hipEventRecord(est, c->stream));
                     HIPCHK(hipStreamWaitEvent(c->stream2, est, 0));
                     select(0, c->stream2);
@@ -1280,7 +1277,20 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
         if (eng == QS_ENGINE_LOOKAHEAD && c->dc.ready) {
             uint64_t w = 0;  // a resolver gave up waiting for its window's lists (device hand-off)
             HIPCHK(hipMemcpy(&w, c->hand.as<uint64_t>() + 2, 8, hipMemcpyDeviceToHost));
-            if (w) fail(QS_ETIMEOUT, "lookahead window hand-off timed out (lists never published)");
+            const char *inj = getenv("QS_INJECT_FAULT");  // test hook: a timed-out hand-off
+            if (inj && std::strcmp(inj, "handoff") == 0) {
+                unsetenv("QS_INJECT_FAULT");
+                w = 1;
+            }
+            if (w) {
+                // the select stream did not run beside the resolvers (e.g. a profiler serialising
+                // dispatches): this context uses cross-stream events from now on; the run's results
+                // and table updates are void and the device table is rebuilt from the host mirror
+                // (guarded(), as for a device fault)
+                c->handoff_off = true;
+                fail(QS_ETIMEOUT, "lookahead window hand-off timed out (lists never published); "
+                                  "the context falls back to stream events");
+            }
         }
         if (eng == QS_ENGINE_LOOKAHEAD && c->nfall.p) {
             uint64_t h[2] = {0, 0};

@@ -80,9 +80,9 @@ struct LaBufs {
 bool spec_resolver_fits(uint32_t n);
 hipError_t spec_prepare();  // dynamic-LDS limit of the speculative resolver (call outside capture)
 bool run_resolver_fits(uint32_t n);
-// In-kernel window hand-off (DevCfg::ready): advance the run epoch / publish window w's lists.
-hipError_t launch_epoch_bump(uint64_t *epoch, hipStream_t stream);
-hipError_t launch_ready_set(uint64_t *ready, const uint64_t *epoch, uint32_t w, hipStream_t stream);
+// In-kernel window hand-off (DevCfg::ready): publish a window's lists (value = run << 32 | w + 1).
+hipError_t launch_ready_set(uint64_t *ready, uint64_t value, hipStream_t stream);
+
 hipError_t run_prepare();
 hipError_t launch_la_window(const DevTable &t, const void *pods, const DPodX *podx, uint32_t s0,
                             uint32_t P, const DevCfg &c, const LaGeom &geo, const LaBufs &bufs,

@@ -84,3 +84,27 @@ def test_rejected_unreserve_leaves_table_unchanged():
         got = s.score_pod(pods[1])
     keys, _ = O.score_pod(nodes, pods_from_struct(pods), 1)
     assert got["best"] == int(0xFFFFFFFF - (int(keys.max()) & 0xFFFFFFFF))
+
+
+def test_handoff_timeout_falls_back_to_events(monkeypatch):
+    """A resolver that gives up waiting for its window's lists (the in-kernel hand-off, e.g. under
+    a profiler that serialises the two streams) makes the run return QS_ETIMEOUT; the device table
+    is rebuilt from the mirror and the context switches to cross-stream events, so re-running the
+    prepared stream gives the oracle's placements (hand-off timeout injected with QS_INJECT_FAULT)."""
+    nodes, pods = synth_generate(2, 1200, 4000)
+    with Scheduler({"engine": "lookahead"}) as s:
+        s.load_nodes(nodes)
+        before = s.read_nodes()
+        st = s.prepare(pods)
+        monkeypatch.setenv("QS_INJECT_FAULT", "handoff")
+        with pytest.raises(QschedError, match="QS_ETIMEOUT"):
+            st.run()
+        mid = s.read_nodes()
+        for k in before:
+            assert np.array_equal(mid[k], before[k]), k
+        st.run()
+        pl, keys = st.results()
+        st.free()
+    on = {k: v.copy() for k, v in nodes.items()}
+    o, ok, _ = O.schedule(on, pods_from_struct(pods), nthreads=16)
+    assert np.array_equal(pl, o) and np.array_equal(keys, ok)

@@ -9,14 +9,21 @@ export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 rm -rf $OUT; mkdir -p $OUT profiles
 ARGS="--steps 2 --warmup 1 --no-cpu --no-config3"
+PMC_ARGS="--steps 1 --warmup 1 --no-cpu --no-config3 --no-scan --no-extra"
+# heartbeat for the GPU pool's silence watchdog (counter passes print nothing for minutes)
+( while sleep 45; do date >> $OUT/heartbeat; done ) &
+HB=$!
+trap "kill $HB 2>/dev/null" EXIT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py $ARGS > $OUT/trace.log 2>&1
 echo "trace done"
-# counter passes replay the windows as individual launches (QS_GRAPH=0) with a host sync every 64
+# counter passes: cross-stream events (QS_HANDOFF=0: counter collection serialises dispatches, so a
+# resolver waiting in-kernel for the other stream's lists would time out), individual launches
+# (QS_GRAPH=0) and a host sync every 64
 # windows (QS_SYNC_EVERY): rocprofv3's counter collection crashed (SIGSEGV) with thousands of
 # dispatches in flight
-QS_GRAPH=0 QS_SYNC_EVERY=64 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o run --output-format csv -- python3 bench.py $ARGS > $OUT/fetch.log 2>&1
+QS_HANDOFF=0 QS_GRAPH=0 QS_SYNC_EVERY=64 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o run --output-format csv -- python3 bench.py $PMC_ARGS > $OUT/fetch.log 2>&1
 echo "fetch done"
-QS_GRAPH=0 QS_SYNC_EVERY=64 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o run --output-format csv -- python3 bench.py $ARGS > $OUT/write.log 2>&1
+QS_HANDOFF=0 QS_GRAPH=0 QS_SYNC_EVERY=64 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o run --output-format csv -- python3 bench.py $PMC_ARGS > $OUT/write.log 2>&1
 echo "write done"
 # configs 4 (normalizing lookahead) and 5 (batched): kernel-trace stats of their own streams
 for cfg in "4 5000 150000 exact 1" "5 10000 200000 batched 0"; do
