@@ -6,8 +6,9 @@ Workloads (BASELINE.json configs):
     The line also carries a ``config3`` object: the 50,000-node × 1,000,000-pod stream on the same
     single GPU, the N = 1 point of the config-3 scaling curve.
   * N > 1 (torchrun, one rank per GPU): configs[2] — 50,000 nodes × 1,000,000 pods with the node
-    table sharded across the N ranks (qs_open_shard: contiguous node ranges, one RCCL all-gather of
-    top-L lists per lookahead window over xGMI).  Total work is fixed: ``scaling`` = "strong".
+    table sharded across the N ranks (qs_open_shard: contiguous node ranges, one exchange of
+    top-L lists per lookahead window over xGMI: the peer-memory mailbox by default, an RCCL
+    all-gather with ``--transport rccl``).  Total work is fixed: ``scaling`` = "strong".
   ``--workload config2|config3`` overrides (config2 at N > 1 = independent replicas, weak scaling).
 
 A *step* = restore the empty cluster on the device (qs_table_restore, a D2D copy) + run the whole
@@ -38,7 +39,7 @@ WORKLOADS = {
     "config2": (2, 5000, 100000, "config2: 5,000 nodes x 100,000 pods, exact sequential, "
                                  "Fit+Balanced+QoS weights, percentageOfNodesToScore=100"),
     "config3": (3, 50000, 1000000, "config3: 50,000 nodes x 1,000,000 pods, exact sequential, "
-                                   "node table sharded across ranks (RCCL all-gather per window)"),
+                                   "node table sharded across ranks (list exchange per window)"),
     "config4": (4, 5000, 150000, "config4: 5,000 nodes x 150,000 pods, exact sequential, Fit + "
                                  "Balanced + TaintToleration + NodeAffinity + amd.com/gpu"),
     "config5": (5, 10000, 200000, "config5: 10,000 nodes x 200,000 pods, BATCHED mode (spec S11: "
@@ -68,6 +69,8 @@ def parse(argv=None):
     ap.add_argument("--no-scan", action="store_true", help="skip the HBM-resident scan roofline leg")
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the end-to-end, framework-path and wide-layout legs")
+    ap.add_argument("--transport", default="mailbox", choices=["mailbox", "rccl"],
+                    help="sharded exchange (N > 1): peer-memory mailbox over xGMI, or RCCL all-gather")
     ap.add_argument("--dry-run", action="store_true",
                     help="print the launch plan (torchrun argv for --gpus N > 1) and exit, no GPU touched")
     return ap.parse_args(argv)
@@ -102,6 +105,10 @@ class Ctx:
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        # QS_BENCH_ONE_GPU=1 (rehearsal on a one-GPU box, with QS_BENCH_BACKEND=gloo): every rank
+        # uses device 0, so the sharded mailbox path runs end to end as N processes on one card
+        if os.environ.get("QS_BENCH_ONE_GPU") == "1":
+            self.local = 0
         # "nccl" (= RCCL) on the GPU box; "gloo" rehearses the plumbing on CPU (tests/test_bench_launch.py)
         self.backend = backend or os.environ.get("QS_BENCH_BACKEND", "nccl")
         self.dev = f"cuda:{self.local}" if self.backend == "nccl" else "cpu"
@@ -139,8 +146,22 @@ class Ctx:
         return (self.rank, self.world, bytes(t.cpu().numpy().tolist()))
 
 
+TRANSPORT = {"name": "mailbox"}  # sharded exchange: peer-memory mailbox (default) or RCCL
+
+
 def open_sched(cx, cfg, sharded):
-    return qsched.Scheduler(cfg, device=cx.local, shard=cx.shard() if sharded else None)
+    """Sharded runs use the peer-memory mailbox (every rank exports its mailbox handle, the handles
+    are all-gathered over the process group) or, with --transport rccl, an RCCL communicator."""
+    if not sharded:
+        return qsched.Scheduler(cfg, device=cx.local)
+    if TRANSPORT["name"] == "rccl":
+        return qsched.Scheduler(cfg, device=cx.local, shard=cx.shard())
+    s = qsched.Scheduler(cfg, device=cx.local, shard=(cx.rank, cx.world, None))
+    h = s.mailbox_export()
+    allh = [None] * cx.world
+    cx.dist.all_gather_object(allh, h)
+    s.mailbox_connect(allh)
+    return s
 
 
 def diag_runs(cx, nodes, pods, cfg, sharded):
@@ -427,6 +448,7 @@ def framework_leg(cx, n_nodes=5000, n_pods=2000):
 def main():
     argv = sys.argv[1:]
     a = parse(argv)
+    TRANSPORT["name"] = a.transport
     plan = launch_plan(a, argv)
     if a.dry_run:
         print(json.dumps(plan), flush=True)
@@ -453,7 +475,8 @@ def main():
     if cx.rank == 0:
         rl = roofline(m["kp"], m["n_nodes"], m["n_pods"], m["wall_fallback"])
         if m["sharded"]:
-            par, scaling = f"node-sharded x{cx.world} (RCCL all-gather per window)", "strong"
+            how = "RCCL all-gather" if TRANSPORT["name"] == "rccl" else "peer-memory mailbox"
+            par, scaling = f"node-sharded x{cx.world} ({how} per window)", "strong"
         elif cx.world > 1:
             par, scaling = f"replicas x{cx.world}", "weak"
         else:

@@ -130,10 +130,17 @@ struct qs_ctx {
     qs_host::DevBuf hand;  // window hand-off words: {unused, ready, timeout flag} (u64 each)
     bool handoff_off = false;  // a hand-off timed out once: cross-stream events from then on
     uint64_t run_seq = 0;      // lookahead runs of this context (the hand-off's epoch)
+    bool last_waits = false;   // the last lookahead run waited on device words (hand-off / mailbox)
     uint32_t cap = 0;
     // sharding (qs_open_shard): RCCL communicator of this rank, nullptr when unsharded
     int rank = 0, world = 1;
     ncclComm_t comm = nullptr;
+    // peer-memory mailbox transport (qs_dist_mailbox_*): this rank's mailbox, the
+    // device array of every rank's mailbox base (peers mapped with hipIpcOpenMemHandle), on when
+    // connected
+    qs_host::DevBuf mbox, mbox_peers;
+    std::vector<void *> mbox_opened;
+    bool mbox_on = false;
 };
 
 namespace qs_host {
@@ -154,5 +161,27 @@ void exchange_lists(qs_ctx *c, uint64_t *lists, size_t per_rank_entries, hipStre
 void exchange_u32(qs_ctx *c, uint32_t *buf, size_t per_rank_words, hipStream_t stream);
 // {count, nodes[64]} dirty-set hand-off between overlapped lookahead windows (+ pad)
 constexpr size_t kDioWords = 68;
+// Mailbox layout (bytes from the base): flags [2 phases][16 ranks] u64 | lists [3 slots][16 ranks]
+// [64 pods][64] u64 | normalization partials [3 slots][16 ranks][4096] uint4.  Window w uses slot
+// w % 3: a rank writes window w+2 into a peer's slot only after seeing that peer's window-w+1
+// flags, by which time the peer's resolver of window w-1 (the slot's previous user) has finished.
+constexpr size_t kMbRanks = 16, kMbSlots = 3, kMbPartPerRank = 4096;
+constexpr size_t kMbFlags = 2 * kMbRanks * 8;
+constexpr size_t kMbListSlot = kMbRanks * 64 * 64 * 8;
+constexpr size_t kMbPartSlot = kMbRanks * kMbPartPerRank * 16;
+constexpr size_t kMbBytes = kMbFlags + kMbSlots * (kMbListSlot + kMbPartSlot);
+inline uint64_t *mbox_lists(qs_ctx *c, uint32_t slot) {
+    return reinterpret_cast<uint64_t *>(static_cast<char *>(c->mbox.p) + kMbFlags + slot * kMbListSlot);
+}
+inline uint4 *mbox_npart(qs_ctx *c, uint32_t slot) {
+    return reinterpret_cast<uint4 *>(static_cast<char *>(c->mbox.p) + kMbFlags + kMbSlots * kMbListSlot +
+                                     slot * kMbPartSlot);
+}
+// One mailbox exchange on `stream`: copy this rank's block of the slot region (phase 0: partials,
+// phase 1: lists; L > 0: lists of `pods` x 64 entries, entries >= L written as 0) into every peer's
+// mailbox, raise flag[phase][rank] = seq there, then wait until every rank's flag reaches seq in
+// this rank's mailbox (bounded; a timeout sets *werr).
+void mbox_exchange(qs_ctx *c, int phase, uint32_t slot, size_t block_bytes, uint32_t pods, uint32_t L,
+                   uint64_t seq, uint32_t *werr, hipStream_t stream);
 }  // namespace qs_host
 

@@ -38,6 +38,63 @@ void exchange_u32(qs_ctx *c, uint32_t *buf, size_t per_rank_words, hipStream_t s
                           c->comm, stream));
 }
 
+// ---- peer-memory mailbox: one hop per exchange instead of a ring ----------
+// Block p writes this rank's block into rank p's mailbox over xGMI (p == rank: only the zero
+// padding of its own lists), then publishes flag[phase][rank] = seq there with a system-scope
+// release after a system-scope fence, so a peer that observes the flag also observes the block.
+__global__ __launch_bounds__(256) void k_mbox_put(char *const *__restrict__ peers, uint32_t rank,
+                                                  size_t region, size_t block_bytes, uint32_t pods,
+                                                  uint32_t L, uint32_t phase, uint64_t seq) {
+    const uint32_t p = blockIdx.x;
+    char *dst = peers[p] + region + (size_t)rank * block_bytes;
+    const char *src = peers[rank] + region + (size_t)rank * block_bytes;
+    if (L > 0) {  // lists: pods x 64 entries, entries >= L are padding
+        uint64_t *d = reinterpret_cast<uint64_t *>(dst);
+        const uint64_t *q = reinterpret_cast<const uint64_t *>(src);
+        for (uint32_t i = threadIdx.x; i < pods * 64u; i += blockDim.x) {
+            const uint32_t e = i & 63u;
+            if (e >= L) d[i] = 0ull;
+            else if (p != rank) d[i] = q[i];
+        }
+    } else if (p != rank) {
+        uint4 *d = reinterpret_cast<uint4 *>(dst);
+        const uint4 *q = reinterpret_cast<const uint4 *>(src);
+        for (size_t i = threadIdx.x; i < block_bytes / 16; i += blockDim.x) d[i] = q[i];
+    }
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0)
+        __hip_atomic_store(reinterpret_cast<uint64_t *>(peers[p]) + phase * kMbRanks + rank, seq,
+                           __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Waits until every rank's flag[phase] in this rank's mailbox reaches seq (0.5 s bound: *werr = 1).
+__global__ void k_mbox_wait(const uint64_t *__restrict__ flags, uint32_t world, uint32_t phase, uint64_t seq,
+                            uint32_t *__restrict__ werr) {
+    if (threadIdx.x != 0) return;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (uint32_t r = 0; r < world; ++r)
+        while (__hip_atomic_load(flags + phase * kMbRanks + r, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < seq) {
+            __builtin_amdgcn_s_sleep(2);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 50000000ull) {
+                __hip_atomic_store(werr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                return;
+            }
+        }
+}
+
+void mbox_exchange(qs_ctx *c, int phase, uint32_t slot, size_t block_bytes, uint32_t pods, uint32_t L,
+                   uint64_t seq, uint32_t *werr, hipStream_t stream) {
+    const size_t region = phase == 1 ? kMbFlags + slot * kMbListSlot
+                                     : kMbFlags + kMbSlots * kMbListSlot + slot * kMbPartSlot;
+    hipLaunchKernelGGL(k_mbox_put, dim3(c->world), dim3(256), 0, stream, c->mbox_peers.as<char *>(),
+                       (uint32_t)c->rank, region, block_bytes, pods, L, (uint32_t)phase, seq);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_mbox_wait, dim3(1), dim3(64), 0, stream, c->mbox.as<uint64_t>(), (uint32_t)c->world,
+                       (uint32_t)phase, seq, werr);
+    HIPCHK(hipGetLastError());
+}
+
 }  // namespace qs_host
 
 extern "C" {
@@ -54,13 +111,14 @@ qs_status qs_dist_unique_id(uint8_t out[128]) {
 qs_status qs_open_shard(const qs_config *cfg, int device, int rank, int world,
                         const uint8_t nccl_id[128], qs_ctx **out) {
     if (!cfg || !out || world < 1 || world > 16 || rank < 0 || rank >= world) return QS_EINVAL;
-    if (world > 1 && !nccl_id) return QS_EINVAL;
     qs_status st = qs_open(cfg, device, out);
-    // world == 1 with an id still builds a (one-rank) communicator: the RCCL path on one GPU
-    if (st != QS_OK || !nccl_id) return st;
+    if (st != QS_OK) return st;
     qs_ctx *c = *out;
     c->rank = rank;
     c->world = world;
+    // no id: the peer-memory mailbox transport, connected with qs_dist_mailbox_export/_connect;
+    // world == 1 with an id still builds a (one-rank) communicator: the RCCL path on one GPU
+    if (!nccl_id) return QS_OK;
     ncclUniqueId id;
     std::memcpy(&id, nccl_id, sizeof id);
     ncclComm_t comm = nullptr;
@@ -72,6 +130,57 @@ qs_status qs_open_shard(const qs_config *cfg, int device, int rank, int world,
     }
     c->comm = comm;
     return QS_OK;
+}
+
+qs_status qs_dist_mailbox_export(qs_ctx *c, uint8_t handle[64]) {
+    if (!c || !handle) return QS_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    try {
+        HIPCHK(hipSetDevice(c->device));
+        if (!c->mbox.p) {
+            c->mbox.ensure(kMbBytes);
+            HIPCHK(hipMemset(c->mbox.p, 0, kMbBytes));
+            HIPCHK(hipDeviceSynchronize());
+        }
+        hipIpcMemHandle_t h;
+        static_assert(sizeof(h) == 64, "hipIpcMemHandle_t is 64 bytes");
+        HIPCHK(hipIpcGetMemHandle(&h, c->mbox.p));
+        std::memcpy(handle, &h, sizeof h);
+        return QS_OK;
+    } catch (const QsError &e) {
+        c->err = e.msg;
+        return e.st;
+    }
+}
+
+qs_status qs_dist_mailbox_connect(qs_ctx *c, const uint8_t *handles) {
+    if (!c || !handles) return QS_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    try {
+        if (!c->mbox.p) fail(QS_ESTATE, "qs_dist_mailbox_export first");
+        if (c->comm) fail(QS_ESTATE, "this context already uses RCCL");
+        HIPCHK(hipSetDevice(c->device));
+        std::vector<char *> bases((size_t)c->world);
+        for (int r = 0; r < c->world; ++r) {
+            if (r == c->rank) {
+                bases[(size_t)r] = static_cast<char *>(c->mbox.p);
+                continue;
+            }
+            hipIpcMemHandle_t h;
+            std::memcpy(&h, handles + 64 * (size_t)r, sizeof h);
+            void *p = nullptr;
+            HIPCHK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+            c->mbox_opened.push_back(p);
+            bases[(size_t)r] = static_cast<char *>(p);
+        }
+        c->mbox_peers.ensure(sizeof(char *) * bases.size());
+        HIPCHK(hipMemcpy(c->mbox_peers.p, bases.data(), sizeof(char *) * bases.size(), hipMemcpyHostToDevice));
+        c->mbox_on = true;
+        return QS_OK;
+    } catch (const QsError &e) {
+        c->err = e.msg;
+        return e.st;
+    }
 }
 
 }  // extern "C"

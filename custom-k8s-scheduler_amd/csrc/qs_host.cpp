@@ -756,6 +756,8 @@ qs_status qs_close(qs_ctx *c) {
         if (c->stream) (void)hipStreamSynchronize(c->stream);
         if (c->comm) (void)ncclCommDestroy(c->comm);
         c->comm = nullptr;
+        for (void *p : c->mbox_opened) (void)hipIpcCloseMemHandle(p);
+        c->mbox_opened.clear();
     }
     hipStream_t s = c->stream, s2 = c->stream2;
     if (s2) (void)hipStreamSynchronize(s2);
@@ -1027,6 +1029,11 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                 LaGeom geo = lookahead_geometry(c, n, overlap);
                 static const char *rw = getenv("QS_RESOLVER_WAVES");  // 1 = single-wave resolver
                 const bool norm = (c->dc.feat & (kFeatTaint | kFeatAffinity)) != 0;
+                // sharded transport: RCCL (c->comm) or the peer-memory mailbox (c->mbox_on)
+                const bool mbox = c->mbox_on && !c->comm;
+                if (c->world > 1 && !c->comm && !mbox)
+                    fail(QS_ESTATE, "sharded context without a transport: pass an RCCL id to qs_open_shard "
+                                    "or connect the mailbox (qs_dist_mailbox_connect)");
                 // normalizing profiles: k_la_norm pre-pass + the single-wave k_la_resolve_norm
                 geo.waves = norm || (rw && rw[0] == '1' && !overlap) ? 1u : 4u;
                 // normalizing profiles: the four-wave resolver with its stop/resume hand-off
@@ -1082,7 +1089,9 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                 // graph replay (and events), QS_HANDOFF=0 keeps events.
                 static const char *ho = getenv("QS_HANDOFF");
                 static const char *genv0 = getenv("QS_GRAPH");
-                const bool handoff_ok = overlap && !c->comm && !c->handoff_off && !(ho && ho[0] == '0');
+                // (not in profile_kernels runs: their per-launch events should bracket the
+                // resolver's own time, not an in-kernel wait)
+                const bool handoff_ok = overlap && !c->comm && !c->handoff_off && !kt.on && !(ho && ho[0] == '0');
                 const bool graph_forced = genv0 && genv0[0] == '1';
                 const bool handoff = handoff_ok && !graph_forced;
                 if (!c->hand.p) {
@@ -1091,7 +1100,13 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                 }
                 uint64_t *hw = c->hand.as<uint64_t>();
                 c->dc.ready = handoff ? hw + 1 : nullptr;
-                c->dc.epoch = handoff ? ++c->run_seq : 0;  // ready words of earlier runs compare lower
+                // the run's sequence number tags the hand-off and mailbox words (earlier runs compare
+                // lower; every rank of a sharded job runs the same streams, so the numbers agree)
+                const uint64_t seq_run = (handoff || mbox) ? ++c->run_seq : 0;
+                c->dc.epoch = handoff ? seq_run : 0;
+                c->last_waits = handoff || mbox;
+                if (mbox && (uint64_t)geo.K * geo.G > kMbPartPerRank)
+                    fail(QS_EINVAL, "mailbox transport: K*G exceeds the mailbox partials capacity");
                 c->dc.werr = handoff ? reinterpret_cast<uint32_t *>(hw + 2) : nullptr;
                 uint64_t *L0 = c->lists.as<uint64_t>(), *C0 = c->clists.as<uint64_t>();
                 uint32_t *dio = c->dio.as<uint32_t>();
@@ -1112,6 +1127,10 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                               c->normi.as<NormInfo>() + (size_t)b * geo.K, nullptr, nullptr,
                               c->nfall.as<unsigned long long>()};
                     bf.rec = c->nrec.as<uint32_t>();
+                    if (mbox) {  // lists and partials live in this rank's mailbox, slot w % 3
+                        bf.lists = mbox_lists(c, w % 3);
+                        bf.npart = mbox_npart(c, w % 3);
+                    }
                     if (overlap) {
                         bf.dprev = dio + ((w + 1) & 1) * kDioWords;
                         bf.dcur = dio + (w & 1) * kDioWords;
@@ -1123,13 +1142,16 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                 auto select = [&](uint32_t w, hipStream_t ss) {
                     const LaBufs bf = bufs(w);
                     kt.begin(2, ss);
+                    uint32_t *werr = reinterpret_cast<uint32_t *>(hw + 2);
                     if (norm) {
                         HIPCHK(launch_la_window(c->dt, dp, dx, w * geo.K, P, c->dc, geo, bf, on, ok, st, diag, ss, 4));
                         if (c->comm) exchange_u32(c, (uint32_t *)bf.npart, 4 * (size_t)geo.K * geo.G, ss);
+                        else if (mbox) mbox_exchange(c, 0, w % 3, 16 * (size_t)geo.K * geo.G, 0, 0, (seq_run << 32) | (w + 1), werr, ss);
                     }
                     HIPCHK(launch_la_window(c->dt, dp, dx, w * geo.K, P, c->dc, geo, bf, on, ok, st, diag, ss, 1));
                     kt.end(2, ss);
                     if (c->comm) exchange_lists(c, bf.lists, rank_entries, ss);
+                    else if (mbox) mbox_exchange(c, 1, w % 3, 8 * rank_entries, geo.K, geo.L, (seq_run << 32) | (w + 1), werr, ss);
                     if (handoff) HIPCHK(launch_ready_set(hw + 1, (c->dc.epoch << 32) | (w + 1), ss));
                 };
                 auto resolve = [&](uint32_t w) {
@@ -1156,7 +1178,7 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                         HIPCHK(hipEventCreateWithFlags(&eres[r], hipEventDisableTiming));
                     }
                     HIPCHK(hipEventCreateWithFlags(&est, hipEventDisableTiming));
-                    if (handoff) HIPCHK(hipMemsetAsync(hw + 2, 0, 8, c->stream));
+                    if (handoff || mbox) HIPCHK(hipMemsetAsync(hw + 2, 0, 8, c->stream));
                     HIPCHK(hipEventRecord(est, c->stream));
                     HIPCHK(hipStreamWaitEvent(c->stream2, est, 0));
                     select(0, c->stream2);
@@ -1197,7 +1219,7 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                 // across ranks have not been observed on this pool yet; QS_GRAPH=1
                 // forces capture for them.
                 const bool graph_ok = !c->comm || (genv && genv[0] == '1');
-                const bool use_graph = graph_ok && !handoff && !kt.on && !diag_on && !(genv && genv[0] == '0');
+                const bool use_graph = graph_ok && !handoff && !mbox && !kt.on && !diag_on && !(genv && genv[0] == '0');
                 if (use_graph) {
                     std::vector<uint8_t> key;
                     auto put = [&](const void *p, size_t nb) {
@@ -1274,7 +1296,7 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
         (void)hipEventDestroy(e0);
         (void)hipEventDestroy(e1);
         uint64_t rescans = 0, resumed = 0;
-        if (eng == QS_ENGINE_LOOKAHEAD && c->dc.ready) {
+        if (eng == QS_ENGINE_LOOKAHEAD && c->last_waits) {
             uint64_t w = 0;  // a resolver gave up waiting for its window's lists (device hand-off)
             HIPCHK(hipMemcpy(&w, c->hand.as<uint64_t>() + 2, 8, hipMemcpyDeviceToHost));
             const char *inj = getenv("QS_INJECT_FAULT");  // test hook: a timed-out hand-off
@@ -1284,12 +1306,13 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
             }
             if (w) {
                 // the select stream did not run beside the resolvers (e.g. a profiler serialising
-                // dispatches): this context uses cross-stream events from now on; the run's results
-                // and table updates are void and the device table is rebuilt from the host mirror
-                // (guarded(), as for a device fault)
-                c->handoff_off = true;
-                fail(QS_ETIMEOUT, "lookahead window hand-off timed out (lists never published); "
-                                  "the context falls back to stream events");
+                // dispatches), or a mailbox peer never posted: the run's results and table updates
+                // are void and the device table is rebuilt from the host mirror (guarded(), as for
+                // a device fault); an unsharded context uses cross-stream events from now on
+                if (!c->mbox_on) c->handoff_off = true;
+                fail(QS_ETIMEOUT, c->mbox_on ? "mailbox exchange timed out (a peer never posted its window)"
+                                             : "lookahead window hand-off timed out (lists never published); "
+                                               "the context falls back to stream events");
             }
         }
         if (eng == QS_ENGINE_LOOKAHEAD && c->nfall.p) {

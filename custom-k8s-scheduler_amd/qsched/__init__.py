@@ -110,7 +110,8 @@ class Scheduler:
 
     def __init__(self, config=None, device: int = 0, shard=None):
         """shard = (rank, world, unique_id bytes) opens a node-sharded context (qs_open_shard):
-        every rank loads the same full table and pod stream; RCCL exchanges the per-window lists."""
+        every rank loads the same full table and pod stream; RCCL exchanges the per-window lists.
+        unique_id None: the peer-memory mailbox transport (mailbox_export / mailbox_connect)."""
         self.lib = load()
         self.cfg = Config(config or {}).to_c()
         ctx = ctypes.c_void_p()
@@ -125,6 +126,19 @@ class Scheduler:
             raise QschedError(st, "qs_open failed (no HIP device?)")
         self.ctx = ctx
         self.n = 0
+
+    def mailbox_export(self) -> bytes:
+        """qs_dist_mailbox_export: this rank's 64-byte mailbox IPC handle (sharded contexts opened
+        without an RCCL id)."""
+        buf = (ctypes.c_uint8 * 64)()
+        self._chk(self.lib.qs_dist_mailbox_export(self.ctx, buf))
+        return bytes(buf)
+
+    def mailbox_connect(self, handles):
+        """qs_dist_mailbox_connect with every rank's handle, in rank order."""
+        blob = b"".join(bytes(h) for h in handles)
+        buf = (ctypes.c_uint8 * len(blob)).from_buffer_copy(blob)
+        self._chk(self.lib.qs_dist_mailbox_connect(self.ctx, buf))
 
     def close(self):
         if getattr(self, "ctx", None):

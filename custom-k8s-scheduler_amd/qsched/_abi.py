@@ -123,6 +123,8 @@ _SIGS = {
     "qs_open": (ctypes.c_int, [_P, ctypes.c_int, _P]),
     "qs_open_shard": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, _P]),
     "qs_dist_unique_id": (ctypes.c_int, [_P]),
+    "qs_dist_mailbox_export": (ctypes.c_int, [_P, _P]),
+    "qs_dist_mailbox_connect": (ctypes.c_int, [_P, _P]),
     "qs_close": (ctypes.c_int, [_P]),
     "qs_last_error": (ctypes.c_char_p, [_P]),
     "qs_version": (ctypes.c_char_p, []),

@@ -177,7 +177,8 @@ typedef struct qs_stream qs_stream;
 QS_API void qs_config_default(qs_config *cfg);
 QS_API qs_status qs_open(const qs_config *cfg, int device, qs_ctx **out);
 /* Sharded context for one rank of `world` (one process per GPU, world <= 16).  nccl_id = 128 bytes
- * from qs_dist_unique_id on rank 0, broadcast by the caller (any out-of-band channel).  Every rank
+ * from qs_dist_unique_id on rank 0, broadcast by the caller (any out-of-band channel); NULL selects
+ * the peer-memory mailbox transport instead (qs_dist_mailbox_connect before the first stream).  Every rank
  * loads the SAME full node table (qs_nodes_load) and the SAME pod stream; rank r scores only its
  * contiguous node shard [r*n/world, (r+1)*n/world), the per-window top-L lists are exchanged with
  * one RCCL all-gather over xGMI, and every rank resolves the window identically, so placements and
@@ -186,6 +187,17 @@ QS_API qs_status qs_open(const qs_config *cfg, int device, qs_ctx **out);
 QS_API qs_status qs_open_shard(const qs_config *cfg, int device, int rank, int world,
                         const uint8_t nccl_id[128], qs_ctx **out);
 QS_API qs_status qs_dist_unique_id(uint8_t out[128]);
+/* Peer-memory mailbox transport, the alternative to RCCL: open
+ * every rank with qs_open_shard(..., nccl_id = NULL, ...), call qs_dist_mailbox_export on each rank
+ * (allocates this rank's ~5 MB mailbox and returns its 64-byte IPC handle), exchange the handles
+ * out of band, and call qs_dist_mailbox_connect with all `world` handles in rank order.  Per
+ * lookahead window every rank then writes its list block (and, for TaintToleration/NodeAffinity
+ * profiles, its partial maxima) straight into every peer's mailbox over xGMI and raises a flag
+ * there (one hop), instead of an RCCL all-gather; a peer that never posts makes the run return
+ * QS_ETIMEOUT after 0.5 s.  All ranks must run the same streams in the same order.
+ * Replaces (with qs_open_shard) the per-pod ncclAllReduce exchange of SURVEY.md §8(e). */
+QS_API qs_status qs_dist_mailbox_export(qs_ctx *ctx, uint8_t handle[64]);
+QS_API qs_status qs_dist_mailbox_connect(qs_ctx *ctx, const uint8_t *handles /* world x 64 bytes */);
 QS_API qs_status qs_close(qs_ctx *ctx);
 QS_API const char *qs_last_error(const qs_ctx *ctx);
 QS_API const char *qs_version(void);
