@@ -129,6 +129,10 @@ struct qs_ctx {
     qs_host::DevBuf scratch, lists, clists, dio, npart, normi, nfall, nrec, bctrl, one_pod, one_podx, out_feas, out_score, out_total;
     qs_host::DevBuf hand;  // window hand-off words: {unused, ready, timeout flag} (u64 each)
     bool handoff_off = false;  // a hand-off timed out once: cross-stream events from then on
+    qs_host::DevBuf resctl;    // resident stream's hand-off counters
+    bool resident_off = false; // a resident stream timed out once: per-window launches from then on
+    bool last_resident = false;  // the last lookahead run was a resident stream
+    int cus = 0;               // compute units of the device (resident stream's selector count)
     uint64_t run_seq = 0;      // lookahead runs of this context (the hand-off's epoch)
     bool last_waits = false;   // the last lookahead run waited on device words (hand-off / mailbox)
     uint32_t cap = 0;

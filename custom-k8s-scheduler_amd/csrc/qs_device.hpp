@@ -271,6 +271,60 @@ __device__ __forceinline__ void store_dynx(const DevTable &t, uint32_t i, const 
         w[3] = x.re1;
     }
 }
+// ---- in-launch hand-off forms of the resident stream -------------------------
+// Per MI355X_MICROARCH.md § inter-workgroup visibility (valid forms, row 1): every handed-off byte
+// is stored write-through (sc1) and read with sc1 loads to registers, so neither side needs an L2
+// write-back or an L1 invalidate.  Only compact rows (DRow) are handed off this way.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) uint64_t gu64;
+typedef __attribute__((address_space(1))) uint32_t gu32;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const DevTable &t) {
+    return __builtin_amdgcn_make_buffer_rsrc((void *)t.rows, (short)0, (int)(t.n * sizeof(DRow)), 0x00020000);
+}
+__device__ __forceinline__ uint64_t load_coh_u64(const uint64_t *p) {
+    return __hip_atomic_load((gu64 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void store_coh_u64(uint64_t *p, uint64_t v) {
+    __hip_atomic_store((gu64 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t load_coh_u32(const uint32_t *p) {
+    return __hip_atomic_load((gu32 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Every storing wave drains its sc1 stores before the workgroup barrier that precedes a signal.
+__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// A compact row whose dynamic quads (q0 = ac am rc rm, q1 = zc zm np mp, q3 = extended) another
+// workgroup writes during the launch: those quads by sc1 loads, the static reciprocals plainly.
+template <uint32_t F>
+__device__ __forceinline__ Row load_row_coh(const DevTable &t, __amdgpu_buffer_rsrc_t rs, uint32_t i, RowX &x) {
+    static_assert((F & kFeatWide) == 0, "compact rows only");
+    const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(i * sizeof(DRow)), 0, 16);
+    const u32x4 b = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(i * sizeof(DRow) + 16), 0, 16);
+    const double2 y = reinterpret_cast<const double2 *>(t.rows + i)[2];
+    Row r;
+    r.ac = (int32_t)a.x; r.am = (int32_t)a.y; r.rc = (int32_t)a.z; r.rm = (int32_t)a.w;
+    r.zc = (int32_t)b.x; r.zm = (int32_t)b.y; r.np = (int32_t)b.z; r.mp = (int32_t)b.w;
+    r.yc = y.x; r.ym = y.y;
+    x = RowX{};
+    if (F & kFeatExt) {
+        const u32x4 e = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(i * sizeof(DRow) + 48), 0, 16);
+        x.ae0 = (int32_t)e.x; x.re0 = (int32_t)e.y; x.ae1 = (int32_t)e.z; x.re1 = (int32_t)e.w;
+    }
+    return r;
+}
+template <uint32_t F>
+__device__ __forceinline__ void store_row_coh(const DevTable &t, __amdgpu_buffer_rsrc_t rs, uint32_t i, const Row &r,
+                                              const RowX &x) {
+    (void)t;
+    const u32x4 a = {(uint32_t)r.ac, (uint32_t)r.am, (uint32_t)r.rc, (uint32_t)r.rm};
+    const u32x4 b = {(uint32_t)r.zc, (uint32_t)r.zm, (uint32_t)r.np, (uint32_t)r.mp};
+    __builtin_amdgcn_raw_buffer_store_b128(a, rs, (int)(i * sizeof(DRow)), 0, 16);
+    __builtin_amdgcn_raw_buffer_store_b128(b, rs, (int)(i * sizeof(DRow) + 16), 0, 16);
+    if (F & kFeatExt) {
+        const u32x4 e = {(uint32_t)x.ae0, (uint32_t)x.re0, (uint32_t)x.ae1, (uint32_t)x.re1};
+        __builtin_amdgcn_raw_buffer_store_b128(e, rs, (int)(i * sizeof(DRow) + 48), 0, 16);
+    }
+}
+
 // Reserve (spec S7; UP framework/types.go#NodeInfo.update(+1))
 template <class R, class P>
 __device__ __forceinline__ void reserve(R &r, RowX &x, const P &p, int sign) {

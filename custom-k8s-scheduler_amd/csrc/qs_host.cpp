@@ -1220,7 +1220,37 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                 // forces capture for them.
                 const bool graph_ok = !c->comm || (genv && genv[0] == '1');
                 const bool use_graph = graph_ok && !handoff && !mbox && !kt.on && !diag_on && !(genv && genv[0] == '0');
-                if (use_graph) {
+                // Resident stream: the whole overlapped window sequence of an
+                // unsharded Fit + Balanced (+ extended) stream as ONE launch (resolver + selector
+                // workgroups handing off inside it); QS_RESIDENT=0 keeps per-window launches.
+                static const char *renv = getenv("QS_RESIDENT");
+                const bool resident = overlap && !norm && !c->comm && !mbox && c->world == 1 && !c->resident_off &&
+                                      !kt.on && !diag_on && !c->wide && !(renv && renv[0] == '0') &&
+                                      la_stream_res_supported(geo, c->dc.feat, n);
+                c->last_resident = resident;
+                if (resident) {
+                    c->resctl.ensure(la_stream_res_ctl_bytes());
+                    if (!c->cus) {
+                        int cu = 0;
+                        HIPCHK(hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, c->device));
+                        c->cus = cu;
+                    }
+                    c->dc.ready = nullptr;
+                    c->dc.epoch = 0;
+                    c->dc.werr = reinterpret_cast<uint32_t *>(hw + 2);
+                    c->last_waits = true;
+                    HIPCHK(hipMemsetAsync(c->lists.p, 0, 8 * lwords * nbuf, c->stream));  // padding stays 0
+                    HIPCHK(hipMemsetAsync(c->dio.p, 0, 2 * kDioWords * 4, c->stream));
+                    HIPCHK(hipMemsetAsync(c->resctl.p, 0, la_stream_res_ctl_bytes(), c->stream));
+                    HIPCHK(hipMemsetAsync(hw + 2, 0, 8, c->stream));
+                    // one selector workgroup per (pod, chunk) task of a window, at most one per
+                    // remaining CU (they loop over the tasks otherwise); QS_RES_SEL overrides
+                    static const char *senv = getenv("QS_RES_SEL");
+                    uint32_t sel = std::max(1u, std::min(geo.K * geo.G, (uint32_t)std::max(2, c->cus) - 1u));
+                    if (senv && atoi(senv) > 0) sel = (uint32_t)atoi(senv);
+                    HIPCHK(launch_la_stream_res(c->dt, dp, c->dc, P, geo, L0, C0, (uint32_t)lwords, (uint32_t)cwords,
+                                                dio, on, ok, st, c->resctl.p, sel, c->stream));
+                } else if (use_graph) {
                     std::vector<uint8_t> key;
                     auto put = [&](const void *p, size_t nb) {
                         key.insert(key.end(), (const uint8_t *)p, (const uint8_t *)p + nb);
@@ -1309,10 +1339,14 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                 // dispatches), or a mailbox peer never posted: the run's results and table updates
                 // are void and the device table is rebuilt from the host mirror (guarded(), as for
                 // a device fault); an unsharded context uses cross-stream events from now on
-                if (!c->mbox_on) c->handoff_off = true;
+                if (c->last_resident) c->resident_off = true;
+                else if (!c->mbox_on) c->handoff_off = true;
                 fail(QS_ETIMEOUT, c->mbox_on ? "mailbox exchange timed out (a peer never posted its window)"
-                                             : "lookahead window hand-off timed out (lists never published); "
-                                               "the context falls back to stream events");
+                                             : c->last_resident
+                                                   ? "resident lookahead stream timed out (a hand-off never arrived); "
+                                                     "the context falls back to per-window launches"
+                                                   : "lookahead window hand-off timed out (lists never published); "
+                                                     "the context falls back to stream events");
             }
         }
         if (eng == QS_ENGINE_LOOKAHEAD && c->nfall.p) {

@@ -167,6 +167,24 @@ hipError_t launch_la_window(const DevTable &t, const void *pods, const DPodX *po
     return la_window_f<0>(t, pods, podx, s0, P, c, geo, bf, on, ok, st, diag, stream, part);
 }
 
+bool la_stream_res_supported(const LaGeom &geo, uint32_t feat, uint32_t n) {
+    return (feat == 0 || feat == kFeatExt) && geo.W == 1 && geo.nv == 1 && geo.epl == 1 && geo.waves == 4 &&
+           geo.spec == 0 && (uint64_t)n * sizeof(DRow) < (1ull << 31) && la_stream_res_geometry(geo);
+}
+size_t la_stream_res_ctl_bytes() { return kResCtlBytes; }
+
+hipError_t launch_la_stream_res(const DevTable &t, const void *pods, const DevCfg &c, uint32_t P, const LaGeom &geo,
+                                uint64_t *lists0, uint64_t *clists0, uint32_t lwords, uint32_t cwords, uint32_t *dio,
+                                int32_t *on, uint64_t *ok, uint64_t *st, void *ctl, uint32_t sel_blocks,
+                                hipStream_t stream) {
+    if (t.wrows || !la_stream_res_supported(geo, c.feat, t.n)) return hipErrorInvalidValue;
+    if (c.feat & kFeatExt)
+        return la_stream_res_f<kFeatExt>(t, pods, c, P, geo, lists0, clists0, lwords, cwords, dio, on, ok, st, ctl,
+                                         sel_blocks, stream);
+    return la_stream_res_f<0>(t, pods, c, P, geo, lists0, clists0, lwords, cwords, dio, on, ok, st, ctl, sel_blocks,
+                              stream);
+}
+
 LaGeom la_geometry(uint32_t n, uint32_t K, uint32_t W, uint32_t L) {
     // Per shard (W shards of <= ceil(n/W) nodes; W = 1 unsharded): G node chunks of `chunk` nodes
     // per pod (E nodes per lane of a 256-thread select block; about 1,280 nodes by default, env

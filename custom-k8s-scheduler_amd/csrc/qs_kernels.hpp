@@ -622,6 +622,12 @@ __global__ __launch_bounds__(256) void k_la_merge(const uint64_t *__restrict__ c
 // Entry m (0 <= m < EPL) of resolver lane `lane` for window pod `pod`.  Lists are laid out
 // [shard][pod][GLp] (GLp = 64 * 2^lr entries per pod and shard: the all-gathered layout of the
 // sharded engine); entries of shards >= W read as empty.
+// Address of entry m of lane `lane` (the entry must exist: m >> lr < W).
+__device__ __forceinline__ const uint64_t &list_ref(const uint64_t *lists, uint32_t pod, uint32_t GLp, uint32_t lr,
+                                                   const LaShard &sh, int m, int lane) {
+    const uint32_t q = (uint32_t)m >> lr;
+    return lists[(size_t)q * sh.RS + (size_t)pod * GLp + (uint32_t)lane + 64u * ((uint32_t)m & ((1u << lr) - 1u))];
+}
 __device__ __forceinline__ uint64_t list_ent(const uint64_t *__restrict__ lists, uint32_t pod,
                                              uint32_t GLp, uint32_t lr, const LaShard &sh, int m,
                                              int lane) {
@@ -1078,7 +1084,7 @@ __device__ __forceinline__ ResPub read_pub(const ResPub *p) {
     return r;
 }
 
-template <uint32_t F, int EPL, bool DIAG, bool K32>
+template <uint32_t F, int EPL, bool DIAG, bool K32, bool RES = false>
 __device__ __forceinline__ void la_resolve4_block(uint32_t *lds, const DevTable &t, const PodT<F> *__restrict__ pods,
                                                   const DevCfg &c, uint32_t s0, uint32_t P,
                                                   uint32_t K, uint32_t GLp, uint32_t lr,
@@ -1347,8 +1353,12 @@ __device__ __forceinline__ void la_resolve4_block(uint32_t *lds, const DevTable 
         __syncthreads();  // slotnode written by wave D
         if (wv == 1 && (uint32_t)lane < nd) {
             const uint32_t node = slotnode[lane];
-            store_dyn<F>(t, node, S);
-            store_dynx<F>(t, node, SX);
+            if constexpr (RES) {  // resident stream: the selectors read these rows in this launch
+                store_row_coh<F>(t, row_rsrc(t), node, S, SX);
+            } else {
+                store_dyn<F>(t, node, S);
+                store_dynx<F>(t, node, SX);
+            }
         }
     } else {
         // ---- C: candidate rows, C keys, next pod's top-2 ------------------------------------
@@ -1371,7 +1381,12 @@ __device__ __forceinline__ void la_resolve4_block(uint32_t *lds, const DevTable 
         };
         auto load_ent = [&](uint64_t(&e)[EPL], uint32_t pod) {
 #pragma unroll
-            for (int m = 0; m < EPL; ++m) e[m] = pod < kend ? list_ent(lists, pod, GLp, lr, sh, m, lane) : 0ull;
+            for (int m = 0; m < EPL; ++m) {
+                if constexpr (RES)  // resident stream: lists handed off inside the launch (sc1 loads)
+                    e[m] = pod < kend ? load_coh_u64(&list_ref(lists, pod, GLp, lr, sh, m, lane)) : 0ull;
+                else
+                    e[m] = pod < kend ? list_ent(lists, pod, GLp, lr, sh, m, lane) : 0ull;
+            }
         };
         uint64_t c1, c2;
         uint64_t eX[EPL], eY[EPL];  // ping-pong: entries consumed two pods after their load
@@ -1486,6 +1501,197 @@ __global__ __launch_bounds__(256) void k_la_resolve4(DevTable t, const PodT<F> *
     la_resolve4_block<F, EPL, DIAG, K32>(lds, t, pods, c, s0, P, K, GLp, lr, sh, lists, out_node, out_key,
                                          stamps, diag, dprev, dcur, podx, norm, rec);
 }
+
+// =============================================================================================
+// Resident lookahead stream: the whole window sequence of an unsharded,
+// non-normalizing stream in ONE launch.  Block 0 runs the four-wave resolver (la_resolve4_block)
+// over every window; blocks 1..S are selectors that loop over each window's (pod, chunk) tasks and
+// merge a pod's chunk lists in whichever selector delivers its last chunk.  Nothing per window goes
+// through the host, an event, a kernel boundary or a cache write-back / invalidate: the three
+// in-launch hand-offs use the form MI355X_MICROARCH.md § inter-workgroup visibility lists as valid
+// (row 1: every handed-off byte stored write-through `sc1`, every storing wave drained, a workgroup
+// barrier, ONE lane signals with an agent-scope atomic; the consumer polls relaxed and reads every
+// handed-off byte with `sc1` loads):
+//   resolver -> selectors   dynamic row quads of window w's slots (16-B sc1)   done = w + 1
+//   selector -> merger      the chunk's top-L list (8-B sc1)                    ticket[w&1][k] += 1
+//   merger   -> resolver    the pod's sorted final list (8-B sc1)               rdy[w&1] += 1
+// Selects of window w read the table as it stood after window w-2 (overlapped windows, §4.1 item
+// 4), so a selector waits for done >= w-1; lists, chunk lists and tickets are double-buffered by
+// window parity and window w+2 reuses them only after done >= w+1.  Every wait is bounded: on a
+// timeout the waiter raises werr, every other wait gives up when it sees werr, and the host voids
+// the run (QS_ETIMEOUT).  Placements are those of the launched windows (same kernels' arithmetic).
+// =============================================================================================
+struct ResCtl {                // zeroed before every launch; each counter on its own 128-B line
+    uint32_t done, pad0[31];   // windows resolved
+    uint32_t rdy[2][32];       // pods merged, per window parity
+    uint32_t ticket[2][64];    // chunk lists delivered, per window parity and window pod
+};
+// Bounded relaxed poll by one lane: true once *p >= want; false on werr or after 0.5 s (100 MHz).
+__device__ __forceinline__ bool res_wait_ge(const uint32_t *p, uint32_t want, uint32_t *werr) {
+    if (load_coh_u32(p) >= want) return true;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        __builtin_amdgcn_s_sleep(1);
+        if (load_coh_u32(p) >= want) return true;
+        if (load_coh_u32(werr) != 0u) return false;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 50000000ull) {
+            __hip_atomic_store((gu32 *)werr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return false;
+        }
+    }
+}
+__device__ __forceinline__ uint32_t res_add(uint32_t *p) {
+    return __hip_atomic_fetch_add((gu32 *)p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Wave 0 sorts a pod's list (LDS, L <= 64 entries) best-first into its final slot; then the block
+// signals the resolver (every storing wave drained, barrier, one lane adds).
+__device__ __forceinline__ void res_publish_list(const uint64_t *lbuf, uint32_t L, uint64_t *out, uint32_t *rdy) {
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        uint64_t v = (uint32_t)lane < L ? lbuf[lane] : 0ull;
+        v = wave_sort_desc(v, lane);
+        if ((uint32_t)lane < L) store_coh_u64(out + lane, v);
+        drain_stores();
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) res_add(rdy);
+}
+
+template <int E, int E2, uint32_t F>
+__device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *__restrict__ pods, const DevCfg &c,
+                                             uint32_t P, uint32_t K, uint32_t G, uint32_t L, uint32_t chunk,
+                                             uint32_t nwin, uint64_t *lists0, uint64_t *clists0, uint32_t lwords,
+                                             uint32_t cwords, ResCtl *ctl, uint32_t sid, uint32_t S) {
+    __shared__ uint64_t lbuf[64];
+    __shared__ uint32_t okflag_[4];  // (16 B: keeps the dynamic-LDS base 16-byte aligned)
+    uint32_t &okflag = okflag_[0];
+    const int tid = threadIdx.x, lane = tid & 63, w8 = tid >> 6;
+    const __amdgpu_buffer_rsrc_t rs = row_rsrc(t);
+    const DPodX px{};
+    for (uint32_t w = 0; w < nwin; ++w) {
+        const uint32_t s0 = w * K, kw = min(K, P - s0), b = w & 1;
+        if (sid >= kw * G) continue;  // no task of this window (uniform per block)
+        if (w >= 2) {  // the table after window w-2, and this parity's buffers free again
+            if (tid == 0) okflag = res_wait_ge(&ctl->done, w - 1, c.werr) ? 1u : 0u;
+            __syncthreads();
+            if (!okflag) return;
+        }
+        uint64_t *lists = lists0 + (size_t)b * lwords;
+        uint64_t *clists = clists0 + (size_t)b * cwords;
+        for (uint32_t task = sid; task < kw * G; task += S) {
+            const uint32_t k = task / G, g = task % G;
+            const PodT<F> p = pods[s0 + k];
+            const uint32_t start = g * chunk, end = min(t.n, start + chunk);
+            const uint32_t base = start + (uint32_t)w8 * E * kWave + lane;
+            uint32_t tv[E];
+#pragma unroll
+            for (int j = 0; j < E; ++j) {
+                const uint32_t idx = base + j * kWave;
+                tv[j] = 0;
+                if (idx < end) {
+                    RowX x;
+                    const Row r = load_row_coh<F>(t, rs, idx, x);
+                    const bool f = feasible<F>(r, x, p, px);
+                    const uint32_t tot = node_total<F>(r, x, p, px, c, 0, 0.0, 0, 0.0, nullptr);
+                    tv[j] = f ? tot + 1 : 0;
+                }
+            }
+            block_topl<256, E>(tv, L, lbuf, [&](int j) { return pack_key(tv[j], base + j * kWave); });
+            __syncthreads();  // lbuf complete
+            uint64_t *out = lists + (size_t)k * 64;
+            if (G == 1) {
+                res_publish_list(lbuf, L, out, &ctl->rdy[b][0]);
+            } else {
+                uint64_t *cl = clists + (size_t)k * G * L;
+                if ((uint32_t)tid < L) store_coh_u64(cl + (size_t)g * L + tid, lbuf[tid]);
+                drain_stores();
+                __syncthreads();
+                if (tid == 0) okflag = (res_add(&ctl->ticket[b][k]) + 1) % G == 0 ? 1u : 0u;
+                __syncthreads();
+                if (okflag) {  // this block delivered pod k's last chunk: merge (k_la_merge's routine)
+                    const uint32_t M = G * L;
+                    uint64_t e[E2];
+                    uint32_t te[E2];
+#pragma unroll
+                    for (int j = 0; j < E2; ++j) {
+                        const uint32_t pos = (uint32_t)w8 * E2 * kWave + (uint32_t)j * kWave + lane;
+                        e[j] = pos < M ? load_coh_u64(cl + pos) : 0ull;
+                        te[j] = (uint32_t)(e[j] >> 32);
+                    }
+                    __syncthreads();  // every wave is done reading lbuf
+                    block_topl<256, E2>(te, L, lbuf, [&](int j) { return e[j]; });
+                    __syncthreads();
+                    res_publish_list(lbuf, L, out, &ctl->rdy[b][0]);
+                }
+            }
+            __syncthreads();  // lbuf / okflag reused by the next task
+        }
+    }
+}
+
+template <uint32_t F, int E, int E2, bool K32>
+__global__ __launch_bounds__(256) void k_la_stream_res(DevTable t, const PodT<F> *__restrict__ pods, DevCfg c,
+                                                       uint32_t P, uint32_t K, uint32_t G, uint32_t L,
+                                                       uint32_t chunk, uint32_t nwin, uint64_t *lists0,
+                                                       uint64_t *clists0, uint32_t lwords, uint32_t cwords,
+                                                       uint32_t *dio, int32_t *__restrict__ out_node,
+                                                       uint64_t *__restrict__ out_key,
+                                                       uint64_t *__restrict__ stamps, ResCtl *ctl) {
+    if (blockIdx.x != 0) {
+        res_selector<E, E2, F>(t, pods, c, P, K, G, L, chunk, nwin, lists0, clists0, lwords, cwords, ctl,
+                               blockIdx.x - 1, gridDim.x - 1);
+        return;
+    }
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    __shared__ uint32_t okr_[4];
+    uint32_t &okr = okr_[0];
+    const LaShard sh{1u, 0u, K, 0u, (uint64_t)K * 64};
+    for (uint32_t w = 0; w < nwin; ++w) {
+        const uint32_t s0 = w * K, kw = min(K, P - s0), b = w & 1;
+        if (threadIdx.x == 0) okr = res_wait_ge(&ctl->rdy[b][0], (w >> 1) * K + kw, c.werr) ? 1u : 0u;
+        __syncthreads();
+        if (!okr) return;
+        la_resolve4_block<F, 1, false, K32, true>(lds, t, pods, c, s0, P, K, 64, 0, sh, lists0 + (size_t)b * lwords,
+                                                  out_node, out_key, stamps, nullptr,
+                                                  dio + ((w + 1) & 1) * 68, dio + (w & 1) * 68);
+        drain_stores();  // every wave: its row / dcur stores
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_store((gu32 *)&ctl->done, w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+template <uint32_t F>
+static hipError_t la_stream_res_f(const DevTable &t, const void *pods, const DevCfg &c, uint32_t P, const LaGeom &geo,
+                                  uint64_t *lists0, uint64_t *clists0, uint32_t lwords, uint32_t cwords, uint32_t *dio,
+                                  int32_t *on, uint64_t *ok, uint64_t *st, void *ctl, uint32_t sel_blocks,
+                                  hipStream_t stream) {
+    const uint32_t K = geo.K, G = geo.G, L = geo.L, nwin = (P + K - 1) / K;
+    const uint32_t E2 = (G * L + 255) / 256;
+    const size_t bm = (((t.n + 31) / 32 + 3) & ~3u) * 4;
+    const size_t lds4 = bm + 5 * 2 * 64 * 8 + 2 * 64 * (sizeof(RowT<F>) + sizeof(int4)) + 2 * sizeof(ResPub) + 64 * 4 +
+                        64 * sizeof(PodT<F>);
+    const dim3 grid(1 + sel_blocks);
+    const PodT<F> *pp = (const PodT<F> *)pods;
+    ResCtl *rc = (ResCtl *)ctl;
+#define QS_RESK(EE, EE2, KK)                                                                                          \
+    hipLaunchKernelGGL((k_la_stream_res<F, EE, EE2, KK>), grid, dim3(256), lds4, stream, t, pp, c, P, K, G, L,       \
+                       geo.chunk, nwin, lists0, clists0, lwords, cwords, dio, on, ok, st, rc)
+    if (geo.E == 5 && E2 == 1) {
+        if (geo.k32) QS_RESK(5, 1, true); else QS_RESK(5, 1, false);
+    } else if (geo.E == 8 && E2 == 7) {
+        if (geo.k32) QS_RESK(8, 7, true); else QS_RESK(8, 7, false);
+    } else {
+        return hipErrorInvalidValue;
+    }
+#undef QS_RESK
+    return hipGetLastError();
+}
+// Geometries with a resident-stream instantiation (the host falls back to per-window launches).
+inline bool la_stream_res_geometry(const LaGeom &geo) {
+    const uint32_t E2 = (geo.G * geo.L + 255) / 256;
+    return (geo.E == 5 && E2 == 1) || (geo.E == 8 && E2 == 7);
+}
+constexpr size_t kResCtlBytes = sizeof(ResCtl);
 
 // =============================================================================================
 // Speculative batch resolver: Fit + Balanced (+ extended resources) profiles,

@@ -83,6 +83,18 @@ bool run_resolver_fits(uint32_t n);
 // In-kernel window hand-off (DevCfg::ready): publish a window's lists (value = run << 32 | w + 1).
 hipError_t launch_ready_set(uint64_t *ready, uint64_t value, hipStream_t stream);
 
+// Resident lookahead stream: the whole overlapped window sequence of an
+// unsharded Fit + Balanced (+ extended) stream as ONE launch of 1 resolver + sel_blocks selector
+// workgroups; ctl = la_stream_res_ctl_bytes() of device memory, zeroed before every launch, and
+// c.werr the timeout word.  lists0 / clists0 / dio: the double-buffered window buffers of the
+// per-window path (lwords / cwords per parity).
+bool la_stream_res_supported(const LaGeom &geo, uint32_t feat, uint32_t n);
+size_t la_stream_res_ctl_bytes();
+hipError_t launch_la_stream_res(const DevTable &t, const void *pods, const DevCfg &c, uint32_t P, const LaGeom &geo,
+                                uint64_t *lists0, uint64_t *clists0, uint32_t lwords, uint32_t cwords, uint32_t *dio,
+                                int32_t *on, uint64_t *ok, uint64_t *st, void *ctl, uint32_t sel_blocks,
+                                hipStream_t stream);
+
 hipError_t run_prepare();
 hipError_t launch_la_window(const DevTable &t, const void *pods, const DPodX *podx, uint32_t s0,
                             uint32_t P, const DevCfg &c, const LaGeom &geo, const LaBufs &bufs,
