@@ -51,7 +51,7 @@ PROFILE = {"config4": {"enable_taint": 1, "enable_affinity": 1}}  # plugin switc
 B_NODE = 32  # algorithmic bytes per pod×node evaluation (8 int32 columns)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md:36 (spec); 6,290 GB/s measured
 KERNEL_NAMES = {"resolve": "k_la_resolve4", "select": "k_la_select", "persistent": "k_persistent",
-                "scan": "k_scan_key"}
+                "scan": "k_scan_key", "stream": "k_la_stream_res"}
 
 
 def parse(argv=None):
@@ -179,7 +179,10 @@ def diag_runs(cx, nodes, pods, cfg, sharded):
     s3 = open_sched(cx, dict(cfg, profile_kernels=1), sharded)
     s3.load_nodes(nodes)
     st3 = s3.prepare(pods)
-    kp = st3.run()["kernels"]
+    r3 = st3.run()
+    kp = r3["kernels"]
+    if r3.get("resident") and "resolve" in kp:  # one resident launch
+        kp = {"stream": kp["resolve"]}
     st3.free()
     s3.close()
     return p50, p99, kp
@@ -293,6 +296,7 @@ def measure(cx, a, workload, steps, warmup, with_diag=True):
     ranks_work = cx.world if (cx.world > 1 and not sharded) else 1  # replicas multiply the work
     value = n_pods * steps * ranks_work / elapsed
     out = {"value": value, "ms_per_step": elapsed / steps * 1e3, "engine": last["engine_used"],
+           "launch": "resident" if last.get("resident") else "per-window",
            "table_layout": last["table_layout"],
            "unschedulable_frac": float((placement < 0).mean()), "n_nodes": n_nodes,
            "placement": placement.copy(),
@@ -488,7 +492,8 @@ def main():
             "warmup": a.warmup, "ms_per_step": round(m["ms_per_step"], 3), "higher_is_better": True,
             "scaling": scaling, "vs_baseline": None, "dtype": "int32+f64",
             "data": f"synthetic (spec/synth.md generator, config {WORKLOADS[workload][0]})",
-            "config": {"workload": m["desc"], "engine": m["engine"], "table_layout": m["table_layout"],
+            "config": {"workload": m["desc"], "engine": m["engine"], "launch": m["launch"],
+                       "table_layout": m["table_layout"],
                        "lookahead": a.lookahead or 32, "parallelism": par},
             "evals_per_s": round(m["value"] * m["n_nodes"], 1),
             "p50_pod_latency_us": round(m["p50"], 4), "p99_pod_latency_us": round(m["p99"], 4),
@@ -501,12 +506,12 @@ def main():
                               "value": round(c3["value"], 1), "unit": "pods/s",
                               "evals_per_s": round(c3["value"] * c3["n_nodes"], 1),
                               "ms_per_step": round(c3["ms_per_step"], 3), "steps": 1,
-                              "engine": c3["engine"]}
+                              "engine": c3["engine"], "launch": c3["launch"]}
         if c4 is not None:
             out["config4"] = {"workload": c4["desc"], "value": round(c4["value"], 1), "unit": "pods/s",
                               "evals_per_s": round(c4["value"] * c4["n_nodes"], 1),
                               "ms_per_step": round(c4["ms_per_step"], 3), "steps": 3,
-                              "engine": c4["engine"],
+                              "engine": c4["engine"], "launch": c4["launch"],
                               "unschedulable_frac": round(c4["unschedulable_frac"], 5)}
         if c5 is not None:
             out["config5_batched"] = {"workload": c5["desc"], "value": round(c5["value"], 1),

@@ -1223,18 +1223,18 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                 // Resident stream: the whole overlapped window sequence of an
                 // unsharded Fit + Balanced (+ extended) stream as ONE launch (resolver + selector
                 // workgroups handing off inside it); QS_RESIDENT=0 keeps per-window launches.
-                static const char *renv = getenv("QS_RESIDENT");
+                const char *renv = getenv("QS_RESIDENT");  // read per run (tests switch it per case)
+                if (!c->cus) {
+                    int cu = 0;
+                    HIPCHK(hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, c->device));
+                    c->cus = cu;
+                }
+                const LaGeom rgeo = la_stream_res_plan(geo, c->dc.feat, n, (uint32_t)c->cus);
                 const bool resident = overlap && !norm && !c->comm && !mbox && c->world == 1 && !c->resident_off &&
-                                      !kt.on && !diag_on && !c->wide && !(renv && renv[0] == '0') &&
-                                      la_stream_res_supported(geo, c->dc.feat, n);
+                                      !diag_on && !c->wide && !(renv && renv[0] == '0') && rgeo.G > 0;
                 c->last_resident = resident;
                 if (resident) {
                     c->resctl.ensure(la_stream_res_ctl_bytes());
-                    if (!c->cus) {
-                        int cu = 0;
-                        HIPCHK(hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, c->device));
-                        c->cus = cu;
-                    }
                     c->dc.ready = nullptr;
                     c->dc.epoch = 0;
                     c->dc.werr = reinterpret_cast<uint32_t *>(hw + 2);
@@ -1246,10 +1246,28 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                     // one selector workgroup per (pod, chunk) task of a window, at most one per
                     // remaining CU (they loop over the tasks otherwise); QS_RES_SEL overrides
                     static const char *senv = getenv("QS_RES_SEL");
-                    uint32_t sel = std::max(1u, std::min(geo.K * geo.G, (uint32_t)std::max(2, c->cus) - 1u));
+                    uint32_t sel = rgeo.K * rgeo.G;
                     if (senv && atoi(senv) > 0) sel = (uint32_t)atoi(senv);
-                    HIPCHK(launch_la_stream_res(c->dt, dp, c->dc, P, geo, L0, C0, (uint32_t)lwords, (uint32_t)cwords,
-                                                dio, on, ok, st, c->resctl.p, sel, c->stream));
+                    // QS_RES_DIAG=1: the resolver's time split (list waits / window bodies / between)
+                    static const bool rdiag_on = getenv("QS_RES_DIAG") && getenv("QS_RES_DIAG")[0] == '1';
+                    uint64_t *rdiag = nullptr;
+                    if (rdiag_on) {
+                        c->diag.ensure(256);
+                        rdiag = c->diag.as<uint64_t>();
+                        HIPCHK(hipMemsetAsync(rdiag, 0, 256, c->stream));
+                    }
+                    kt.begin(3, c->stream);  // the one launch, under "resolve"
+                    HIPCHK(launch_la_stream_res(c->dt, dp, c->dc, P, rgeo, L0, C0, (uint32_t)lwords, (uint32_t)cwords,
+                                                dio, on, ok, st, c->resctl.p, sel, rdiag, c->stream));
+                    kt.end(3, c->stream);
+                    if (rdiag) {
+                        uint64_t h[32] = {0};
+                        HIPCHK(hipMemcpyAsync(h, rdiag, 256, hipMemcpyDeviceToHost, c->stream));
+                        HIPCHK(hipStreamSynchronize(c->stream));
+                        const double nw = h[3] ? (double)h[3] : 1.0;
+                        fprintf(stderr, "QS_RES_DIAG resolver %.3f us per window; windows whose lists were not prefetched %llu of %llu (selectors %u)\n",
+                                h[1] * 0.01 / nw, (unsigned long long)h[4], (unsigned long long)h[3], sel);
+                    }
                 } else if (use_graph) {
                     std::vector<uint8_t> key;
                     auto put = [&](const void *p, size_t nb) {
@@ -1380,6 +1398,7 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
             stats->engine_used = eng;
             stats->table_layout = c->wide ? 1 : 0;
             stats->resumed_windows = resumed;
+            stats->resident = (eng == QS_ENGINE_LOOKAHEAD && c->last_resident) ? 1 : 0;
             stats->device_faults = c->device_faults;
         }
     });

@@ -167,22 +167,43 @@ hipError_t launch_la_window(const DevTable &t, const void *pods, const DPodX *po
     return la_window_f<0>(t, pods, podx, s0, P, c, geo, bf, on, ok, st, diag, stream, part);
 }
 
-bool la_stream_res_supported(const LaGeom &geo, uint32_t feat, uint32_t n) {
-    return (feat == 0 || feat == kFeatExt) && geo.W == 1 && geo.nv == 1 && geo.epl == 1 && geo.waves == 4 &&
-           geo.spec == 0 && (uint64_t)n * sizeof(DRow) < (1ull << 31) && la_stream_res_geometry(geo);
+// Resident-stream geometry: every (pod, chunk) task of a window gets its own selector workgroup
+// (K * G <= cus - 1, G <= 8 so a merge reads <= 512 keys), chunks of E * 256 nodes with E from
+// the instantiated set; G = 0 when the table is too large or the profile / layout is not covered.
+LaGeom la_stream_res_plan(const LaGeom &geo, uint32_t feat, uint32_t n, uint32_t cus) {
+    LaGeom r = geo;
+    r.G = 0;
+    if (!((feat == 0 || feat == kFeatExt) && geo.W == 1 && geo.nv == 1 && geo.epl == 1 && geo.waves == 4 &&
+          geo.spec == 0 && geo.L <= 64 && n > 0 && cus > geo.K))
+        return r;
+    const uint32_t gmax = std::min(8u, (cus - 1) / geo.K);
+    if (gmax == 0) return r;
+    constexpr uint32_t bs = kResBS;  // threads of a selector workgroup
+    const uint32_t G0 = std::min(gmax, (n + 5 * bs - 1) / (5 * bs));
+    const uint32_t e_need = ((n + G0 - 1) / G0 + bs - 1) / bs;
+    uint32_t E = 0;
+    for (uint32_t e : {3u, 5u, 8u, 16u})
+        if (e >= e_need) { E = e; break; }
+    if (E == 0) return r;  // more than 8 chunks of 8,192 nodes: per-window launches
+    const uint32_t G = (n + E * bs - 1) / (E * bs);
+    if (G * geo.L > bs) return r;
+    r.E = E;
+    r.chunk = E * bs;
+    r.G = G;
+    return r;
 }
 size_t la_stream_res_ctl_bytes() { return kResCtlBytes; }
 
 hipError_t launch_la_stream_res(const DevTable &t, const void *pods, const DevCfg &c, uint32_t P, const LaGeom &geo,
                                 uint64_t *lists0, uint64_t *clists0, uint32_t lwords, uint32_t cwords, uint32_t *dio,
                                 int32_t *on, uint64_t *ok, uint64_t *st, void *ctl, uint32_t sel_blocks,
-                                hipStream_t stream) {
-    if (t.wrows || !la_stream_res_supported(geo, c.feat, t.n)) return hipErrorInvalidValue;
+                                uint64_t *rdiag, hipStream_t stream) {
+    if (t.wrows || geo.G == 0 || (uint64_t)t.n * sizeof(DRow) >= (1ull << 31)) return hipErrorInvalidValue;
     if (c.feat & kFeatExt)
         return la_stream_res_f<kFeatExt>(t, pods, c, P, geo, lists0, clists0, lwords, cwords, dio, on, ok, st, ctl,
-                                         sel_blocks, stream);
+                                         sel_blocks, rdiag, stream);
     return la_stream_res_f<0>(t, pods, c, P, geo, lists0, clists0, lwords, cwords, dio, on, ok, st, ctl, sel_blocks,
-                              stream);
+                              rdiag, stream);
 }
 
 LaGeom la_geometry(uint32_t n, uint32_t K, uint32_t W, uint32_t L) {

@@ -1521,6 +1521,9 @@ __global__ __launch_bounds__(256) void k_la_resolve4(DevTable t, const PodT<F> *
 // timeout the waiter raises werr, every other wait gives up when it sees werr, and the host voids
 // the run (QS_ETIMEOUT).  Placements are those of the launched windows (same kernels' arithmetic).
 // =============================================================================================
+// Workgroup size of the resident stream: selectors score with eight waves; the resolver workgroup
+// runs its four pipeline waves and parks the other four at the same barriers.
+constexpr int kResBS = 512;
 struct ResCtl {                // zeroed before every launch; each counter on its own 128-B line
     uint32_t done, pad0[31];   // windows resolved
     uint32_t rdy[2][32];       // pods merged, per window parity
@@ -1596,7 +1599,7 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
                     tv[j] = f ? tot + 1 : 0;
                 }
             }
-            block_topl<256, E>(tv, L, lbuf, [&](int j) { return pack_key(tv[j], base + j * kWave); });
+            block_topl<kResBS, E>(tv, L, lbuf, [&](int j) { return pack_key(tv[j], base + j * kWave); });
             __syncthreads();  // lbuf complete
             uint64_t *out = lists + (size_t)k * 64;
             if (G == 1) {
@@ -1619,7 +1622,7 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
                         te[j] = (uint32_t)(e[j] >> 32);
                     }
                     __syncthreads();  // every wave is done reading lbuf
-                    block_topl<256, E2>(te, L, lbuf, [&](int j) { return e[j]; });
+                    block_topl<kResBS, E2>(te, L, lbuf, [&](int j) { return e[j]; });
                     __syncthreads();
                     res_publish_list(lbuf, L, out, &ctl->rdy[b][0]);
                 }
@@ -1629,67 +1632,374 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
     }
 }
 
+// Resident four-wave resolver: la_resolve4_block's pipeline (non-normalizing profiles, one list
+// entry per lane) run over every window of the stream without leaving the kernel.  Nothing crosses
+// a window boundary through global memory: the slots won in window w (window w+1's inherited dirty
+// set, §4.1 item 4) are compacted in place through LDS (rows stay on chip), dropped slots' dirty
+// bits are cleared, wave D loads window w+1's pod records at the start of window w, and wave C
+// polls window w+1's lists five pods before the end of window w and prefetches the entries of its
+// first three pods and the candidate rows of its first pod.  Wave A stores the rows won in window
+// w write-through and, two pods into window w+1 (long drained by then), signals done = w + 1.
+// Per window and wave: one prologue barrier, one barrier per pod, two boundary barriers.
+template <uint32_t F>
+constexpr size_t res_stream_lds_bytes(uint32_t n) {
+    return ((((size_t)n + 31) / 32 + 3) & ~(size_t)3) * 4 + 4 * 2 * 64 * 8 + 2 * 64 * (sizeof(RowT<F>) + sizeof(int4)) +
+           2 * sizeof(ResPub) + 3 * 64 * 4 + 64 * (sizeof(RowT<F>) + sizeof(int4)) + 2 * 64 * sizeof(PodT<F>);
+}
+template <uint32_t F, bool K32>
+__device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable &t, const PodT<F> *__restrict__ pods,
+                                                   const DevCfg &c, uint32_t P, uint32_t K, uint32_t nwin,
+                                                   const uint64_t *lists0, uint32_t lwords,
+                                                   int32_t *__restrict__ out_node, uint64_t *__restrict__ out_key,
+                                                   uint64_t *__restrict__ stamps, ResCtl *ctl, uint64_t *rdiag) {
+    static_assert((F & (kFeatNorm | kFeatWide)) == 0, "compact, non-normalizing profiles");
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t nwords = (t.n + 31) / 32;
+    uint32_t *dirty = lds;
+    char *base = (char *)(lds + ((nwords + 3) & ~3u));
+    uint64_t(*keyA)[64] = (uint64_t(*)[64])base; base += 2 * 64 * 8;
+    uint64_t(*keyB)[64] = (uint64_t(*)[64])base; base += 2 * 64 * 8;
+    uint64_t(*keyC)[64] = (uint64_t(*)[64])base; base += 2 * 64 * 8;
+    uint64_t(*C1)[64] = (uint64_t(*)[64])base; base += 2 * 64 * 8;
+    RowT<F>(*stage)[64] = (RowT<F>(*)[64])base; base += 2 * 64 * sizeof(RowT<F>);
+    int4(*stagex)[64] = (int4(*)[64])base; base += 2 * 64 * sizeof(int4);
+    ResPub *pub = (ResPub *)base; base += 2 * sizeof(ResPub);
+    uint32_t *xrank = (uint32_t *)base; base += 64 * 4;  // slot lane -> rank among the window's won slots, or ~0
+    uint32_t *xnode = (uint32_t *)base; base += 64 * 4;  // slot lane -> node
+    uint32_t *dnode = (uint32_t *)base; base += 64 * 4;  // rank -> node
+    RowT<F> *carry = (RowT<F> *)base; base += 64 * sizeof(RowT<F>);
+    int4 *carryx = (int4 *)base; base += 64 * sizeof(int4);
+    PodT<F>(*wpods2)[64] = (PodT<F>(*)[64])base;  // window pod records, by window parity
+    const ResPub none{0, 0xFFFFFFFFu, -1, -1, 0, {0, 0}};
+    const DPodX px{};
+
+    for (uint32_t i = threadIdx.x; i < nwords; i += 256) dirty[i] = 0;
+    if (threadIdx.x < min(K, P)) wpods2[0][threadIdx.x] = pods[threadIdx.x];
+    if (threadIdx.x == 0) pub[1] = none;
+    __syncthreads();
+
+    if (wv == 0) {
+        // ---- D: pod i's winner from the precomputed keys (la_resolve4_block's wave D) -----------
+        uint32_t nd = 0, didx = 0xFFFFFFFFu;
+        bool won = false;  // slot won a pod of the current window (it stays a slot in the next one)
+        for (uint32_t w = 0; w < nwin; ++w) {
+            const uint32_t s0 = w * K, kend = min(K, P - s0);
+            const uint32_t knext = w + 1 < nwin ? min(K, P - s0 - K) : 0u;
+            // next window's pod records (to LDS at the end; loaded unconditionally, clamped, so the
+            // loads stay in flight through the window instead of being waited for at a branch join)
+            static_assert(sizeof(PodT<F>) == 32, "two 16-byte quads per pod record");
+            const int4 *pq = reinterpret_cast<const int4 *>(pods + min(s0 + K + (uint32_t)lane, P - 1));
+            const int4 npa = pq[0], npb = pq[1];
+            uint64_t res_key = 0, res_stamp = 0;
+            ResPub pv = none;
+            __syncthreads();  // B1
+            for (uint32_t i = 0; i < kend; ++i) {
+                const int par = i & 1, pp = par ^ 1;
+                const uint64_t a = keyA[pp][lane], b = keyB[pp][lane], cl = keyC[pp][lane];
+                const uint64_t e1 = C1[pp][lane];
+                const bool pnew = pv.ks != 0 && pv.slot < 0;
+                const uint64_t sc = (lane == pv.slot) ? b : a;
+                uint64_t fk = ((uint32_t)lane < nd && sc) ? (sc | (uint64_t)(0xFFFFFFFFu - didx)) : 0ull;
+                if (pnew) {
+                    const uint64_t cw = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(cl >> 32), pv.src) << 32) |
+                                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)cl, pv.src);
+                    if ((uint32_t)lane == pv.nd_old) fk = cw;
+                }
+                const uint64_t cand = (pv.ks != 0 && e1 != 0 && key_node(e1) == pv.w) ? 0ull : e1;
+                const uint64_t best = fk > cand ? fk : cand;
+                uint64_t ks;
+                if (K32) {  // (score+1) < 2^10 and n <= 2^22: one 32-bit reduction
+                    const uint32_t tv = (uint32_t)(best >> 32);
+                    const uint32_t k32 = tv ? (tv << 22) | (0x3FFFFFu - key_node(best)) : 0u;
+                    const uint32_t m = wave_max_u32(k32);
+                    ks = m ? (((uint64_t)(m >> 22) << 32) | (uint64_t)(0xFFFFFFFFu - (0x3FFFFFu - (m & 0x3FFFFFu)))) : 0ull;
+                } else {
+                    ks = wave_max_u64(best);
+                }
+                ResPub np{ks, ks ? key_node(ks) : 0xFFFFFFFFu, -1, -1, nd, {0, 0}};
+                if (ks) {
+                    const uint64_t own = __ballot((uint32_t)lane < nd && didx == np.w);
+                    if (own) {
+                        np.slot = (int32_t)__builtin_ctzll(own);
+                        won |= lane == np.slot;
+                    } else {
+                        np.src = (int32_t)__builtin_ctzll(__ballot(cand == ks));
+                        if ((uint32_t)lane == nd) { didx = np.w; won = true; }
+                        ++nd;
+                    }
+                }
+                pv = np;
+                if (lane == 0) pub[par] = np;
+                if ((uint32_t)lane == i) {
+                    res_key = ks;
+                    if (stamps) res_stamp = __builtin_amdgcn_s_memrealtime();
+                }
+                __syncthreads();
+            }
+            if ((uint32_t)lane < kend) {
+                out_node[s0 + lane] = res_key ? (int32_t)key_node(res_key) : -1;
+                if (out_key) out_key[s0 + lane] = res_key;
+                if (stamps) stamps[s0 + lane] = res_stamp;
+            }
+            // boundary: the won slots become the next window's inherited slots (rank order), the
+            // others are clean again for the next window's lists (selected after this window's
+            // predecessor was resolved)
+            const bool act = (uint32_t)lane < nd;
+            const uint64_t wm = __ballot(act && won);
+            const uint32_t rk = (uint32_t)__popcll(wm & ((1ull << lane) - 1ull));
+            xrank[lane] = (act && won) ? rk : 0xFFFFFFFFu;
+            xnode[lane] = didx;
+            if (act && won) {
+                dnode[rk] = didx;
+                // (wave C marks new slots one pod late: the window's last winner is marked here)
+                __hip_atomic_fetch_or(&dirty[didx >> 5], 1u << (didx & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            if (act && !won)
+                __hip_atomic_fetch_and(&dirty[didx >> 5], ~(1u << (didx & 31)), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+            if ((uint32_t)lane < knext) {
+                int4 *dq = reinterpret_cast<int4 *>(&wpods2[(w + 1) & 1][lane]);
+                dq[0] = npa;
+                dq[1] = npb;
+            }
+            __syncthreads();  // B2
+            __syncthreads();  // B3 (wave A stored and staged the won rows)
+            nd = (uint32_t)__popcll(wm);
+            didx = (uint32_t)lane < nd ? dnode[lane] : 0xFFFFFFFFu;
+            won = false;
+            if (lane == 0) pub[1] = none;
+        }
+    } else if (wv <= 2) {
+        // ---- A / B: slot rows; apply pod i-1's winner, then the next pod's keys -----------------
+        RowT<F> S = empty_row<F>();
+        RowX SX{};
+        uint32_t nd = 0;
+        uint32_t pend = 0;  // wave A: windows whose rows are stored but not yet signalled (done value)
+        const __amdgpu_buffer_rsrc_t rs = row_rsrc(t);
+        auto slot_key = [&](const RowT<F> &r, const RowX &x, const PodT<F> &q) -> uint64_t {
+            const bool f = feasible<F>(r, x, q, px);
+            const uint32_t tot = node_total<F>(r, x, q, px, c, 0, 0.0, 0, 0.0, nullptr);
+            return ((uint32_t)lane < nd && f) ? ((uint64_t)(tot + 1) << 32) : 0ull;
+        };
+        auto apply = [&](const ResPub &pv, int pp, const PodT<F> &pprev) {
+            if (pv.ks == 0) return;
+            if (pv.slot >= 0) {
+                if (lane == pv.slot) reserve(S, SX, pprev, +1);
+            } else {
+                if ((uint32_t)lane == pv.nd_old) {
+                    S = stage[pp][pv.src];
+                    if (F & kFeatExt) {
+                        const int4 e = stagex[pp][pv.src];
+                        SX.ae0 = e.x; SX.re0 = e.y; SX.ae1 = e.z; SX.re1 = e.w;
+                    }
+                    reserve(S, SX, pprev, +1);
+                }
+                ++nd;
+            }
+        };
+        for (uint32_t w = 0; w < nwin; ++w) {
+            const uint32_t s0 = w * K, kend = min(K, P - s0);
+            const PodT<F> *wp = wpods2[w & 1];
+            if (wv == 1 && nd > 0) keyA[1][lane] = slot_key(S, SX, wp[0]);  // pod 0, inherited slots
+            __syncthreads();  // B1
+            const uint32_t isig = min(2u, kend - 1);
+            for (uint32_t i = 0; i < kend; ++i) {
+                const int par = i & 1, pp = par ^ 1;
+                const ResPub pv = read_pub(&pub[pp]);
+                if (i > 0) apply(pv, pp, wp[i - 1]);
+                if (wv == 1 && pend && i == isig) {
+                    // the previous window's rows went out write-through a window boundary ago
+                    drain_stores();
+                    if (lane == 0) __hip_atomic_store((gu32 *)&ctl->done, pend, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    pend = 0;
+                }
+                if (i + 1 < kend) {
+                    RowT<F> s2 = S;
+                    RowX x2s = SX;
+                    if (wv == 2) reserve(s2, x2s, wp[i], +1);
+                    (wv == 1 ? keyA : keyB)[par][lane] = slot_key(s2, x2s, wp[i + 1]);
+                }
+                __syncthreads();
+            }
+            apply(read_pub(&pub[(kend - 1) & 1]), (kend - 1) & 1, wp[kend - 1]);
+            __syncthreads();  // B2 (D's slot ranks and nodes)
+            const uint32_t rk = xrank[lane];
+            const bool keep = (uint32_t)lane < nd && rk != 0xFFFFFFFFu;
+            if (wv == 1 && keep) {
+                store_row_coh<F>(t, rs, xnode[lane], S, SX);
+                carry[rk] = S;
+                carryx[rk] = make_int4(SX.ae0, SX.re0, SX.ae1, SX.re1);
+            }
+            if (wv == 1) pend = w + 1;
+            __syncthreads();  // B3
+            nd = (uint32_t)__popcll(__ballot(keep));
+            if ((uint32_t)lane < nd) {
+                S = carry[lane];
+                const int4 e = carryx[lane];
+                SX.ae0 = e.x; SX.re0 = e.y; SX.ae1 = e.z; SX.re1 = e.w;
+            } else {
+                S = empty_row<F>();
+                SX = RowX{};
+            }
+        }
+        if (wv == 1 && pend) {
+            drain_stores();
+            if (lane == 0) __hip_atomic_store((gu32 *)&ctl->done, pend, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    } else {
+        // ---- C: candidate rows, C keys, the next pod's best clean entry; next-window prefetch -----
+        uint64_t eX = 0, eY = 0, c1 = 0;
+        RowT<F> r1 = empty_row<F>();
+        RowX x1{};
+        bool pref = false;  // window w's first entries and first candidate rows already loaded
+        uint64_t pe0 = 0, pe1 = 0, pe2 = 0;
+        uint32_t rdyv = 0, nfallback = 0;
+        auto dirty_bit = [&](uint64_t e) -> bool {
+            const uint32_t nidx = e ? key_node(e) : 0u;
+            return (dirty[nidx >> 5] >> (nidx & 31)) & 1u;
+        };
+        for (uint32_t w = 0; w < nwin; ++w) {
+            const uint32_t s0 = w * K, kend = min(K, P - s0);
+            const uint64_t *lists = lists0 + (size_t)(w & 1) * lwords;
+            const PodT<F> *wp = wpods2[w & 1];
+            const bool hasnext = w + 1 < nwin;
+            const uint32_t knext = hasnext ? min(K, P - s0 - K) : 0u;
+            const uint64_t *listsn = lists0 + (size_t)((w + 1) & 1) * lwords;
+            const uint32_t tnext = ((w + 1) >> 1) * K + knext;
+            auto ent = [&](const uint64_t *l, uint32_t pod, uint32_t kk) -> uint64_t {
+                return pod < kk ? load_coh_u64(l + (size_t)pod * 64 + lane) : 0ull;
+            };
+            uint64_t e0;
+            if (pref) {
+                e0 = pe0; eX = pe1; eY = pe2;
+            } else {
+                ++nfallback;
+                if (lane == 0) (void)res_wait_ge(&ctl->rdy[w & 1][0], (w >> 1) * K + kend, c.werr);
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below)
+                e0 = ent(lists, 0, kend);
+                eX = ent(lists, 1, kend);
+                eY = ent(lists, 2, kend);
+            }
+            c1 = (e0 != 0 && !dirty_bit(e0)) ? e0 : 0ull;
+            C1[1][lane] = c1;
+            if (!pref) {
+                r1 = load_row<F>(t, c1 ? key_node(c1) : 0u);
+                x1 = load_rowx<F>(t, c1 ? key_node(c1) : 0u);
+            }  // else r1 / x1 hold e0's row (loaded at the previous window's last pod)
+            pref = false;
+            __syncthreads();  // B1
+            const bool pfw = hasnext && kend >= 6;  // prefetch the next window during this one
+            auto step = [&](uint32_t i, uint64_t &en) {
+                const int par = i & 1, pp = par ^ 1;
+                const ResPub pv = read_pub(&pub[pp]);
+                if (lane == 0 && pv.ks != 0 && pv.slot < 0)
+                    __hip_atomic_fetch_or(&dirty[pv.w >> 5], 1u << (pv.w & 31), __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_WORKGROUP);
+                const bool use2 = pv.ks != 0 && c1 != 0 && key_node(c1) == pv.w;
+                const uint64_t cc = use2 ? 0ull : c1;
+                stage[par][lane] = r1;
+                if (F & kFeatExt) stagex[par][lane] = make_int4(x1.ae0, x1.re0, x1.ae1, x1.re1);
+                if (i + 1 < kend) {
+                    const RowT<F> crow = r1;
+                    const RowX cx = x1;
+                    const PodT<F> p = wp[i], pn1 = wp[i + 1];
+                    c1 = (en != 0 && !dirty_bit(en)) ? en : 0ull;  // pod i+1 against the dirty set through pod i-1
+                    C1[par][lane] = c1;
+                    r1 = load_row<F>(t, c1 ? key_node(c1) : 0u);
+                    x1 = load_rowx<F>(t, c1 ? key_node(c1) : 0u);
+                    en = ent(lists, i + 3, kend);
+                    RowT<F> cr = crow;
+                    RowX crx = cx;
+                    reserve(cr, crx, p, +1);
+                    const bool f = feasible<F>(cr, crx, pn1, px);
+                    const uint32_t tot = node_total<F>(cr, crx, pn1, px, c, 0, 0.0, 0, 0.0, nullptr);
+                    keyC[par][lane] = (cc != 0 && f) ? pack_key(tot + 1, key_node(cc)) : 0ull;
+                } else if (pref) {
+                    // last pod: the next window's first candidate rows (its entries arrived meanwhile;
+                    // a node dirtied from here on is masked out at the boundary)
+                    r1 = load_row<F>(t, pe0 ? key_node(pe0) : 0u);
+                    x1 = load_rowx<F>(t, pe0 ? key_node(pe0) : 0u);
+                }
+                if (pfw) {
+                    if (i == kend - 5) rdyv = load_coh_u32(&ctl->rdy[(w + 1) & 1][0]);
+                    if (i == kend - 3) {
+                        pref = __builtin_amdgcn_readfirstlane(rdyv) >= tnext;
+                        if (pref) {
+                            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                            pe0 = ent(listsn, 0, knext);
+                            pe1 = ent(listsn, 1, knext);
+                            pe2 = ent(listsn, 2, knext);
+                        }
+                    }
+                }
+                __syncthreads();
+            };
+            uint32_t i = 0;
+            for (; i + 1 < kend; i += 2) {
+                step(i, eX);
+                step(i + 1, eY);
+            }
+            if (i < kend) step(i, eX);
+            __syncthreads();  // B2
+            __syncthreads();  // B3 (D cleared the dropped slots' dirty bits before B2)
+        }
+        if (rdiag && lane == 0) rdiag[4] = nfallback;
+    }
+}
+
 template <uint32_t F, int E, int E2, bool K32>
-__global__ __launch_bounds__(256) void k_la_stream_res(DevTable t, const PodT<F> *__restrict__ pods, DevCfg c,
+__global__ __launch_bounds__(kResBS) void k_la_stream_res(DevTable t, const PodT<F> *__restrict__ pods, DevCfg c,
                                                        uint32_t P, uint32_t K, uint32_t G, uint32_t L,
                                                        uint32_t chunk, uint32_t nwin, uint64_t *lists0,
                                                        uint64_t *clists0, uint32_t lwords, uint32_t cwords,
                                                        uint32_t *dio, int32_t *__restrict__ out_node,
                                                        uint64_t *__restrict__ out_key,
-                                                       uint64_t *__restrict__ stamps, ResCtl *ctl) {
+                                                       uint64_t *__restrict__ stamps, ResCtl *ctl,
+                                                       uint64_t *__restrict__ rdiag) {
     if (blockIdx.x != 0) {
         res_selector<E, E2, F>(t, pods, c, P, K, G, L, chunk, nwin, lists0, clists0, lwords, cwords, ctl,
                                blockIdx.x - 1, gridDim.x - 1);
         return;
     }
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    __shared__ uint32_t okr_[4];
-    uint32_t &okr = okr_[0];
-    const LaShard sh{1u, 0u, K, 0u, (uint64_t)K * 64};
-    for (uint32_t w = 0; w < nwin; ++w) {
-        const uint32_t s0 = w * K, kw = min(K, P - s0), b = w & 1;
-        if (threadIdx.x == 0) okr = res_wait_ge(&ctl->rdy[b][0], (w >> 1) * K + kw, c.werr) ? 1u : 0u;
+    if (threadIdx.x >= 256) {  // not a pipeline wave: the same barrier count (1 + per window kend + 3)
         __syncthreads();
-        if (!okr) return;
-        la_resolve4_block<F, 1, false, K32, true>(lds, t, pods, c, s0, P, K, 64, 0, sh, lists0 + (size_t)b * lwords,
-                                                  out_node, out_key, stamps, nullptr,
-                                                  dio + ((w + 1) & 1) * 68, dio + (w & 1) * 68);
-        drain_stores();  // every wave: its row / dcur stores
-        __syncthreads();
-        if (threadIdx.x == 0) __hip_atomic_store((gu32 *)&ctl->done, w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (uint32_t w = 0; w < nwin; ++w)
+            for (uint32_t j = 0, nb = min(K, P - w * K) + 3; j < nb; ++j) __syncthreads();
+        return;
     }
+    const uint64_t t0 = rdiag ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    la_resolve4_stream<F, K32>(lds, t, pods, c, P, K, nwin, lists0, lwords, out_node, out_key, stamps, ctl, rdiag);
+    if (rdiag && threadIdx.x == 0) { rdiag[1] = __builtin_amdgcn_s_memrealtime() - t0; rdiag[3] = nwin; }
+    (void)dio;
 }
 
 template <uint32_t F>
 static hipError_t la_stream_res_f(const DevTable &t, const void *pods, const DevCfg &c, uint32_t P, const LaGeom &geo,
                                   uint64_t *lists0, uint64_t *clists0, uint32_t lwords, uint32_t cwords, uint32_t *dio,
                                   int32_t *on, uint64_t *ok, uint64_t *st, void *ctl, uint32_t sel_blocks,
-                                  hipStream_t stream) {
+                                  uint64_t *rdiag, hipStream_t stream) {
     const uint32_t K = geo.K, G = geo.G, L = geo.L, nwin = (P + K - 1) / K;
-    const uint32_t E2 = (G * L + 255) / 256;
-    const size_t bm = (((t.n + 31) / 32 + 3) & ~3u) * 4;
-    const size_t lds4 = bm + 5 * 2 * 64 * 8 + 2 * 64 * (sizeof(RowT<F>) + sizeof(int4)) + 2 * sizeof(ResPub) + 64 * 4 +
-                        64 * sizeof(PodT<F>);
+    const uint32_t E2 = 1;  // a pod's G*L <= 512 chunk keys, one per merging thread
+    if (G * L > (uint32_t)kResBS) return hipErrorInvalidValue;
+    const size_t lds4 = res_stream_lds_bytes<F>(t.n);
+    if (lds4 > 64 * 1024) return hipErrorInvalidValue;
     const dim3 grid(1 + sel_blocks);
     const PodT<F> *pp = (const PodT<F> *)pods;
     ResCtl *rc = (ResCtl *)ctl;
 #define QS_RESK(EE, EE2, KK)                                                                                          \
-    hipLaunchKernelGGL((k_la_stream_res<F, EE, EE2, KK>), grid, dim3(256), lds4, stream, t, pp, c, P, K, G, L,       \
-                       geo.chunk, nwin, lists0, clists0, lwords, cwords, dio, on, ok, st, rc)
-    if (geo.E == 5 && E2 == 1) {
-        if (geo.k32) QS_RESK(5, 1, true); else QS_RESK(5, 1, false);
-    } else if (geo.E == 8 && E2 == 7) {
-        if (geo.k32) QS_RESK(8, 7, true); else QS_RESK(8, 7, false);
-    } else {
-        return hipErrorInvalidValue;
+    hipLaunchKernelGGL((k_la_stream_res<F, EE, EE2, KK>), grid, dim3(kResBS), lds4, stream, t, pp, c, P, K, G, L,       \
+                       geo.chunk, nwin, lists0, clists0, lwords, cwords, dio, on, ok, st, rc, rdiag)
+#define QS_RESE(EE, EE2) \
+    else if (geo.E == EE && E2 == EE2) { if (geo.k32) QS_RESK(EE, EE2, true); else QS_RESK(EE, EE2, false); }
+    if (false) {
     }
+    QS_RESE(3, 1) QS_RESE(5, 1) QS_RESE(8, 1) QS_RESE(16, 1)
+    else return hipErrorInvalidValue;
+#undef QS_RESE
 #undef QS_RESK
     return hipGetLastError();
-}
-// Geometries with a resident-stream instantiation (the host falls back to per-window launches).
-inline bool la_stream_res_geometry(const LaGeom &geo) {
-    const uint32_t E2 = (geo.G * geo.L + 255) / 256;
-    return (geo.E == 5 && E2 == 1) || (geo.E == 8 && E2 == 7);
 }
 constexpr size_t kResCtlBytes = sizeof(ResCtl);
 

@@ -88,12 +88,12 @@ hipError_t launch_ready_set(uint64_t *ready, uint64_t value, hipStream_t stream)
 // workgroups; ctl = la_stream_res_ctl_bytes() of device memory, zeroed before every launch, and
 // c.werr the timeout word.  lists0 / clists0 / dio: the double-buffered window buffers of the
 // per-window path (lwords / cwords per parity).
-bool la_stream_res_supported(const LaGeom &geo, uint32_t feat, uint32_t n);
+LaGeom la_stream_res_plan(const LaGeom &geo, uint32_t feat, uint32_t n, uint32_t cus);  // G = 0: unsupported
 size_t la_stream_res_ctl_bytes();
 hipError_t launch_la_stream_res(const DevTable &t, const void *pods, const DevCfg &c, uint32_t P, const LaGeom &geo,
                                 uint64_t *lists0, uint64_t *clists0, uint32_t lwords, uint32_t cwords, uint32_t *dio,
                                 int32_t *on, uint64_t *ok, uint64_t *st, void *ctl, uint32_t sel_blocks,
-                                hipStream_t stream);
+                                uint64_t *rdiag, hipStream_t stream);
 
 hipError_t run_prepare();
 hipError_t launch_la_window(const DevTable &t, const void *pods, const DPodX *podx, uint32_t s0,

@@ -92,7 +92,7 @@ class QsStats(ctypes.Structure):
                 ("max_cycle_us", ctypes.c_double), ("engine_used", ctypes.c_int32),
                 ("table_layout", ctypes.c_int32), ("resumed_windows", ctypes.c_uint64),
                 ("device_faults", ctypes.c_uint64),
-                ("reserved", ctypes.c_int32 * 2), ("kernel_s", ctypes.c_double * 4),
+                ("resident", ctypes.c_int32), ("reserved", ctypes.c_int32), ("kernel_s", ctypes.c_double * 4),
                 ("kernel_launches", ctypes.c_uint64 * 4)]
 
     KERNELS = ("persistent", "scan", "select", "resolve")

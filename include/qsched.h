@@ -163,9 +163,12 @@ typedef struct qs_stats {
     uint64_t resumed_windows;       /* normalizing LOOKAHEAD: windows stopped for an exact rescan */
     uint64_t device_faults;         /* QS_EDEVICE results of this context so far (each one drops
                                        the device table; the next call rebuilds it from the mirror) */
-    int32_t reserved[2];
+    int32_t resident;               /* 1: LOOKAHEAD ran as one resident launch (resolver + selector
+                                       workgroups, k_la_stream_res); 0: per-window launches */
+    int32_t reserved;
     /* per-kernel device time (config.profile_kernels = 1; HIP events on the library's stream):
-     * [0] persistent, [1] scan (all per-pod kernels), [2] lookahead select, [3] lookahead resolve */
+     * [0] persistent, [1] scan (all per-pod kernels), [2] lookahead select, [3] lookahead resolve
+     * (a resident stream is one launch, counted under [3]) */
     double kernel_s[4];
     uint64_t kernel_launches[4];
 } qs_stats;

@@ -105,6 +105,34 @@ def test_config2_full_lookahead(oracle):
     assert 0.01 <= (g[0] < 0).mean() <= 0.05  # spec/synth.md G4: 1-5 % unschedulable
 
 
+@pytest.mark.parametrize("config,n,p,K", [(1, 100, 1000, 32), (2, 1500, 6000, 32), (2, 5000, 3000, 32),
+                                          (2, 9000, 7000, 32), (2, 30000, 4000, 32), (2, 1500, 6000, 7),
+                                          (2, 2000, 5000, 16), (2, 3000, 2000, 1)])
+def test_resident_stream(oracle, monkeypatch, config, n, p, K):
+    """The resident lookahead stream (the whole window sequence as one launch of a resolver and
+    selector workgroups) across selector geometries (1 to 7 node chunks, 3 to 16
+    nodes per lane, partial last windows, K = 1..32): bit-exact vs the oracle, reported in
+    stats.resident, and identical to the per-window launches (QS_RESIDENT=0)."""
+    nodes, pods = synth_generate(config, n, p)
+    g = run_gpu(nodes, pods, {}, "lookahead", lookahead=K)
+    assert g[3]["resident"] == 1
+    o = run_oracle(oracle, nodes, pods, {})
+    assert_same(g[:2], o[:2], g[2], o[2])
+    monkeypatch.setenv("QS_RESIDENT", "0")
+    w = run_gpu(nodes, pods, {}, "lookahead", lookahead=K)
+    assert w[3]["resident"] == 0
+    assert np.array_equal(w[0], g[0]) and np.array_equal(w[1], g[1])
+
+
+def test_resident_declines_large_tables(oracle):
+    """Beyond 7 chunks of 8,192 nodes (K = 32) the stream runs as per-window launches."""
+    nodes, pods = synth_generate(2, 70000, 600)
+    g = run_gpu(nodes, pods, {}, "lookahead")
+    assert g[3]["resident"] == 0
+    o = run_oracle(oracle, nodes, pods, {})
+    assert_same(g[:2], o[:2], g[2], o[2])
+
+
 def test_config2_full_persistent(oracle):
     nodes, pods = synth_generate(2, 5000, 100000)
     g = run_gpu(nodes, pods, {}, "persistent")
