@@ -1804,10 +1804,12 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
             if (wv == 1 && nd > 0) keyA[1][lane] = slot_key(S, SX, wp[0]);  // pod 0, inherited slots
             __syncthreads();  // B1
             const uint32_t isig = min(2u, kend - 1);
+            PodT<F> pprev = wp[0], pcur = wp[0];  // pods i-1 and i (pod i+1's record is read each step)
             for (uint32_t i = 0; i < kend; ++i) {
                 const int par = i & 1, pp = par ^ 1;
                 const ResPub pv = read_pub(&pub[pp]);
-                if (i > 0) apply(pv, pp, wp[i - 1]);
+                const PodT<F> pn1 = wp[i + 1];
+                if (i > 0) apply(pv, pp, pprev);
                 if (wv == 1 && pend && i == isig) {
                     // the previous window's rows went out write-through a window boundary ago
                     drain_stores();
@@ -1817,12 +1819,14 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                 if (i + 1 < kend) {
                     RowT<F> s2 = S;
                     RowX x2s = SX;
-                    if (wv == 2) reserve(s2, x2s, wp[i], +1);
-                    (wv == 1 ? keyA : keyB)[par][lane] = slot_key(s2, x2s, wp[i + 1]);
+                    if (wv == 2) reserve(s2, x2s, pcur, +1);
+                    (wv == 1 ? keyA : keyB)[par][lane] = slot_key(s2, x2s, pn1);
                 }
+                pprev = pcur;
+                pcur = pn1;
                 __syncthreads();
             }
-            apply(read_pub(&pub[(kend - 1) & 1]), (kend - 1) & 1, wp[kend - 1]);
+            apply(read_pub(&pub[(kend - 1) & 1]), (kend - 1) & 1, pprev);
             __syncthreads();  // B2 (D's slot ranks and nodes)
             const uint32_t rk = xrank[lane];
             const bool keep = (uint32_t)lane < nd && rk != 0xFFFFFFFFu;
@@ -1890,37 +1894,43 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
             pref = false;
             __syncthreads();  // B1
             const bool pfw = hasnext && kend >= 6;  // prefetch the next window during this one
+            PodT<F> pcur = wp[0];  // pod i's record (pod i+1's is read each step)
             auto step = [&](uint32_t i, uint64_t &en) {
                 const int par = i & 1, pp = par ^ 1;
+                // the step's LDS reads first, together: pod i-1's winner, the dirty word of pod
+                // i+1's entry (the set through pod i-2; pod i-1's winner is masked by compare), pod i+1
                 const ResPub pv = read_pub(&pub[pp]);
-                if (lane == 0 && pv.ks != 0 && pv.slot < 0)
-                    __hip_atomic_fetch_or(&dirty[pv.w >> 5], 1u << (pv.w & 31), __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_WORKGROUP);
-                const bool use2 = pv.ks != 0 && c1 != 0 && key_node(c1) == pv.w;
-                const uint64_t cc = use2 ? 0ull : c1;
+                const uint32_t en_node = en ? key_node(en) : 0u;
+                const uint32_t dword = dirty[en_node >> 5];
+                const PodT<F> pn1 = wp[i + 1];
+                // keyC's score (candidate c1's row + pod i, scored for pod i+1) needs no pub
+                RowT<F> cr = r1;
+                RowX crx = x1;
+                reserve(cr, crx, pcur, +1);
+                const bool f = feasible<F>(cr, crx, pn1, px);
+                const uint32_t tot = node_total<F>(cr, crx, pn1, px, c, 0, 0.0, 0, 0.0, nullptr);
                 stage[par][lane] = r1;
                 if (F & kFeatExt) stagex[par][lane] = make_int4(x1.ae0, x1.re0, x1.ae1, x1.re1);
+                const bool use2 = pv.ks != 0 && c1 != 0 && key_node(c1) == pv.w;
+                const uint64_t cc = use2 ? 0ull : c1;
                 if (i + 1 < kend) {
-                    const RowT<F> crow = r1;
-                    const RowX cx = x1;
-                    const PodT<F> p = wp[i], pn1 = wp[i + 1];
-                    c1 = (en != 0 && !dirty_bit(en)) ? en : 0ull;  // pod i+1 against the dirty set through pod i-1
+                    keyC[par][lane] = (cc != 0 && f) ? pack_key(tot + 1, key_node(cc)) : 0ull;
+                    const bool dirt = ((dword >> (en_node & 31)) & 1u) != 0 || (pv.ks != 0 && en_node == pv.w);
+                    c1 = (en != 0 && !dirt) ? en : 0ull;  // pod i+1 against the dirty set through pod i-1
                     C1[par][lane] = c1;
                     r1 = load_row<F>(t, c1 ? key_node(c1) : 0u);
                     x1 = load_rowx<F>(t, c1 ? key_node(c1) : 0u);
                     en = ent(lists, i + 3, kend);
-                    RowT<F> cr = crow;
-                    RowX crx = cx;
-                    reserve(cr, crx, p, +1);
-                    const bool f = feasible<F>(cr, crx, pn1, px);
-                    const uint32_t tot = node_total<F>(cr, crx, pn1, px, c, 0, 0.0, 0, 0.0, nullptr);
-                    keyC[par][lane] = (cc != 0 && f) ? pack_key(tot + 1, key_node(cc)) : 0ull;
                 } else if (pref) {
                     // last pod: the next window's first candidate rows (its entries arrived meanwhile;
                     // a node dirtied from here on is masked out at the boundary)
                     r1 = load_row<F>(t, pe0 ? key_node(pe0) : 0u);
                     x1 = load_rowx<F>(t, pe0 ? key_node(pe0) : 0u);
                 }
+                pcur = pn1;
+                if (lane == 0 && pv.ks != 0 && pv.slot < 0)  // (read by the next step's dirty word)
+                    __hip_atomic_fetch_or(&dirty[pv.w >> 5], 1u << (pv.w & 31), __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_WORKGROUP);
                 if (pfw) {
                     if (i == kend - 5) rdyv = load_coh_u32(&ctl->rdy[(w + 1) & 1][0]);
                     if (i == kend - 3) {
