@@ -1267,6 +1267,10 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                         const double nw = h[3] ? (double)h[3] : 1.0;
                         fprintf(stderr, "QS_RES_DIAG resolver %.3f us per window; windows whose lists were not prefetched %llu of %llu (selectors %u)\n",
                                 h[1] * 0.01 / nw, (unsigned long long)h[4], (unsigned long long)h[3], sel);
+                        if (h[12])  // QS_RES_DIAG_BLOCK build: busy shader cycles per pod step by role
+                            fprintf(stderr, "QS_RES_DIAG busy cycles/step: D %.0f A %.0f B %.0f C %.0f (steps %llu)\n",
+                                    h[8] / (double)h[12], h[9] / (double)h[12], h[10] / (double)h[12],
+                                    h[11] / (double)h[12], (unsigned long long)h[12]);
                     }
                 } else if (use_graph) {
                     std::vector<uint8_t> key;

@@ -1646,6 +1646,15 @@ constexpr size_t res_stream_lds_bytes(uint32_t n) {
     return ((((size_t)n + 31) / 32 + 3) & ~(size_t)3) * 4 + 4 * 2 * 64 * 8 + 2 * 64 * (sizeof(RowT<F>) + sizeof(int4)) +
            2 * sizeof(ResPub) + 3 * 64 * 4 + 64 * (sizeof(RowT<F>) + sizeof(int4)) + 2 * 64 * sizeof(PodT<F>);
 }
+// QS_RES_DIAG_BLOCK build (experiments): per-role busy shader cycles per pod step, barrier exit
+// to barrier entry, into rdiag[8 + role] (D, A, B, C) with the step count in rdiag[12].
+#ifdef QS_RES_DIAG_BLOCK
+constexpr bool kResDiag = true;
+#else
+constexpr bool kResDiag = false;
+#endif
+#define QS_RSTAMP_BEGIN() if (kResDiag && rdiag) ts_ = diag_stamp();
+#define QS_RSTAMP_END() if (kResDiag && rdiag) busy_ += diag_stamp() - ts_;
 template <uint32_t F, bool K32>
 __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable &t, const PodT<F> *__restrict__ pods,
                                                    const DevCfg &c, uint32_t P, uint32_t K, uint32_t nwin,
@@ -1673,6 +1682,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
     PodT<F>(*wpods2)[64] = (PodT<F>(*)[64])base;  // window pod records, by window parity
     const ResPub none{0, 0xFFFFFFFFu, -1, -1, 0, {0, 0}};
     const DPodX px{};
+    uint64_t ts_ = 0, busy_ = 0, steps_ = 0;
 
     for (uint32_t i = threadIdx.x; i < nwords; i += 256) dirty[i] = 0;
     if (threadIdx.x < min(K, P)) wpods2[0][threadIdx.x] = pods[threadIdx.x];
@@ -1695,6 +1705,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
             ResPub pv = none;
             __syncthreads();  // B1
             for (uint32_t i = 0; i < kend; ++i) {
+                QS_RSTAMP_BEGIN()
                 const int par = i & 1, pp = par ^ 1;
                 const uint64_t a = keyA[pp][lane], b = keyB[pp][lane], cl = keyC[pp][lane];
                 const uint64_t e1 = C1[pp][lane];
@@ -1735,8 +1746,10 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                     res_key = ks;
                     if (stamps) res_stamp = __builtin_amdgcn_s_memrealtime();
                 }
+                QS_RSTAMP_END()
                 __syncthreads();
             }
+            steps_ += kend;
             if ((uint32_t)lane < kend) {
                 out_node[s0 + lane] = res_key ? (int32_t)key_node(res_key) : -1;
                 if (out_key) out_key[s0 + lane] = res_key;
@@ -1806,6 +1819,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
             const uint32_t isig = min(2u, kend - 1);
             PodT<F> pprev = wp[0], pcur = wp[0];  // pods i-1 and i (pod i+1's record is read each step)
             for (uint32_t i = 0; i < kend; ++i) {
+                QS_RSTAMP_BEGIN()
                 const int par = i & 1, pp = par ^ 1;
                 const ResPub pv = read_pub(&pub[pp]);
                 const PodT<F> pn1 = wp[i + 1];
@@ -1824,6 +1838,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                 }
                 pprev = pcur;
                 pcur = pn1;
+                QS_RSTAMP_END()
                 __syncthreads();
             }
             apply(read_pub(&pub[(kend - 1) & 1]), (kend - 1) & 1, pprev);
@@ -1895,7 +1910,9 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
             __syncthreads();  // B1
             const bool pfw = hasnext && kend >= 6;  // prefetch the next window during this one
             PodT<F> pcur = wp[0];  // pod i's record (pod i+1's is read each step)
-            auto step = [&](uint32_t i, uint64_t &en) {
+            // HOOK: the step may carry the next-window prefetch (only the last steps of a window)
+            auto step = [&](auto hook, uint32_t i, uint64_t &en) {
+                QS_RSTAMP_BEGIN()
                 const int par = i & 1, pp = par ^ 1;
                 // the step's LDS reads first, together: pod i-1's winner, the dirty word of pod
                 // i+1's entry (the set through pod i-2; pod i-1's winner is masked by compare), pod i+1
@@ -1931,7 +1948,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                 if (lane == 0 && pv.ks != 0 && pv.slot < 0)  // (read by the next step's dirty word)
                     __hip_atomic_fetch_or(&dirty[pv.w >> 5], 1u << (pv.w & 31), __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (pfw) {
+                if (decltype(hook)::value && pfw) {
                     if (i == kend - 5) rdyv = load_coh_u32(&ctl->rdy[(w + 1) & 1][0]);
                     if (i == kend - 3) {
                         pref = __builtin_amdgcn_readfirstlane(rdyv) >= tnext;
@@ -1943,20 +1960,34 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                         }
                     }
                 }
+                QS_RSTAMP_END()
                 __syncthreads();
             };
+            const std::integral_constant<bool, false> plain{};
+            const std::integral_constant<bool, true> hooked{};
+            const uint32_t ih = pfw ? ((kend - 5) & ~1u) : kend;  // first step with the hooks (even)
             uint32_t i = 0;
-            for (; i + 1 < kend; i += 2) {
-                step(i, eX);
-                step(i + 1, eY);
+            for (; i + 1 < ih; i += 2) {
+                step(plain, i, eX);
+                step(plain, i + 1, eY);
             }
-            if (i < kend) step(i, eX);
+            for (; i + 1 < kend; i += 2) {
+                step(hooked, i, eX);
+                step(hooked, i + 1, eY);
+            }
+            if (i < kend) step(hooked, i, eX);
             __syncthreads();  // B2
             __syncthreads();  // B3 (D cleared the dropped slots' dirty bits before B2)
         }
         if (rdiag && lane == 0) rdiag[4] = nfallback;
     }
+    if (kResDiag && rdiag && lane == 0) {
+        rdiag[8 + wv] = busy_;
+        if (wv == 0) rdiag[12] = steps_;
+    }
 }
+#undef QS_RSTAMP_BEGIN
+#undef QS_RSTAMP_END
 
 template <uint32_t F, int E, int E2, bool K32>
 __global__ __launch_bounds__(kResBS) void k_la_stream_res(DevTable t, const PodT<F> *__restrict__ pods, DevCfg c,

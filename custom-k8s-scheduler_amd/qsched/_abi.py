@@ -13,7 +13,8 @@ import os
 import numpy as np
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_ROOT, "libqsched.so")
+# QSCHED_LIB (diagnostic builds, e.g. tools/diag_build.sh) overrides the in-tree library
+LIB_PATH = os.environ.get("QSCHED_LIB") or os.path.join(PKG_ROOT, "libqsched.so")
 
 QS_ABI_VERSION = 2
 QS_MAX_EXT = 2

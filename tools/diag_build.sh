@@ -1,0 +1,13 @@
+#!/bin/bash
+# Builds the diagnostic variant of libqsched (resident resolver busy-cycle stamps,
+# -DQS_RES_DIAG_BLOCK) as custom-k8s-scheduler_amd/libqsched_diag.so without touching the in-tree
+# library; select it at run time with QSCHED_LIB=<path> and QS_RES_DIAG=1.
+set -e
+cd "$(dirname "$0")/../custom-k8s-scheduler_amd"
+B=build_diag
+mkdir -p $B
+F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -fvisibility=hidden -ffp-contract=off -DQS_RES_DIAG_BLOCK"
+for f in qs_kernels qs_kernels_wide; do /opt/rocm/bin/hipcc $F -c csrc/$f.hip -o $B/$f.o & done
+for f in qs_host qs_helpers qs_dist; do /opt/rocm/bin/hipcc $F -x hip -c csrc/$f.cpp -o $B/$f.o & done
+wait
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o libqsched_diag.so $B/*.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
