@@ -437,7 +437,8 @@ __device__ __forceinline__ uint32_t la_score(const R &r, const P &p, const DevCf
     const double yd = __builtin_bit_cast(
         double, (__builtin_bit_cast(uint64_t, c.yd_both) & mb) |
                     (__builtin_bit_cast(uint64_t, c.yd_c) & mc) | (__builtin_bit_cast(uint64_t, c.yd_m) & mm));
-    return den ? floor_div(num, yd) : 0u;
+    (void)den;  // den == 0 means num == 0 and yd == 0.0: floor_div gives 0 without a branch
+    return floor_div(num, yd);
 }
 // BalancedAllocation (UP balanced_allocation.go#balancedResourceScorer), Requested + pod req
 template <class R, class P>

@@ -1823,6 +1823,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                 const int par = i & 1, pp = par ^ 1;
                 const ResPub pv = read_pub(&pub[pp]);
                 const PodT<F> pn1 = wp[i + 1];
+                __builtin_amdgcn_sched_barrier(0);  // both LDS reads go out before the pub's wait
                 if (i > 0) apply(pv, pp, pprev);
                 if (wv == 1 && pend && i == isig) {
                     // the previous window's rows went out write-through a window boundary ago
@@ -1920,6 +1921,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                 const uint32_t en_node = en ? key_node(en) : 0u;
                 const uint32_t dword = dirty[en_node >> 5];
                 const PodT<F> pn1 = wp[i + 1];
+                __builtin_amdgcn_sched_barrier(0);  // the three LDS reads go out before any of their waits
                 // keyC's score (candidate c1's row + pod i, scored for pod i+1) needs no pub
                 RowT<F> cr = r1;
                 RowX crx = x1;
