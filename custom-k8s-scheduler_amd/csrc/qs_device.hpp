@@ -517,6 +517,29 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
     v = dpp_max32<0x143, 0xC>(v);  // row_bcast:31 into rows 2, 3
     return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
+// The same reduction with the DPP moves folded into the max (v_max_u32_dpp: 6 instead of 12 VALU
+// instructions on the resolver's critical path); the s_nop 1 before each step covers the DPP
+// read-after-VALU-write hazard that the compiler cannot see inside the asm.
+__device__ __forceinline__ uint32_t wave_max_u32_dpp(uint32_t v) {
+    uint32_t r;
+    asm volatile(
+        "s_nop 1\n\t"
+        "v_max_u32_dpp %1, %1, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_max_u32_dpp %1, %1, %1 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_max_u32_dpp %1, %1, %1 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_max_u32_dpp %1, %1, %1 row_mirror row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_max_u32_dpp %1, %1, %1 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_max_u32_dpp %1, %1, %1 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_readlane_b32 %0, %1, 63"
+        : "=s"(r), "+v"(v));
+    return r;
+}
 // Max of packed keys as two 32-bit reductions: the score half first, then the index half among
 // the lanes holding that score (keys are unique, so this is the u64 max).
 __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {

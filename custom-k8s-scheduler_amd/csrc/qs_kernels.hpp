@@ -1723,7 +1723,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                 if (K32) {  // (score+1) < 2^10 and n <= 2^22: one 32-bit reduction
                     const uint32_t tv = (uint32_t)(best >> 32);
                     const uint32_t k32 = tv ? (tv << 22) | (0x3FFFFFu - key_node(best)) : 0u;
-                    const uint32_t m = wave_max_u32(k32);
+                    const uint32_t m = wave_max_u32_dpp(k32);
                     ks = m ? (((uint64_t)(m >> 22) << 32) | (uint64_t)(0xFFFFFFFFu - (0x3FFFFFu - (m & 0x3FFFFFu)))) : 0ull;
                 } else {
                     ks = wave_max_u64(best);
@@ -1738,6 +1738,9 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                         np.src = (int32_t)__builtin_ctzll(__ballot(cand == ks));
                         if ((uint32_t)lane == nd) { didx = np.w; won = true; }
                         ++nd;
+                        if (lane == 0)  // dirty from now on: wave C's next dirty-word reads see it
+                            __hip_atomic_fetch_or(&dirty[np.w >> 5], 1u << (np.w & 31), __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
                 }
                 pv = np;
@@ -1765,7 +1768,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
             xnode[lane] = didx;
             if (act && won) {
                 dnode[rk] = didx;
-                // (wave C marks new slots one pod late: the window's last winner is marked here)
+                // (already marked when created; kept as the boundary invariant: dirty == live slots)
                 __hip_atomic_fetch_or(&dirty[didx >> 5], 1u << (didx & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
             if (act && !won)
@@ -1914,14 +1917,15 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
             // HOOK: the step may carry the next-window prefetch (only the last steps of a window)
             auto step = [&](auto hook, uint32_t i, uint64_t &en) {
                 QS_RSTAMP_BEGIN()
-                const int par = i & 1, pp = par ^ 1;
-                // the step's LDS reads first, together: pod i-1's winner, the dirty word of pod
-                // i+1's entry (the set through pod i-2; pod i-1's winner is masked by compare), pod i+1
-                const ResPub pv = read_pub(&pub[pp]);
+                const int par = i & 1;
+                // the step's LDS reads first, together: the dirty word of pod i+1's entry (the set
+                // through pod i-1: wave D marks a new slot in the step that creates it) and pod i+1.
+                // C never reads the published winner: a candidate taken by pod i-1's winner is
+                // masked by D, which then never names that lane as a new slot's source.
                 const uint32_t en_node = en ? key_node(en) : 0u;
                 const uint32_t dword = dirty[en_node >> 5];
                 const PodT<F> pn1 = wp[i + 1];
-                __builtin_amdgcn_sched_barrier(0);  // the three LDS reads go out before any of their waits
+                __builtin_amdgcn_sched_barrier(0);  // both LDS reads go out before their waits
                 // keyC's score (candidate c1's row + pod i, scored for pod i+1) needs no pub
                 RowT<F> cr = r1;
                 RowX crx = x1;
@@ -1930,11 +1934,9 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                 const uint32_t tot = node_total<F>(cr, crx, pn1, px, c, 0, 0.0, 0, 0.0, nullptr);
                 stage[par][lane] = r1;
                 if (F & kFeatExt) stagex[par][lane] = make_int4(x1.ae0, x1.re0, x1.ae1, x1.re1);
-                const bool use2 = pv.ks != 0 && c1 != 0 && key_node(c1) == pv.w;
-                const uint64_t cc = use2 ? 0ull : c1;
                 if (i + 1 < kend) {
-                    keyC[par][lane] = (cc != 0 && f) ? pack_key(tot + 1, key_node(cc)) : 0ull;
-                    const bool dirt = ((dword >> (en_node & 31)) & 1u) != 0 || (pv.ks != 0 && en_node == pv.w);
+                    keyC[par][lane] = (c1 != 0 && f) ? pack_key(tot + 1, key_node(c1)) : 0ull;
+                    const bool dirt = ((dword >> (en_node & 31)) & 1u) != 0;
                     c1 = (en != 0 && !dirt) ? en : 0ull;  // pod i+1 against the dirty set through pod i-1
                     C1[par][lane] = c1;
                     r1 = load_row<F>(t, c1 ? key_node(c1) : 0u);
@@ -1947,9 +1949,6 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                     x1 = load_rowx<F>(t, pe0 ? key_node(pe0) : 0u);
                 }
                 pcur = pn1;
-                if (lane == 0 && pv.ks != 0 && pv.slot < 0)  // (read by the next step's dirty word)
-                    __hip_atomic_fetch_or(&dirty[pv.w >> 5], 1u << (pv.w & 31), __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_WORKGROUP);
                 if (decltype(hook)::value && pfw) {
                     if (i == kend - 5) rdyv = load_coh_u32(&ctl->rdy[(w + 1) & 1][0]);
                     if (i == kend - 3) {
