@@ -1287,8 +1287,7 @@ __device__ __forceinline__ void la_resolve4_block(uint32_t *lds, const DevTable 
             if (NORM && k < kend) r = PodN{wpodx[k], wnorm[k], wrcp[k]};
             return r;
         };
-        auto slot_key = [&](const RowT<F> &r, const RowX &x, uint32_t k, const PodN &pn) -> uint64_t {
-            const PodT<F> &q = wpods[k];
+        auto slot_key = [&](const RowT<F> &r, const RowX &x, const PodT<F> &q, const PodN &pn) -> uint64_t {
             const bool act = (uint32_t)lane < nd;
             if (NORM) {
                 const DPodX &qx = pn.x;
@@ -1307,7 +1306,7 @@ __device__ __forceinline__ void la_resolve4_block(uint32_t *lds, const DevTable 
             const uint32_t tot = node_total<F>(r, x, q, px, c, 0, 0.0, 0, 0.0, nullptr);
             return (act && f) ? ((uint64_t)(tot + 1) << 32) : 0ull;
         };
-        if (wv == 1 && nd0 > 0) keyA[1][lane] = slot_key(S, SX, 0, podn(0));  // pod 0, inherited slots
+        if (wv == 1 && nd0 > 0) keyA[1][lane] = slot_key(S, SX, wpods[0], podn(0));  // pod 0, inherited slots
         PodN pnx = podn(1);  // pod i+1's record at step i
         auto apply = [&](const ResPub &pv, int pp, const PodT<F> &pprev) {
             if (pv.ks == 0) return;
@@ -1329,22 +1328,27 @@ __device__ __forceinline__ void la_resolve4_block(uint32_t *lds, const DevTable 
         };
         __syncthreads();
         bool stopped = false;
+        PodT<F> pprev = wpods[0], pcur = wpods[0];  // pods i-1 and i (pod i+1's record is read each step)
         for (uint32_t i = 0; i < kend; ++i) {
             QS_DIAG_BEGIN()
             const int par = i & 1, pp = par ^ 1;
             const ResPub pv = read_pub(&pub[pp]);
+            const PodT<F> pn1 = wpods[min(i + 1, kend - 1)];  // (K may be 64: stay inside the array)
+            __builtin_amdgcn_sched_barrier(0);  // both LDS reads go out before the pub's wait
             if (NORM && pv.slot == -2) { stopped = true; break; }  // D stopped at pod i-1
-            if (i > 0) apply(pv, pp, wpods[i - 1]);
+            if (i > 0) apply(pv, pp, pprev);
             if (DIAG) { const uint64_t t_ = diag_stamp(); dpart += t_ - tprev; }
             if (i + 1 < kend) {
-                const PodN pcur = pnx;
+                const PodN pnc = pnx;
                 if (NORM) pnx = podn(i + 2);  // next step's record: its LDS reads overlap this score
                 RowT<F> s2 = S;
                 RowX x2s = SX;
-                if (wv == 2) reserve(s2, x2s, wpods[i], +1);
+                if (wv == 2) reserve(s2, x2s, pcur, +1);
                 // score half only: wave D owns the slot -> node map and fills the index half
-                (wv == 1 ? keyA : keyB)[par][lane] = slot_key(s2, x2s, i + 1, pcur);
+                (wv == 1 ? keyA : keyB)[par][lane] = slot_key(s2, x2s, pn1, pnc);
             }
+            pprev = pcur;
+            pcur = pn1;
             QS_DIAG_END()
             __syncthreads();
         }
@@ -1404,9 +1408,59 @@ __device__ __forceinline__ void la_resolve4_block(uint32_t *lds, const DevTable 
         RowT<F> r1 = load_row<F>(t, c1 ? key_node(c1) : 0u), r2 = TWO ? load_row<F>(t, c2 ? key_node(c2) : 0u) : empty_row<F>();
         RowX x1 = load_rowx<F>(t, c1 ? key_node(c1) : 0u), x2 = TWO ? load_rowx<F>(t, c2 ? key_node(c2) : 0u) : RowX{};
         __syncthreads();
+        PodT<F> pcurC = wpods[0];  // (EPL == 1 path) pod i's record, carried
         auto step = [&](uint32_t i, uint64_t(&en)[EPL]) -> bool {
             QS_DIAG_BEGIN()
             const int par = i & 1, pp = par ^ 1;
+            if constexpr (EPL == 1) {
+                // one entry per lane (merged lists): the step's LDS reads go out together (the
+                // pub, the dirty word of pod i+1's entry through pod i-2 — pod i-1's winner is
+                // masked by compare — and pod i+1's records), and the candidate's score, which
+                // needs no pub, is computed while they land
+                const ResPub pv = read_pub(&pub[pp]);
+                const uint32_t en_node = en[0] ? key_node(en[0]) : 0u;
+                const uint32_t dword = dirty[en_node >> 5];
+                const uint32_t kn = min(i + 1, kend - 1);
+                const PodT<F> pn1 = wpods[kn];
+                DPodX qx{};
+                NormInfo nf{0, 0, 0, 0};
+                double2 yr = make_double2(0.0, 0.0);
+                if (NORM) { qx = wpodx[kn]; nf = wnorm[kn]; yr = wrcp[kn]; }
+                __builtin_amdgcn_sched_barrier(0);
+                RowT<F> cr = r1;
+                RowX crx = x1;
+                reserve(cr, crx, pcurC, +1);
+                const bool f = feasible<F>(cr, crx, pn1, NORM ? qx : px);
+                const uint32_t tot = node_total<F>(cr, crx, pn1, NORM ? qx : px, c, nf.mt, yr.x, nf.ma, yr.y, nullptr);
+                uint32_t fl = 0;
+                if (NORM && !f) {
+                    if (F & kFeatTaint) fl |= taint_raw(crx, qx) == nf.mt ? 1u : 0u;
+                    if (F & kFeatAffinity) fl |= affinity_raw(crx, pn1, qx) == nf.ma ? 2u : 0u;
+                }
+                if (NORM && pv.slot == -2) return false;  // D stopped at pod i-1
+                stage[par][lane] = r1;
+                if (NORM) stagexN[par][lane] = x1;
+                else if (F & kFeatExt) stagex[par][lane] = make_int4(x1.ae0, x1.re0, x1.ae1, x1.re1);
+                const bool use2 = pv.ks != 0 && c1 != 0 && key_node(c1) == pv.w;
+                const uint64_t cc = use2 ? 0ull : c1;
+                if (i + 1 < kend) {
+                    keyC[par][lane] = (cc != 0 && f) ? pack_key(tot + 1, key_node(cc)) : 0ull;
+                    if (NORM) flagC[par][lane] = fl;
+                    const bool dirt = ((dword >> (en_node & 31)) & 1u) != 0 || (pv.ks != 0 && en_node == pv.w);
+                    c1 = (en[0] != 0 && !dirt) ? en[0] : 0ull;  // pod i+1 against the dirty set through pod i-1
+                    C1[par][lane] = c1;
+                    r1 = load_row<F>(t, c1 ? key_node(c1) : 0u);
+                    x1 = load_rowx<F>(t, c1 ? key_node(c1) : 0u);
+                    load_ent(en, i + 3);
+                }
+                pcurC = pn1;
+                if (lane == 0 && pv.ks != 0 && pv.slot < 0)  // (read by the next step's dirty word)
+                    __hip_atomic_fetch_or(&dirty[pv.w >> 5], 1u << (pv.w & 31), __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_WORKGROUP);
+                QS_DIAG_END()
+                __syncthreads();
+                return true;
+            }
             const ResPub pv = read_pub(&pub[pp]);
             if (NORM && pv.slot == -2) return false;  // D stopped at pod i-1
             if (lane == 0 && pv.ks != 0 && pv.slot < 0)
