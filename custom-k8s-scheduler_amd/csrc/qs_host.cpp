@@ -1267,6 +1267,10 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                         const double nw = h[3] ? (double)h[3] : 1.0;
                         fprintf(stderr, "QS_RES_DIAG resolver %.3f us per window; windows whose lists were not prefetched %llu of %llu (selectors %u)\n",
                                 h[1] * 0.01 / nw, (unsigned long long)h[4], (unsigned long long)h[3], sel);
+                        if (h[19])
+                            fprintf(stderr, "QS_RES_DIAG selector task (us): scoring %.2f chunk top-L %.2f publish/merge %.2f (tasks %llu, merges %llu)\n",
+                                    h[16] * 0.01 / (double)h[19], h[17] * 0.01 / (double)h[19], h[18] * 0.01 / (double)h[19],
+                                    (unsigned long long)h[19], (unsigned long long)h[20]);
                         if (h[12])  // QS_RES_DIAG_BLOCK build: busy shader cycles per pod step by role
                             fprintf(stderr, "QS_RES_DIAG busy cycles/step: D %.0f A %.0f B %.0f C %.0f (steps %llu)\n",
                                     h[8] / (double)h[12], h[9] / (double)h[12], h[10] / (double)h[12],

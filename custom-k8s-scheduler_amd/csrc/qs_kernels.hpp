@@ -804,15 +804,13 @@ __global__ __launch_bounds__(64) void k_la_resolve(DevTable t, const PodT<F> *__
 // only wave 0 writes results.
 constexpr uint32_t kResNormWaves = 4;
 template <uint32_t F, int EPL>
-__global__ __launch_bounds__(64 * kResNormWaves) void k_la_resolve_norm(
-    DevTable t, const PodT<F> *__restrict__ pods, const DPodX *__restrict__ podx, DevCfg c,
-    uint32_t s0, uint32_t P, uint32_t K, uint32_t GLp, uint32_t lr, LaShard sh,
+__device__ __forceinline__ void la_resolve_norm_body(
+    uint32_t *lds, const DevTable &t, const PodT<F> *__restrict__ pods, const DPodX *__restrict__ podx,
+    const DevCfg &c, uint32_t s0, uint32_t P, uint32_t K, uint32_t GLp, uint32_t lr, const LaShard &sh,
     const uint64_t *__restrict__ lists, const NormInfo *__restrict__ norm,
     int32_t *__restrict__ out_node, uint64_t *__restrict__ out_key, uint64_t *__restrict__ stamps,
     const uint32_t *__restrict__ dprev, uint32_t *__restrict__ dcur, unsigned long long *nfall,
     const uint32_t *__restrict__ rec) {
-    if (!rec) wait_lists_ready(c, s0, K);  // resume mode follows the four-wave kernel on its stream
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     __shared__ uint32_t red_m[2 * kResNormWaves];  // per-wave rescan maxima (taint, affinity)
     __shared__ uint64_t red_k[kResNormWaves];      // per-wave rescan best keys
     const int lane = threadIdx.x & 63;
@@ -824,13 +822,14 @@ __global__ __launch_bounds__(64 * kResNormWaves) void k_la_resolve_norm(
     uint64_t won0 = 0;
     const uint32_t *init = dprev;
     if (rec) {
-        const uint32_t stop = rec[0];
+        // (vector loads: the record may have been written earlier in this launch, by wave D)
+        const uint32_t stop = load_coh_u32(rec);
         if (stop == 0xFFFFFFFFu) return;
         if (threadIdx.x == 0 && nfall) atomicAdd(nfall + 1, 1ull);  // resumed windows (QS_NORM_DIAG)
         pbase = stop;
         s0 += stop;
         K -= stop;
-        won0 = (uint64_t)rec[2] | ((uint64_t)rec[3] << 32);
+        won0 = (uint64_t)load_coh_u32(rec + 2) | ((uint64_t)load_coh_u32(rec + 3) << 32);
         init = rec + 3;  // init[1 + j] = rec[4 + j]; the count is rec[1]
     }
     const uint32_t n = t.n, nwords = (n + 31) / 32;
@@ -842,13 +841,13 @@ __global__ __launch_bounds__(64 * kResNormWaves) void k_la_resolve_norm(
     uint32_t *sidx = (uint32_t *)(stagex + 1);         // [64] slot -> node, staged for a rescan
     for (uint32_t i = lane; i < nwords; i += 64) dirty[i] = 0;
     const uint32_t kend = min(K, P - s0);
-    const uint32_t nd0 = rec ? rec[1] : (dprev ? dprev[0] : 0u);
+    const uint32_t nd0 = rec ? load_coh_u32(rec + 1) : (dprev ? dprev[0] : 0u);
     __syncthreads();
     RowT<F> dr = empty_row<F>();
     RowX dx{};
     uint32_t didx = 0xFFFFFFFFu;
     if ((uint32_t)lane < nd0) {
-        didx = init[1 + lane];
+        didx = rec ? load_coh_u32(init + 1 + lane) : init[1 + lane];
         dr = load_row<F>(t, didx);
         dx = load_rowx<F>(t, didx);
         atomicOr(&dirty[didx >> 5], 1u << (didx & 31));
@@ -1049,6 +1048,20 @@ __global__ __launch_bounds__(64 * kResNormWaves) void k_la_resolve_norm(
         if (won && (uint32_t)lane < nd) dcur[1 + __popcll(wm & ((1ull << lane) - 1ull))] = didx;
         if (lane == 0) dcur[0] = (uint32_t)__popcll(wm);
     }
+}
+
+template <uint32_t F, int EPL>
+__global__ __launch_bounds__(64 * kResNormWaves) void k_la_resolve_norm(
+    DevTable t, const PodT<F> *__restrict__ pods, const DPodX *__restrict__ podx, DevCfg c,
+    uint32_t s0, uint32_t P, uint32_t K, uint32_t GLp, uint32_t lr, LaShard sh,
+    const uint64_t *__restrict__ lists, const NormInfo *__restrict__ norm,
+    int32_t *__restrict__ out_node, uint64_t *__restrict__ out_key, uint64_t *__restrict__ stamps,
+    const uint32_t *__restrict__ dprev, uint32_t *__restrict__ dcur, unsigned long long *nfall,
+    const uint32_t *__restrict__ rec) {
+    if (!rec) wait_lists_ready(c, s0, K);  // resume mode follows the four-wave kernel on its stream
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    la_resolve_norm_body<F, EPL>(lds, t, pods, podx, c, s0, P, K, GLp, lr, sh, lists, norm, out_node, out_key,
+                                 stamps, dprev, dcur, nfall, rec);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1549,11 +1562,21 @@ __global__ __launch_bounds__(256) void k_la_resolve4(DevTable t, const PodT<F> *
                                                      uint32_t *__restrict__ dcur,
                                                      const DPodX *__restrict__ podx,
                                                      const NormInfo *__restrict__ norm,
-                                                     uint32_t *__restrict__ rec) {
+                                                     uint32_t *__restrict__ rec,
+                                                     unsigned long long *nfall) {
     wait_lists_ready(c, s0, K);
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     la_resolve4_block<F, EPL, DIAG, K32>(lds, t, pods, c, s0, P, K, GLp, lr, sh, lists, out_node, out_key,
                                          stamps, diag, dprev, dcur, podx, norm, rec);
+    if constexpr ((F & kFeatNorm) != 0) {
+        // a window that stopped on a lost maximum resumes here (no second launch per window): the
+        // stop record wave D just wrote decides, after the barrier, in every wave alike
+        if (rec) {
+            __syncthreads();
+            la_resolve_norm_body<F, 1>(lds, t, pods, podx, c, s0, P, K, GLp, lr, sh, lists, norm, out_node, out_key,
+                                       stamps, dprev, dcur, nfall, rec);
+        }
+    }
 }
 
 // =============================================================================================
@@ -1618,7 +1641,11 @@ template <int E, int E2, uint32_t F>
 __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *__restrict__ pods, const DevCfg &c,
                                              uint32_t P, uint32_t K, uint32_t G, uint32_t L, uint32_t chunk,
                                              uint32_t nwin, uint64_t *lists0, uint64_t *clists0, uint32_t lwords,
-                                             uint32_t cwords, ResCtl *ctl, uint32_t sid, uint32_t S) {
+                                             uint32_t cwords, ResCtl *ctl, uint32_t sid, uint32_t S,
+                                             uint64_t *rdiag) {
+    // rdiag (QS_RES_DIAG=1): summed s_memrealtime ticks of the selectors' phases, [16] scoring,
+    // [17] chunk top-L, [18] publish / merge, [19] tasks, [20] merges
+    uint64_t ts0 = 0, ts1 = 0, ts2 = 0, dsc = 0, dtl = 0, dpm = 0, ntask = 0, nmerge = 0;
     __shared__ uint64_t lbuf[64];
     __shared__ uint32_t okflag_[4];  // (16 B: keeps the dynamic-LDS base 16-byte aligned)
     uint32_t &okflag = okflag_[0];
@@ -1637,6 +1664,7 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
         uint64_t *clists = clists0 + (size_t)b * cwords;
         for (uint32_t task = sid; task < kw * G; task += S) {
             const uint32_t k = task / G, g = task % G;
+            if (rdiag) ts0 = __builtin_amdgcn_s_memrealtime();
             const PodT<F> p = pods[s0 + k];
             const uint32_t start = g * chunk, end = min(t.n, start + chunk);
             const uint32_t base = start + (uint32_t)w8 * E * kWave + lane;
@@ -1653,8 +1681,10 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
                     tv[j] = f ? tot + 1 : 0;
                 }
             }
+            if (rdiag) { __syncthreads(); ts1 = __builtin_amdgcn_s_memrealtime(); }
             block_topl<kResBS, E>(tv, L, lbuf, [&](int j) { return pack_key(tv[j], base + j * kWave); });
             __syncthreads();  // lbuf complete
+            if (rdiag) ts2 = __builtin_amdgcn_s_memrealtime();
             uint64_t *out = lists + (size_t)k * 64;
             if (G == 1) {
                 res_publish_list(lbuf, L, out, &ctl->rdy[b][0]);
@@ -1679,10 +1709,22 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
                     block_topl<kResBS, E2>(te, L, lbuf, [&](int j) { return e[j]; });
                     __syncthreads();
                     res_publish_list(lbuf, L, out, &ctl->rdy[b][0]);
+                    ++nmerge;
                 }
             }
             __syncthreads();  // lbuf / okflag reused by the next task
+            if (rdiag) {
+                const uint64_t t3 = __builtin_amdgcn_s_memrealtime();
+                dsc += ts1 - ts0; dtl += ts2 - ts1; dpm += t3 - ts2; ++ntask;
+            }
         }
+    }
+    if (rdiag && tid == 0) {
+        atomicAdd((unsigned long long *)&rdiag[16], (unsigned long long)dsc);
+        atomicAdd((unsigned long long *)&rdiag[17], (unsigned long long)dtl);
+        atomicAdd((unsigned long long *)&rdiag[18], (unsigned long long)dpm);
+        atomicAdd((unsigned long long *)&rdiag[19], (unsigned long long)ntask);
+        atomicAdd((unsigned long long *)&rdiag[20], (unsigned long long)nmerge);
     }
 }
 
@@ -2055,7 +2097,7 @@ __global__ __launch_bounds__(kResBS) void k_la_stream_res(DevTable t, const PodT
                                                        uint64_t *__restrict__ rdiag) {
     if (blockIdx.x != 0) {
         res_selector<E, E2, F>(t, pods, c, P, K, G, L, chunk, nwin, lists0, clists0, lwords, cwords, ctl,
-                               blockIdx.x - 1, gridDim.x - 1);
+                               blockIdx.x - 1, gridDim.x - 1, rdiag);
         return;
     }
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -3104,18 +3146,17 @@ static hipError_t la_window_f(const DevTable &t, const void *pods_, const DPodX 
                 const size_t lds4n = bm + 5 * 2 * 64 * 8 + 2 * 64 * (sizeof(RowT<F>) + sizeof(int4)) + 2 * sizeof(ResPub) +
                                      64 * 4 + 64 * sizeof(PodT<F>) + 64 * sizeof(DPodX) + 64 * sizeof(NormInfo) +
                                      64 * sizeof(double2) + 2 * 64 * 4 + 2 * 64 * sizeof(RowX);
+                // (the resume of a stopped window runs inside the same launch: LDS for both)
+                const size_t ldsr = std::max(lds4n, ldsn);
                 if (diag)
-                    hipLaunchKernelGGL((k_la_resolve4<F, 1, true, false>), dim3(1), dim3(256), lds4n, stream, t, pods, c, s0, P,
-                                       K, GLp, geo.lr, sh, bf.lists, on, ok, st, diag, bf.dprev, bf.dcur, podx, bf.norm, bf.rec);
+                    hipLaunchKernelGGL((k_la_resolve4<F, 1, true, false>), dim3(1), dim3(256), ldsr, stream, t, pods, c, s0, P,
+                                       K, GLp, geo.lr, sh, bf.lists, on, ok, st, diag, bf.dprev, bf.dcur, podx, bf.norm, bf.rec, bf.nfall);
                 else if (geo.k32)
-                    hipLaunchKernelGGL((k_la_resolve4<F, 1, false, true>), dim3(1), dim3(256), lds4n, stream, t, pods, c, s0, P,
-                                       K, GLp, geo.lr, sh, bf.lists, on, ok, st, diag, bf.dprev, bf.dcur, podx, bf.norm, bf.rec);
+                    hipLaunchKernelGGL((k_la_resolve4<F, 1, false, true>), dim3(1), dim3(256), ldsr, stream, t, pods, c, s0, P,
+                                       K, GLp, geo.lr, sh, bf.lists, on, ok, st, diag, bf.dprev, bf.dcur, podx, bf.norm, bf.rec, bf.nfall);
                 else
-                    hipLaunchKernelGGL((k_la_resolve4<F, 1, false, false>), dim3(1), dim3(256), lds4n, stream, t, pods, c, s0, P,
-                                       K, GLp, geo.lr, sh, bf.lists, on, ok, st, diag, bf.dprev, bf.dcur, podx, bf.norm, bf.rec);
-                QS_RET(hipGetLastError());
-                hipLaunchKernelGGL((k_la_resolve_norm<F, 1>), dim3(1), dim3(64 * kResNormWaves), ldsn, stream, t, pods, podx, c, s0, P, K, GLp,
-                                   geo.lr, sh, bf.lists, bf.norm, on, ok, st, bf.dprev, bf.dcur, bf.nfall, bf.rec);
+                    hipLaunchKernelGGL((k_la_resolve4<F, 1, false, false>), dim3(1), dim3(256), ldsr, stream, t, pods, c, s0, P,
+                                       K, GLp, geo.lr, sh, bf.lists, on, ok, st, diag, bf.dprev, bf.dcur, podx, bf.norm, bf.rec, bf.nfall);
                 return hipGetLastError();
             }
             switch (geo.epl) {
@@ -3162,9 +3203,9 @@ static hipError_t la_window_f(const DevTable &t, const void *pods_, const DPodX 
                 if (diag) hipLaunchKernelGGL((k_la_resolve<F, EP, true>), dim3(1), dim3(64), lds, stream, t, pods, c, s0, P, K, GLp, geo.lr, sh, lists, on, ok, st, diag); \
                 else hipLaunchKernelGGL((k_la_resolve<F, EP, false>), dim3(1), dim3(64), lds, stream, t, pods, c, s0, P, K, GLp, geo.lr, sh, lists, on, ok, st, diag); \
             } else { \
-                if (diag) hipLaunchKernelGGL((k_la_resolve4<F, EP, true, false>), dim3(1), dim3(256), lds4, stream, t, pods, c, s0, P, K, GLp, geo.lr, sh, lists, on, ok, st, diag, dprev, dcur, nullptr, nullptr, nullptr); \
-                else if (geo.k32) hipLaunchKernelGGL((k_la_resolve4<F, EP, false, true>), dim3(1), dim3(256), lds4, stream, t, pods, c, s0, P, K, GLp, geo.lr, sh, lists, on, ok, st, diag, dprev, dcur, nullptr, nullptr, nullptr); \
-                else hipLaunchKernelGGL((k_la_resolve4<F, EP, false, false>), dim3(1), dim3(256), lds4, stream, t, pods, c, s0, P, K, GLp, geo.lr, sh, lists, on, ok, st, diag, dprev, dcur, nullptr, nullptr, nullptr); \
+                if (diag) hipLaunchKernelGGL((k_la_resolve4<F, EP, true, false>), dim3(1), dim3(256), lds4, stream, t, pods, c, s0, P, K, GLp, geo.lr, sh, lists, on, ok, st, diag, dprev, dcur, nullptr, nullptr, nullptr, nullptr); \
+                else if (geo.k32) hipLaunchKernelGGL((k_la_resolve4<F, EP, false, true>), dim3(1), dim3(256), lds4, stream, t, pods, c, s0, P, K, GLp, geo.lr, sh, lists, on, ok, st, diag, dprev, dcur, nullptr, nullptr, nullptr, nullptr); \
+                else hipLaunchKernelGGL((k_la_resolve4<F, EP, false, false>), dim3(1), dim3(256), lds4, stream, t, pods, c, s0, P, K, GLp, geo.lr, sh, lists, on, ok, st, diag, dprev, dcur, nullptr, nullptr, nullptr, nullptr); \
             } break;
             QS_RES(1) QS_RES(2) QS_RES(4) QS_RES(8) QS_RES(16)
 #undef QS_RES
