@@ -1808,11 +1808,12 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                 const bool pnew = pv.ks != 0 && pv.slot < 0;
                 const uint64_t sc = (lane == pv.slot) ? b : a;
                 uint64_t fk = ((uint32_t)lane < nd && sc) ? (sc | (uint64_t)(0xFFFFFFFFu - didx)) : 0ull;
-                if (pnew) {
-                    const uint64_t cw = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(cl >> 32), pv.src) << 32) |
-                                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)cl, pv.src);
-                    if ((uint32_t)lane == pv.nd_old) fk = cw;
-                }
+                // the new slot's key, read unconditionally (under a branch the compiler sank the
+                // keyC load into it: a second, dependent LDS round trip on D's chain)
+                const int srcl = pv.src >= 0 ? pv.src : 0;
+                const uint64_t cw = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(cl >> 32), srcl) << 32) |
+                                    (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)cl, srcl);
+                if (pnew && (uint32_t)lane == pv.nd_old) fk = cw;
                 const uint64_t cand = (pv.ks != 0 && e1 != 0 && key_node(e1) == pv.w) ? 0ull : e1;
                 const uint64_t best = fk > cand ? fk : cand;
                 uint64_t ks;
