@@ -1778,6 +1778,11 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
     PodT<F>(*wpods2)[64] = (PodT<F>(*)[64])base;  // window pod records, by window parity
     const ResPub none{0, 0xFFFFFFFFu, -1, -1, 0, {0, 0}};
     const DPodX px{};
+    // the LeastAllocated weights and weight-sum reciprocals held in VGPRs: the score's per-lane
+    // selects then read them directly (gfx950 VALU takes one scalar operand: from SGPRs every
+    // select needed a v_mov first, on every wave's critical path)
+    DevCfg cv = c;
+    asm volatile("" : "+v"(cv.yd_both), "+v"(cv.yd_c), "+v"(cv.yd_m), "+v"(cv.wc), "+v"(cv.wm));
     uint64_t ts_ = 0, busy_ = 0, steps_ = 0;
 
     for (uint32_t i = threadIdx.x; i < nwords; i += 256) dirty[i] = 0;
@@ -1892,7 +1897,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
         const __amdgpu_buffer_rsrc_t rs = row_rsrc(t);
         auto slot_key = [&](const RowT<F> &r, const RowX &x, const PodT<F> &q) -> uint64_t {
             const bool f = feasible<F>(r, x, q, px);
-            const uint32_t tot = node_total<F>(r, x, q, px, c, 0, 0.0, 0, 0.0, nullptr);
+            const uint32_t tot = node_total<F>(r, x, q, px, cv, 0, 0.0, 0, 0.0, nullptr);
             return ((uint32_t)lane < nd && f) ? ((uint64_t)(tot + 1) << 32) : 0ull;
         };
         auto apply = [&](const ResPub &pv, int pp, const PodT<F> &pprev) {
@@ -2028,7 +2033,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                 RowX crx = x1;
                 reserve(cr, crx, pcur, +1);
                 const bool f = feasible<F>(cr, crx, pn1, px);
-                const uint32_t tot = node_total<F>(cr, crx, pn1, px, c, 0, 0.0, 0, 0.0, nullptr);
+                const uint32_t tot = node_total<F>(cr, crx, pn1, px, cv, 0, 0.0, 0, 0.0, nullptr);
                 stage[par][lane] = r1;
                 if (F & kFeatExt) stagex[par][lane] = make_int4(x1.ae0, x1.re0, x1.ae1, x1.re1);
                 if (i + 1 < kend) {
