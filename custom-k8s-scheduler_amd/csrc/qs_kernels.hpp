@@ -1153,6 +1153,8 @@ __device__ __forceinline__ void la_resolve4_block(uint32_t *lds, const DevTable 
         }
     }
     const DPodX px{};
+    DevCfg cv = c;  // (weights in VGPRs, as in la_resolve4_stream)
+    asm volatile("" : "+v"(cv.yd_both), "+v"(cv.yd_c), "+v"(cv.yd_m), "+v"(cv.wc), "+v"(cv.wm));
     // Overlapped windows (dprev != nullptr): this window's lists were selected against the table
     // as it stood BEFORE the previous window, so the nodes that window dirtied (dprev[1..nd0])
     // start as dirty slots: their list entries are stale and their rows are re-read here.
@@ -1307,7 +1309,7 @@ __device__ __forceinline__ void la_resolve4_block(uint32_t *lds, const DevTable 
                 const NormInfo nf = pn.nf;
                 const double2 yr = pn.yr;
                 const bool f = feasible<F>(r, x, q, qx);
-                const uint32_t tot = node_total<F>(r, x, q, qx, c, nf.mt, yr.x, nf.ma, yr.y, nullptr);
+                const uint32_t tot = node_total<F>(r, x, q, qx, cv, nf.mt, yr.x, nf.ma, yr.y, nullptr);
                 uint32_t fl = 0;
                 if (act && !f) {
                     if (F & kFeatTaint) fl |= taint_raw(x, qx) == nf.mt ? 1u : 0u;
@@ -1316,7 +1318,7 @@ __device__ __forceinline__ void la_resolve4_block(uint32_t *lds, const DevTable 
                 return ((act && f) ? ((uint64_t)(tot + 1) << 32) : 0ull) | fl;
             }
             const bool f = feasible<F>(r, x, q, px);
-            const uint32_t tot = node_total<F>(r, x, q, px, c, 0, 0.0, 0, 0.0, nullptr);
+            const uint32_t tot = node_total<F>(r, x, q, px, cv, 0, 0.0, 0, 0.0, nullptr);
             return (act && f) ? ((uint64_t)(tot + 1) << 32) : 0ull;
         };
         if (wv == 1 && nd0 > 0) keyA[1][lane] = slot_key(S, SX, wpods[0], podn(0));  // pod 0, inherited slots
@@ -1444,7 +1446,7 @@ __device__ __forceinline__ void la_resolve4_block(uint32_t *lds, const DevTable 
                 RowX crx = x1;
                 reserve(cr, crx, pcurC, +1);
                 const bool f = feasible<F>(cr, crx, pn1, NORM ? qx : px);
-                const uint32_t tot = node_total<F>(cr, crx, pn1, NORM ? qx : px, c, nf.mt, yr.x, nf.ma, yr.y, nullptr);
+                const uint32_t tot = node_total<F>(cr, crx, pn1, NORM ? qx : px, cv, nf.mt, yr.x, nf.ma, yr.y, nullptr);
                 uint32_t fl = 0;
                 if (NORM && !f) {
                     if (F & kFeatTaint) fl |= taint_raw(crx, qx) == nf.mt ? 1u : 0u;
@@ -1510,7 +1512,7 @@ __device__ __forceinline__ void la_resolve4_block(uint32_t *lds, const DevTable 
                     const NormInfo nf = wnorm[i + 1];
                     const double2 yr = wrcp[i + 1];
                     const bool f = feasible<F>(cr, crx, pn1, qx);
-                    const uint32_t tot = node_total<F>(cr, crx, pn1, qx, c, nf.mt, yr.x, nf.ma, yr.y, nullptr);
+                    const uint32_t tot = node_total<F>(cr, crx, pn1, qx, cv, nf.mt, yr.x, nf.ma, yr.y, nullptr);
                     keyC[par][lane] = (cc != 0 && f) ? pack_key(tot + 1, key_node(cc)) : 0ull;
                     uint32_t fl = 0;
                     if (!f) {
@@ -1520,7 +1522,7 @@ __device__ __forceinline__ void la_resolve4_block(uint32_t *lds, const DevTable 
                     flagC[par][lane] = fl;
                 } else {
                     const bool f = feasible<F>(cr, crx, pn1, px);
-                    const uint32_t tot = node_total<F>(cr, crx, pn1, px, c, 0, 0.0, 0, 0.0, nullptr);
+                    const uint32_t tot = node_total<F>(cr, crx, pn1, px, cv, 0, 0.0, 0, 0.0, nullptr);
                     keyC[par][lane] = (cc != 0 && f) ? pack_key(tot + 1, key_node(cc)) : 0ull;
                 }
             }
@@ -1652,6 +1654,8 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
     const int tid = threadIdx.x, lane = tid & 63, w8 = tid >> 6;
     const __amdgpu_buffer_rsrc_t rs = row_rsrc(t);
     const DPodX px{};
+    DevCfg cv = c;  // (weights in VGPRs, as in la_resolve4_stream)
+    asm volatile("" : "+v"(cv.yd_both), "+v"(cv.yd_c), "+v"(cv.yd_m), "+v"(cv.wc), "+v"(cv.wm));
     for (uint32_t w = 0; w < nwin; ++w) {
         const uint32_t s0 = w * K, kw = min(K, P - s0), b = w & 1;
         if (sid >= kw * G) continue;  // no task of this window (uniform per block)
@@ -1677,7 +1681,7 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
                     RowX x;
                     const Row r = load_row_coh<F>(t, rs, idx, x);
                     const bool f = feasible<F>(r, x, p, px);
-                    const uint32_t tot = node_total<F>(r, x, p, px, c, 0, 0.0, 0, 0.0, nullptr);
+                    const uint32_t tot = node_total<F>(r, x, p, px, cv, 0, 0.0, 0, 0.0, nullptr);
                     tv[j] = f ? tot + 1 : 0;
                 }
             }
