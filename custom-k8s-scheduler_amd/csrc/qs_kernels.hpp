@@ -622,12 +622,6 @@ __global__ __launch_bounds__(256) void k_la_merge(const uint64_t *__restrict__ c
 // Entry m (0 <= m < EPL) of resolver lane `lane` for window pod `pod`.  Lists are laid out
 // [shard][pod][GLp] (GLp = 64 * 2^lr entries per pod and shard: the all-gathered layout of the
 // sharded engine); entries of shards >= W read as empty.
-// Address of entry m of lane `lane` (the entry must exist: m >> lr < W).
-__device__ __forceinline__ const uint64_t &list_ref(const uint64_t *lists, uint32_t pod, uint32_t GLp, uint32_t lr,
-                                                   const LaShard &sh, int m, int lane) {
-    const uint32_t q = (uint32_t)m >> lr;
-    return lists[(size_t)q * sh.RS + (size_t)pod * GLp + (uint32_t)lane + 64u * ((uint32_t)m & ((1u << lr) - 1u))];
-}
 __device__ __forceinline__ uint64_t list_ent(const uint64_t *__restrict__ lists, uint32_t pod,
                                              uint32_t GLp, uint32_t lr, const LaShard &sh, int m,
                                              int lane) {
@@ -1097,7 +1091,7 @@ __device__ __forceinline__ ResPub read_pub(const ResPub *p) {
     return r;
 }
 
-template <uint32_t F, int EPL, bool DIAG, bool K32, bool RES = false>
+template <uint32_t F, int EPL, bool DIAG, bool K32>
 __device__ __forceinline__ void la_resolve4_block(uint32_t *lds, const DevTable &t, const PodT<F> *__restrict__ pods,
                                                   const DevCfg &c, uint32_t s0, uint32_t P,
                                                   uint32_t K, uint32_t GLp, uint32_t lr,
@@ -1372,12 +1366,8 @@ __device__ __forceinline__ void la_resolve4_block(uint32_t *lds, const DevTable 
         __syncthreads();  // slotnode written by wave D
         if (wv == 1 && (uint32_t)lane < nd) {
             const uint32_t node = slotnode[lane];
-            if constexpr (RES) {  // resident stream: the selectors read these rows in this launch
-                store_row_coh<F>(t, row_rsrc(t), node, S, SX);
-            } else {
-                store_dyn<F>(t, node, S);
-                store_dynx<F>(t, node, SX);
-            }
+            store_dyn<F>(t, node, S);
+            store_dynx<F>(t, node, SX);
         }
     } else {
         // ---- C: candidate rows, C keys, next pod's top-2 ------------------------------------
@@ -1400,12 +1390,7 @@ __device__ __forceinline__ void la_resolve4_block(uint32_t *lds, const DevTable 
         };
         auto load_ent = [&](uint64_t(&e)[EPL], uint32_t pod) {
 #pragma unroll
-            for (int m = 0; m < EPL; ++m) {
-                if constexpr (RES)  // resident stream: lists handed off inside the launch (sc1 loads)
-                    e[m] = pod < kend ? load_coh_u64(&list_ref(lists, pod, GLp, lr, sh, m, lane)) : 0ull;
-                else
-                    e[m] = pod < kend ? list_ent(lists, pod, GLp, lr, sh, m, lane) : 0ull;
-            }
+            for (int m = 0; m < EPL; ++m) e[m] = pod < kend ? list_ent(lists, pod, GLp, lr, sh, m, lane) : 0ull;
         };
         uint64_t c1, c2;
         uint64_t eX[EPL], eY[EPL];  // ping-pong: entries consumed two pods after their load
