@@ -171,6 +171,7 @@ def diag_runs(cx, nodes, pods, cfg, sharded):
     s2 = open_sched(cx, dict(cfg, record_timestamps=1), sharded)
     s2.load_nodes(nodes)
     st2 = s2.prepare(pods)
+    cx.barrier()  # every rank's first window within the exchange's wait bound
     st2.run()
     d = np.diff(st2.stamps().astype(np.int64)) * 0.01  # 100 MHz s_memrealtime ticks -> us
     p50, p99 = float(np.percentile(d, 50)), float(np.percentile(d, 99))
@@ -179,6 +180,7 @@ def diag_runs(cx, nodes, pods, cfg, sharded):
     s3 = open_sched(cx, dict(cfg, profile_kernels=1), sharded)
     s3.load_nodes(nodes)
     st3 = s3.prepare(pods)
+    cx.barrier()
     r3 = st3.run()
     kp = r3["kernels"]
     if r3.get("resident") and "resolve" in kp:  # one resident launch
@@ -281,6 +283,9 @@ def measure(cx, a, workload, steps, warmup, with_diag=True):
         s.restore_table()
         return st.run(mode=mode)
 
+    # all ranks enter their first run together: a sharded rank's first window waits (bounded) for
+    # its peers' lists, and a one-sided timeout would void only that rank's run
+    cx.barrier()
     for _ in range(warmup):
         step()
     cx.barrier()
@@ -290,7 +295,8 @@ def measure(cx, a, workload, steps, warmup, with_diag=True):
         last = step()
     cx.barrier()
     elapsed = cx.max(time.perf_counter() - t0)
-    placement, _ = st.results()
+    placement, keys = st.results()
+    final = s.read_nodes()  # the table after the last timed step (which started from the snapshot)
     st.free()
     s.close()
     ranks_work = cx.world if (cx.world > 1 and not sharded) else 1  # replicas multiply the work
@@ -299,13 +305,42 @@ def measure(cx, a, workload, steps, warmup, with_diag=True):
            "launch": "resident" if last.get("resident") else "per-window",
            "table_layout": last["table_layout"],
            "unschedulable_frac": float((placement < 0).mean()), "n_nodes": n_nodes,
-           "placement": placement.copy(),
+           "placement": placement.copy(), "keys": keys, "final": final, "cfg": cfg,
            "n_pods": n_pods, "desc": desc, "sharded": sharded, "nodes": nodes, "pods": pods,
            "replicas": ranks_work}
     if with_diag:
         out["p50"], out["p99"], out["kp"] = diag_runs(cx, nodes, pods, cfg, sharded)
         out["wall_fallback"] = last["wall_s"]
     return out
+
+
+def check_stream(m):
+    """Correctness of a timed leg: the oracle over the WHOLE stream, diffed
+    against the GPU's placements, per-pod keys and final table, plus qsched.checks' size-independent
+    invariants.  Fit + Balanced profiles use or_schedule_incremental (the brute-force oracle's
+    node_key() with an incremental argmax: seconds for config 3's 1,000,000 x 50,000), normalizing
+    profiles the brute-force oracle with 16 threads."""
+    from oracle import oracle as O
+    from qsched.checks import stream_invariants
+
+    norm = bool(m["cfg"].get("enable_taint") or m["cfg"].get("enable_affinity"))
+    ocfg = {k: m["cfg"][k] for k in ("enable_taint", "enable_affinity") if k in m["cfg"]}
+    on = {k: v.copy() for k, v in m["nodes"].items()}
+    sub = qsched.pods_from_struct(m["pods"])
+    t0 = time.perf_counter()
+    if norm:
+        ref, rkeys, _ = O.schedule(on, sub, ocfg, nthreads=16)
+        how = "oracle/qs_oracle.c or_schedule, 16 OpenMP threads"
+    else:
+        ref, rkeys, _ = O.schedule_incremental(on, sub, ocfg, nthreads=16)
+        how = "oracle/qs_oracle.c or_schedule_incremental, 16 OpenMP threads"
+    dt = time.perf_counter() - t0
+    inv = stream_invariants(m["nodes"], m["pods"], m["placement"], m["final"], fit_only=not norm)
+    return {"placements_match": bool(np.array_equal(ref, m["placement"])),
+            "keys_match": bool(np.array_equal(rkeys, m["keys"])),
+            "table_match": all(bool(np.array_equal(on[k], m["final"][k])) for k in on),
+            "oracle": how, "oracle_s": round(dt, 2),
+            "invariants": {k: v for k, v in inv.items() if v is not None}}
 
 
 def scan_roofline(cx, a, n_nodes=1 << 24, n_pods=32):
@@ -501,18 +536,23 @@ def main():
             "roofline": rl,
             "kernels_us_per_step": {k: round(v["s"] * 1e6, 1) for k, v in m["kp"].items()},
         }
+        if m["sharded"] or (cx.world == 1 and not a.no_cpu):
+            out["check"] = check_stream(m)
         if c3 is not None:
             out["config3"] = {"workload": c3["desc"] + " (1 GPU: the N=1 point of the curve)",
                               "value": round(c3["value"], 1), "unit": "pods/s",
                               "evals_per_s": round(c3["value"] * c3["n_nodes"], 1),
                               "ms_per_step": round(c3["ms_per_step"], 3), "steps": 1,
-                              "engine": c3["engine"], "launch": c3["launch"]}
+                              "engine": c3["engine"], "launch": c3["launch"],
+                              "unschedulable_frac": round(c3["unschedulable_frac"], 5),
+                              "check": check_stream(c3)}
         if c4 is not None:
             out["config4"] = {"workload": c4["desc"], "value": round(c4["value"], 1), "unit": "pods/s",
                               "evals_per_s": round(c4["value"] * c4["n_nodes"], 1),
                               "ms_per_step": round(c4["ms_per_step"], 3), "steps": 3,
                               "engine": c4["engine"], "launch": c4["launch"],
-                              "unschedulable_frac": round(c4["unschedulable_frac"], 5)}
+                              "unschedulable_frac": round(c4["unschedulable_frac"], 5),
+                              "check": check_stream(c4)}
         if c5 is not None:
             out["config5_batched"] = {"workload": c5["desc"], "value": round(c5["value"], 1),
                                       "unit": "pods/s", "evals_per_s": round(c5["value"] * c5["n_nodes"], 1),

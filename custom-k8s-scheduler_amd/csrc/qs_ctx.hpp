@@ -145,6 +145,9 @@ struct qs_ctx {
     qs_host::DevBuf mbox, mbox_peers;
     std::vector<void *> mbox_opened;
     bool mbox_on = false;
+    bool mbox_fine = false;  // the mailbox is fine-grained device memory (hipDeviceMallocFinegrained)
+    bool mbox_broken = false;  // a mailbox wait timed out: the ranks are out of step until every
+                               // rank calls qs_dist_mailbox_connect again
 };
 
 namespace qs_host {

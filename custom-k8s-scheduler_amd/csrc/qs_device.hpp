@@ -96,6 +96,10 @@ struct DevCfg {
     const uint64_t *ready;
     uint64_t epoch;  // the run's sequence number (host counter)
     uint32_t *werr;  // set to 1 when a wait times out (the run returns QS_ETIMEOUT)
+    // Test hook (QS_INJECT_FAULT=resident_stall, tests/test_gpu_recovery.py): 1 = the selectors of
+    // the resident stream never deliver window 3's first task, so the resolver's wait times out
+    // and the in-kernel werr drain runs for real.  0 in every normal run.
+    uint32_t inject;
 };
 
 // Resolver prologue: thread 0 spins (s_sleep) until window s0/K's lists are published, then every

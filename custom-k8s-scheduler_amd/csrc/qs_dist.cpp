@@ -69,14 +69,19 @@ __global__ __launch_bounds__(256) void k_mbox_put(char *const *__restrict__ peer
 }
 
 // Waits until every rank's flag[phase] in this rank's mailbox reaches seq (0.5 s bound: *werr = 1).
+// Once a wait of the run has timed out, later waits return at once: the run is void anyway, and
+// a dead peer would otherwise cost the bound once per remaining window.
+// The bound is 0.5 s per window, and 5 s for a run's first window, whose peers may still be in
+// their host-side preparation.
 __global__ void k_mbox_wait(const uint64_t *__restrict__ flags, uint32_t world, uint32_t phase, uint64_t seq,
-                            uint32_t *__restrict__ werr) {
+                            uint32_t *__restrict__ werr, uint64_t bound) {
     if (threadIdx.x != 0) return;
+    if (__hip_atomic_load(werr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (uint32_t r = 0; r < world; ++r)
         while (__hip_atomic_load(flags + phase * kMbRanks + r, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < seq) {
             __builtin_amdgcn_s_sleep(2);
-            if (__builtin_amdgcn_s_memrealtime() - t0 > 50000000ull) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > bound) {
                 __hip_atomic_store(werr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 return;
             }
@@ -90,8 +95,9 @@ void mbox_exchange(qs_ctx *c, int phase, uint32_t slot, size_t block_bytes, uint
     hipLaunchKernelGGL(k_mbox_put, dim3(c->world), dim3(256), 0, stream, c->mbox_peers.as<char *>(),
                        (uint32_t)c->rank, region, block_bytes, pods, L, (uint32_t)phase, seq);
     HIPCHK(hipGetLastError());
+    const bool first = (uint32_t)seq == 1u;  // window 0 of the run (seq = run << 32 | w + 1)
     hipLaunchKernelGGL(k_mbox_wait, dim3(1), dim3(64), 0, stream, c->mbox.as<uint64_t>(), (uint32_t)c->world,
-                       (uint32_t)phase, seq, werr);
+                       (uint32_t)phase, seq, werr, first ? 500000000ull : 50000000ull);
     HIPCHK(hipGetLastError());
 }
 
@@ -138,7 +144,24 @@ qs_status qs_dist_mailbox_export(qs_ctx *c, uint8_t handle[64]) {
     try {
         HIPCHK(hipSetDevice(c->device));
         if (!c->mbox.p) {
-            c->mbox.ensure(kMbBytes);
+            // Fine-grained device memory: peers write it over xGMI while this GPU polls
+            // its flags and reads its slots, so it must stay coherent with remote writers without
+            // relying on the coarse-grained L2's write-back/invalidate points.  If this pool
+            // cannot export a fine-grained allocation, fall back to hipMalloc (the sc1 / system-scope
+            // accesses of the kernels remain); c->mbox_fine records which one is in use.
+            void *p = nullptr;
+            hipIpcMemHandle_t probe;
+            if (hipExtMallocWithFlags(&p, kMbBytes, hipDeviceMallocFinegrained) == hipSuccess &&
+                hipIpcGetMemHandle(&probe, p) == hipSuccess) {
+                c->mbox.p = p;
+                c->mbox.bytes = kMbBytes;
+                c->mbox_fine = true;
+            } else {
+                if (p) (void)hipFree(p);
+                (void)hipGetLastError();
+                c->mbox.ensure(kMbBytes);
+                c->mbox_fine = false;
+            }
             HIPCHK(hipMemset(c->mbox.p, 0, kMbBytes));
             HIPCHK(hipDeviceSynchronize());
         }
@@ -160,6 +183,16 @@ qs_status qs_dist_mailbox_connect(qs_ctx *c, const uint8_t *handles) {
         if (!c->mbox.p) fail(QS_ESTATE, "qs_dist_mailbox_export first");
         if (c->comm) fail(QS_ESTATE, "this context already uses RCCL");
         HIPCHK(hipSetDevice(c->device));
+        // (re)connect: a second call after a mailbox timeout brings the ranks back in step — every
+        // rank's runs have returned (no write is in flight), the caller barriers before and after
+        // this call on every rank, and each rank restarts from an empty mailbox and sequence 0
+        for (void *p : c->mbox_opened) (void)hipIpcCloseMemHandle(p);
+        c->mbox_opened.clear();
+        c->mbox_on = false;
+        HIPCHK(hipMemset(c->mbox.p, 0, kMbBytes));
+        HIPCHK(hipDeviceSynchronize());
+        c->run_seq = 0;
+        c->mbox_broken = false;
         std::vector<char *> bases((size_t)c->world);
         for (int r = 0; r < c->world; ++r) {
             if (r == c->rank) {

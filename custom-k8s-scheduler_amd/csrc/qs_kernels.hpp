@@ -1652,6 +1652,7 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
         uint64_t *lists = lists0 + (size_t)b * lwords;
         uint64_t *clists = clists0 + (size_t)b * cwords;
         for (uint32_t task = sid; task < kw * G; task += S) {
+            if (c.inject == 1u && w == 3 && task == 0) continue;  // test hook: window 3 never completes
             const uint32_t k = task / G, g = task % G;
             if (rdiag) ts0 = __builtin_amdgcn_s_memrealtime();
             const PodT<F> p = pods[s0 + k];
@@ -2136,679 +2137,23 @@ static hipError_t la_stream_res_f(const DevTable &t, const void *pods, const Dev
 }
 constexpr size_t kResCtlBytes = sizeof(ResCtl);
 
-// =============================================================================================
-// Speculative batch resolver: Fit + Balanced (+ extended resources) profiles,
-// unsharded sorted lists.  The window is resolved in batches of up to four pods, one per wave
-// (wave w owns the window's pods p ≡ w (mod 4)).  Speculation: every pod of a batch takes its
-// best clean list entry (lists are sorted best-first, so: its first clean lane) that no earlier
-// pod of the batch took.  Each wave then scores its pod exactly against every dirty node (the
-// slots, replicated in every wave's lanes) and against the batch's earlier candidates reserved
-// with their pods.  The first pod whose best dirty key beats its candidate is resolved by that
-// key — exact, because every earlier pod of the batch did take its candidate — and ends the
-// batch; the pods before it commit their candidates as new slots.  Two barriers per batch; in
-// config 2 about 84 % of the pods take their clean candidate, i.e. ~3 pods per batch.
-// =============================================================================================
-constexpr uint32_t kSpecM = 4;  // pods per batch = waves
-constexpr uint32_t kSpecRing = 4;  // list ring slots per wave (pod ordinals in flight)
-// Candidate record: its list key and where its row sits in the row ring.
-struct alignas(16) SpecCand {
-    uint64_t key;
-    uint32_t ring;  // row ring index ((wave * kSpecRing + slot) * 64 + lane)
-    uint32_t pad;
-};
-// Dynamic LDS: dirty bitmap | row ring [4][4][64] R | ext ring [4][4][64] int4 (kFeatExt) |
-// key ring [4][4][64] u64 | cand [2][4][4] | resk [4] u64 | ccount [2][4] u32 | pods [64].
+// Workgroups of the instantiation la_stream_res_f would launch that the occupancy API admits per
+// CU (every workgroup of the launch carries the resolver's dynamic LDS); 0 if not instantiated.
 template <uint32_t F>
-constexpr size_t spec_lds_bytes(uint32_t n) {
-    constexpr size_t ring = (size_t)kSpecM * kSpecRing * 64;
-    return (((size_t)(n + 31) / 32 + 3) & ~(size_t)3) * 4 + ring * sizeof(RowT<F>) +
-           ((F & kFeatExt) ? ring * sizeof(int4) : 0) + ring * 8 + 2 * kSpecM * kSpecM * sizeof(SpecCand) +
-           8 * kSpecM + 4 * 2 * kSpecM + 64 * sizeof(PodT<F>);
-}
-
-template <uint32_t F, bool K32, bool DIAG>
-__global__ __launch_bounds__(64 * kSpecM) void k_la_resolve_spec(
-    DevTable t, const PodT<F> *__restrict__ pods, DevCfg c, uint32_t s0, uint32_t P, uint32_t K,
-    uint32_t GLp, const uint64_t *__restrict__ lists, int32_t *__restrict__ out_node,
-    uint64_t *__restrict__ out_key, uint64_t *__restrict__ stamps, const uint32_t *__restrict__ dprev,
-    uint32_t *__restrict__ dcur, uint64_t *__restrict__ diag) {
-    wait_lists_ready(c, s0, K);
-    uint64_t dph[3] = {0, 0, 0}, dnb = 0, dfail = 0, tprev = 0;
-    const uint64_t t_start = DIAG ? diag_stamp() : 0ull;
-    using R = RowT<F>;
-    using PD = PodT<F>;
-    constexpr bool EXT = (F & kFeatExt) != 0;
-    constexpr uint32_t kRing = kSpecM * kSpecRing * 64;
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    const int lane = threadIdx.x & 63;
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t n = t.n, nwords = (n + 31) / 32;
-    uint32_t *dirty = lds;
-    char *base = (char *)(lds + ((nwords + 3) & ~3u));
-    R *rring = (R *)base;  // rows of the wave's pods' list entries, by pod ordinal mod 4
-    base += kRing * sizeof(R);
-    int4 *xring = (int4 *)base;  // their extended-resource columns
-    if (EXT) base += kRing * sizeof(int4);
-    uint64_t *kring = (uint64_t *)base;  // their list keys
-    base += kRing * 8;
-    SpecCand(*cand)[kSpecM][kSpecM] = (SpecCand(*)[kSpecM][kSpecM])base;  // [step parity][wave][rank]
-    base += 2 * kSpecM * kSpecM * sizeof(SpecCand);
-    uint64_t *resk = (uint64_t *)base;  // [batch position] best dirty key
-    base += 8 * kSpecM;
-    uint32_t *ccount = (uint32_t *)base;  // [step parity][wave] clean candidates found (<= 4)
-    base += 4 * 2 * kSpecM;
-    PD *wpods = (PD *)base;  // the window's pod records (K <= 64)
-    const DPodX px{};
-    const uint32_t kend = min(K, P - s0);
-    auto ridx = [&](uint32_t w, uint32_t ord, uint32_t l) { return (w * kSpecRing + (ord & (kSpecRing - 1))) * 64 + l; };
-    auto fetch_key = [&](uint32_t ord) -> uint64_t {
-        const uint32_t j = wv + kSpecM * ord;
-        return j < kend ? lists[(size_t)j * GLp + lane] : 0ull;
-    };
-    for (uint32_t i = threadIdx.x; i < nwords; i += 64 * kSpecM) dirty[i] = 0;
-    if (threadIdx.x < kend) wpods[threadIdx.x] = pods[s0 + threadIdx.x];
-    // slots (dirty nodes, one per lane), replicated bit for bit in every wave: the nodes the
-    // previous (overlapped) window dirtied first
-    const uint32_t nd0 = dprev ? dprev[0] : 0u;
-    uint32_t nd = nd0;
-    uint32_t sidx = (uint32_t)lane < nd0 ? dprev[1 + lane] : 0xFFFFFFFFu;
-    R S = empty_row<F>();
-    RowX SX{};
-    if ((uint32_t)lane < nd0) {
-        S = load_row<F>(t, sidx);
-        SX = load_rowx<F>(t, sidx);
+static int la_stream_res_per_cu(const LaGeom &geo, uint32_t n) {
+    const size_t lds4 = res_stream_lds_bytes<F>(n);
+    const void *fn = nullptr;
+#define QS_RESP(EE, KK) \
+    if (geo.E == EE && (geo.k32 != 0) == KK) fn = (const void *)k_la_stream_res<F, EE, 1, KK>;
+    QS_RESP(3, true) QS_RESP(3, false) QS_RESP(5, true) QS_RESP(5, false)
+    QS_RESP(8, true) QS_RESP(8, false) QS_RESP(16, true) QS_RESP(16, false)
+#undef QS_RESP
+    int per = 0;
+    if (!fn || hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, kResBS, lds4) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
     }
-    bool won = false;  // slot won a pod of THIS window (handed to the next window's dprev)
-    // This wave's pods j = wv + 4m (ordinal m).  Keys and rows of their list entries live in LDS
-    // rings; every step re-issues, unconditionally, the key load of ordinal m+3 (kT) and the row
-    // loads of ordinal m+2 (T) and stores the previous step's ones: no load is waited for in the
-    // step that issues it, and no loaded register is carried conditionally.
-    {
-        uint64_t k0 = fetch_key(0), k1 = fetch_key(1), k2 = fetch_key(2);
-        kring[ridx(wv, 0, lane)] = k0;
-        kring[ridx(wv, 1, lane)] = k1;
-        kring[ridx(wv, 2, lane)] = k2;
-        const uint32_t a0 = k0 ? key_node(k0) : 0u, a1 = k1 ? key_node(k1) : 0u;
-        const R ra = load_row<F>(t, a0), rb = load_row<F>(t, a1);
-        const RowX xa = load_rowx<F>(t, a0), xb = load_rowx<F>(t, a1);
-        rring[ridx(wv, 0, lane)] = ra;
-        rring[ridx(wv, 1, lane)] = rb;
-        if (EXT) {
-            xring[ridx(wv, 0, lane)] = make_int4(xa.ae0, xa.re0, xa.ae1, xa.re1);
-            xring[ridx(wv, 1, lane)] = make_int4(xb.ae0, xb.re0, xb.ae1, xb.re1);
-        }
-    }
-    uint32_t mo = 0, oT = 2, oK = 3;
-    uint64_t kT = fetch_key(3);
-    R T;
-    RowX TX;
-    {
-        const uint64_t k2 = kring[ridx(wv, 2, lane)];
-        const uint32_t a2 = k2 ? key_node(k2) : 0u;
-        T = load_row<F>(t, a2);
-        TX = load_rowx<F>(t, a2);
-    }
-    __syncthreads();
-    if (threadIdx.x < nd0) atomicOr(&dirty[sidx >> 5], 1u << (sidx & 31));
-    uint64_t res_key = 0, res_stamp = 0;  // wave 0, lane k: window pod k's result
-    uint32_t newd[kSpecM] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};  // last batch's new slots
-    uint32_t i = 0;
-    int par = 0;
-    __syncthreads();
-    if (DIAG) {
-        tprev = diag_stamp();
-        if (threadIdx.x == 0) atomicAdd((unsigned long long *)&diag[8], (unsigned long long)(tprev - t_start));
-    }
-    while (i < kend) {
-        const uint32_t bn = min(kSpecM, kend - i);
-        const uint32_t k_me = (wv - i) & (kSpecM - 1);  // my pod = i + k_me (ordinal mo)
-        // ---- ring upkeep: store last step's loads, issue this step's (ordinals mo+2, mo+3)
-        kring[ridx(wv, oK, lane)] = kT;
-        rring[ridx(wv, oT, lane)] = T;
-        if (EXT) xring[ridx(wv, oT, lane)] = make_int4(TX.ae0, TX.re0, TX.ae1, TX.re1);
-        oK = mo + 3;
-        oT = mo + 2;
-        kT = fetch_key(oK);
-        {
-            const uint64_t kk = kring[ridx(wv, oT, lane)];
-            const uint32_t a = kk ? key_node(kk) : 0u;
-            T = load_row<F>(t, a);
-            TX = load_rowx<F>(t, a);
-        }
-        // ---- phase 1: my pod's top-4 clean entries (dirty: bitmap + the last batch's new slots)
-        if (k_me < bn) {
-            const uint64_t e = kring[ridx(wv, mo, lane)];
-            const uint32_t node = e ? key_node(e) : 0u;
-            bool cl = e != 0 && !((dirty[node >> 5] >> (node & 31)) & 1u);
-#pragma unroll
-            for (uint32_t q = 0; q < kSpecM; ++q) cl &= node != newd[q];
-            const uint64_t B = __ballot(cl);
-            const uint32_t rank = (uint32_t)__popcll(B & ((1ull << lane) - 1ull));
-            if (cl && rank < kSpecM) cand[par][wv][rank] = SpecCand{e, ridx(wv, mo, lane), 0u};
-            if (lane == 0) ccount[par * kSpecM + wv] = min((uint32_t)__popcll(B), kSpecM);
-        }
-        if (DIAG) { const uint64_t t_ = diag_stamp(); dph[0] += t_ - tprev; tprev = t_; }
-        __syncthreads();
-        // ---- phase 2 (every wave): the batch's candidates in pod order, replayed identically
-        const uint32_t q = (uint32_t)lane & (kSpecM * kSpecM - 1);
-        const uint32_t qw = q / kSpecM, qr = q % kSpecM;
-        const SpecCand qc = cand[par][qw][qr];
-        const uint64_t qkey = qr < ccount[par * kSpecM + qw] ? qc.key : 0ull;
-        const uint32_t qnode = qkey ? key_node(qkey) : 0xFFFFFFFFu;
-        uint64_t ck[kSpecM];
-        uint32_t cring[kSpecM], cpos[kSpecM];
-        uint32_t ncand = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < kSpecM; ++k) {
-            ck[k] = 0;
-            cring[k] = 0;
-            cpos[k] = 0xFFFFFFFFu;
-            if (k < bn) {
-                bool ok = lane < (int)(kSpecM * kSpecM) && qw == ((i + k) & (kSpecM - 1)) && qkey != 0;
-#pragma unroll
-                for (uint32_t t2 = 0; t2 < kSpecM; ++t2)
-                    ok &= !(t2 < k && ck[t2] != 0 && qnode == key_node(ck[t2]));
-                const uint64_t m = __ballot(ok);
-                if (m) {
-                    const int src = (int)__builtin_ctzll(m);
-                    ck[k] = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(qkey >> 32), src) << 32) |
-                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)qkey, src);
-                    cring[k] = (uint32_t)__builtin_amdgcn_readlane((int)qc.ring, src);
-                    cpos[k] = ncand++;
-                }
-            }
-        }
-        // candidate lanes nd + cpos[t]: candidate t's row reserved with pod t (every wave keeps
-        // them: the committed ones become slots in phase 3)
-        const int ct = lane - (int)nd;  // candidate ordinal of this lane
-        uint32_t tl = 0xFFFFFFFFu, tr = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < kSpecM; ++k)
-            if (ct >= 0 && (uint32_t)ct == cpos[k]) { tl = k; tr = cring[k]; }
-        R Rc = empty_row<F>();
-        RowX Xc{};
-        if (tl != 0xFFFFFFFFu) {
-            Rc = rring[tr];
-            if (EXT) {
-                const int4 e = xring[tr];
-                Xc.ae0 = e.x; Xc.re0 = e.y; Xc.ae1 = e.z; Xc.re1 = e.w;
-            }
-            reserve(Rc, Xc, wpods[i + tl], +1);
-        }
-        if (k_me < bn) {
-            // my pod vs every dirty node: the slots, and the candidates of the batch's earlier pods
-            const PD p = wpods[i + k_me];
-            const bool act = (uint32_t)lane < nd || tl < k_me;
-            const R rr = sel_row((uint32_t)lane < nd, S, Rc);
-            const RowX xx = sel_rowx((uint32_t)lane < nd, SX, Xc);
-            uint32_t node = sidx;
-#pragma unroll
-            for (uint32_t k = 0; k < kSpecM; ++k)
-                if (tl == k) node = ck[k] ? key_node(ck[k]) : 0u;
-            const bool f = act && feasible<F>(rr, xx, p, px);
-            const uint32_t tot = node_total<F>(rr, xx, p, px, c, 0, 0.0, 0, 0.0, nullptr);
-            const uint64_t key = f ? pack_key(tot + 1, node) : 0ull;
-            uint64_t best;
-            if (K32) {  // (score+1) < 2^10 and n <= 2^22: one 32-bit reduction
-                const uint32_t tv = (uint32_t)(key >> 32);
-                const uint32_t k32 = tv ? (tv << 22) | (0x3FFFFFu - key_node(key)) : 0u;
-                const uint32_t m = wave_max_u32(k32);
-                best = m ? (((uint64_t)(m >> 22) << 32) | (uint64_t)(0xFFFFFFFFu - (0x3FFFFFu - (m & 0x3FFFFFu)))) : 0ull;
-            } else {
-                best = wave_max_u64(key);
-            }
-            if (lane == 0) resk[k_me] = best;
-        }
-        if (DIAG) { const uint64_t t_ = diag_stamp(); dph[1] += t_ - tprev; tprev = t_; }
-        __syncthreads();
-        // ---- phase 3 (every wave, identical): commit the batch up to its first dirty win
-        uint32_t committed = bn, fail = 0xFFFFFFFFu;
-        uint64_t fkey = 0;
-        uint64_t rk[kSpecM];
-#pragma unroll
-        for (uint32_t k = 0; k < kSpecM; ++k) {
-            rk[k] = 0;
-            if (k < bn && fail == 0xFFFFFFFFu) {
-                const uint64_t bd = resk[k];
-                if (bd > ck[k]) {  // a dirty node beats the clean candidate: pod k is exact, stop
-                    fail = k;
-                    fkey = bd;
-                    rk[k] = bd;
-                    committed = k + 1;
-                } else {
-                    rk[k] = ck[k];  // the candidate (0: unschedulable)
-                }
-            }
-        }
-        // new slots: the committed candidates (pods before the failing one)
-        uint32_t nadd = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < kSpecM; ++k) {
-            const bool take = k < committed && k != fail && ck[k] != 0;
-            newd[k] = take ? key_node(ck[k]) : 0xFFFFFFFFu;
-            nadd += take ? 1u : 0u;
-        }
-        if (tl != 0xFFFFFFFFu && tl < committed && tl != fail) {
-            S = Rc;
-            SX = Xc;
-            sidx = key_node(ck[tl]);
-            won = true;
-        }
-        nd += nadd;  // committed candidates hold the lanes nd .. nd + nadd - 1 (cpos order)
-        if (fail != 0xFFFFFFFFu) {  // the failing pod's dirty winner takes it
-            const uint32_t w = key_node(fkey);
-            const uint64_t own = __ballot((uint32_t)lane < nd && sidx == w);
-            if (lane == (int)__builtin_ctzll(own)) {
-                reserve(S, SX, wpods[i + fail], +1);
-                won = true;
-            }
-        }
-        if (wv == 0) {
-            if (lane == 0) {
-#pragma unroll
-                for (uint32_t k = 0; k < kSpecM; ++k)
-                    if (newd[k] != 0xFFFFFFFFu) atomicOr(&dirty[newd[k] >> 5], 1u << (newd[k] & 31));
-            }
-            const uint64_t now = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
-#pragma unroll
-            for (uint32_t k = 0; k < kSpecM; ++k)
-                if (k < committed && (uint32_t)lane == i + k) { res_key = rk[k]; res_stamp = now; }
-        }
-        if (wv + kSpecM * mo < i + committed) ++mo;  // my pod committed
-        i += committed;
-        par ^= 1;
-        if (DIAG) {
-            const uint64_t t_ = diag_stamp();
-            dph[2] += t_ - tprev;
-            tprev = t_;
-            ++dnb;
-            dfail += fail != 0xFFFFFFFFu ? 1u : 0u;
-        }
-    }
-    if (DIAG && threadIdx.x == 0) {
-        for (int k = 0; k < 3; ++k) atomicAdd((unsigned long long *)&diag[k], (unsigned long long)dph[k]);
-        atomicAdd((unsigned long long *)&diag[3], (unsigned long long)dnb);
-        atomicAdd((unsigned long long *)&diag[4], (unsigned long long)dfail);
-        atomicAdd((unsigned long long *)&diag[5], (unsigned long long)kend);
-    }
-    if (wv != 0) return;
-    if ((uint32_t)lane < kend) {
-        const uint32_t s = s0 + lane;
-        out_node[s] = res_key ? (int32_t)key_node(res_key) : -1;
-        if (out_key) out_key[s] = res_key;
-        if (stamps) stamps[s] = res_stamp;
-    }
-    if (won && (uint32_t)lane < nd) { store_dyn<F>(t, sidx, S); store_dynx<F>(t, sidx, SX); }
-    if (dcur) {  // nodes dirtied in this window, for the next (overlapped) window
-        const uint64_t wm = __ballot(won && (uint32_t)lane < nd);
-        if (won && (uint32_t)lane < nd) dcur[1 + __popcll(wm & ((1ull << lane) - 1ull))] = sidx;
-        if (lane == 0) dcur[0] = (uint32_t)__popcll(wm);
-    }
-}
-
-template <uint32_t F>
-static hipError_t spec_prepare_f() {
-    // the rings take the dynamic LDS past the default 64 KB: raise the limit once, outside capture
-    static const hipError_t a1 = hipFuncSetAttribute((const void *)k_la_resolve_spec<F, true, false>,
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    static const hipError_t a2 = hipFuncSetAttribute((const void *)k_la_resolve_spec<F, false, false>,
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    static const hipError_t a3 = hipFuncSetAttribute((const void *)k_la_resolve_spec<F, true, true>,
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    return a1 != hipSuccess ? a1 : a2 != hipSuccess ? a2 : a3;
-}
-
-// =============================================================================================
-// Speculative-run resolver: Fit + Balanced (+ extended resources), unsharded
-// best-first lists, 32-bit keys (geo.k32), K <= 32.  The window is resolved in rounds.  A round
-// starting at pod s speculates that pods s .. s+H-1 all land on clean nodes:
-//   picks  (wave 0, sequential but short): pod j's pick = its first list entry whose node is not
-//          dirty and not picked by pods s..j-1 of the round; the pick's row is loaded and
-//          reserved with pod j at row index nd + (picks before j) — the slot it would become;
-//   score  (every wave, parallel): each new row (a pick row, or a slot row that won a pod in the
-//          last round) is scored against every later pod of the window, lane = pod, two rows per
-//          wave pass, into the key matrix keym[row][pod] (0 where the row does not apply);
-//   verify (wave 0): pod j's exact dirty maximum is the max of keym[·][j] over the slot rows and
-//          the pick rows of pods s..j-1 (a pick row holds 0 for its own and earlier pods); the
-//          speculation holds for pod j iff that maximum is below its pick.  The first pod f that
-//          fails is resolved by its dirty maximum — exact, since pods s..f-1 did take their picks
-//          — and the round commits s..f; the winning row is re-reserved and re-scored next round.
-// Two barriers per round, ~4.7 pods per round at H = 8 in config 2 (84 % of pods land on their
-// clean candidate).  Slot rows live in LDS for the whole window and are stored once at its end.
-// =============================================================================================
-constexpr uint32_t kRunWaves = 8;  // 512 threads
-constexpr uint32_t kRunH = 8;      // pods speculated per round (8 x 8 candidates = one wave)
-constexpr uint32_t kRunRows = 64;  // slot + pick rows: <= 32 inherited + <= 32 won in the window
-constexpr uint32_t kRunNone = 0xFFFFFFFFu;
-constexpr uint32_t kRunStage = 48;  // rows scored per round: <= 32 inherited (first round) + 1 + H
-template <class R>
-struct RunStage;
-// Dynamic LDS: taken bytes [n + 1] | stage [48] | rows [64] R | ext [64] int4 | lists [32][64] u64 |
-// keym [64][32] u32 | dmax [32] u32 | pods [32] | slotnode [64] | cand [2][64] | plan [4].
-template <uint32_t F>
-constexpr size_t run_lds_bytes(uint32_t n) {
-    return (size_t)(n + 1 + 15) / 16 * 16 + kRunStage * (sizeof(RowT<F>) + 32) +
-           kRunRows * sizeof(RowT<F>) + ((F & kFeatExt) ? kRunRows * sizeof(int4) : 0) + 32 * 64 * 8 +
-           kRunRows * 32 * 4 + 32 * 4 + 32 * sizeof(PodT<F>) + kRunRows * 4 + 2 * 64 * 4 + 4 * 4;
-}
-__device__ __forceinline__ uint32_t key32(uint64_t k) {  // list key -> (score+1) << 22 | ~node
-    return k ? ((uint32_t)(k >> 32) << 22) | (0x3FFFFFu - key_node(k)) : 0u;
-}
-__device__ __forceinline__ uint64_t key64(uint32_t k) {
-    return k ? pack_key(k >> 22, 0x3FFFFFu - (k & 0x3FFFFFu)) : 0ull;
-}
-__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
-    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), l) << 32) |
-           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
-}
-
-// One row to score this round, prepared by wave 0 (slot index, node, first pod it applies after).
-template <class R>
-struct alignas(16) RunStage {
-    R row;
-    int4 x;
-    uint32_t node, ridx;
-    int32_t from;
-    uint32_t pad;
-};
-
-template <uint32_t F, bool DIAG>
-__global__ __launch_bounds__(64 * kRunWaves) void k_la_resolve_run(
-    DevTable t, const PodT<F> *__restrict__ pods, DevCfg c, uint32_t s0, uint32_t P, uint32_t K,
-    uint32_t GLp, const uint64_t *__restrict__ lists, int32_t *__restrict__ out_node,
-    uint64_t *__restrict__ out_key, uint64_t *__restrict__ stamps, const uint32_t *__restrict__ dprev,
-    uint32_t *__restrict__ dcur, uint64_t *__restrict__ diag) {
-    using R = RowT<F>;
-    using PD = PodT<F>;
-    using ST = RunStage<R>;
-    constexpr bool EXT = (F & kFeatExt) != 0;
-    wait_lists_ready(c, s0, K);
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    const int lane = threadIdx.x & 63;
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t half = (uint32_t)lane >> 5;
-    const uint32_t n = t.n, nwords = (n + 1 + 15) / 16 * 4;  // bytes + the dummy node n, as words
-    const uint32_t kend = min(K, P - s0);  // <= 32 (host-checked)
-    uint8_t *taken = (uint8_t *)lds;  // one byte per node: dirty, or picked in this round
-    char *base = (char *)(lds + nwords);
-    ST *stage = (ST *)base;  // rows to score this round, in plan order
-    base += kRunStage * sizeof(ST);
-    R *rows = (R *)base;  // slot rows (committed) and pick rows (speculative), reserved
-    base += kRunRows * sizeof(R);
-    int4 *rowsx = (int4 *)base;  // their extended-resource columns
-    if (EXT) base += kRunRows * sizeof(int4);
-    uint32_t *wlk = (uint32_t *)base;  // the window's lists [pod][64], best first: 32-bit keys
-    base += 32 * 64 * 4;
-    uint32_t *wln = (uint32_t *)base;  // and their nodes (n: no entry)
-    base += 32 * 64 * 4;
-    uint32_t *keym = (uint32_t *)base;  // [row][pod] 32-bit keys of row r for pod j
-    base += kRunRows * 32 * 4;
-    uint32_t *dmax = (uint32_t *)base;  // [pod] dirty maxima of this round (LDS max atomics)
-    base += 32 * 4;
-    PD *wpods = (PD *)base;
-    base += 32 * sizeof(PD);
-    uint32_t *slotnode = (uint32_t *)base;  // row -> node
-    base += kRunRows * 4;
-    uint32_t *cand_n = (uint32_t *)base;  // [8 pods][8] first clean entries: nodes
-    base += 64 * 4;
-    uint32_t *cand_k = (uint32_t *)base;  // and their keys
-    base += 64 * 4;
-    uint32_t *plan = (uint32_t *)base;  // {done, rows to score, unchanged rows bound, pending row}
-    const DPodX px{};
-    uint64_t dph[4] = {0, 0, 0, 0}, dsub[3] = {0, 0, 0}, drounds = 0, dfail = 0, tprev = 0;
-    if (kend == 0) return;
-
-    // ---- prologue: bitmap, lists, pods, inherited slots (the previous window's winners; they
-    // are threads < 32, i.e. wave 0, which stages them for the first round's scoring)
-    for (uint32_t i = threadIdx.x; i < nwords; i += 64 * kRunWaves) lds[i] = 0;
-    for (uint32_t i = threadIdx.x; i < kend * 64; i += 64 * kRunWaves) {
-        const uint64_t k = lists[(size_t)(i >> 6) * GLp + (i & 63)];
-        wlk[i] = key32(k);
-        wln[i] = k ? key_node(k) : n;
-    }
-    if (threadIdx.x < kend) wpods[threadIdx.x] = pods[s0 + threadIdx.x];
-    const uint32_t nd0 = dprev ? dprev[0] : 0u;
-    uint32_t inode = 0;
-    if (threadIdx.x < nd0) {
-        inode = dprev[1 + threadIdx.x];
-        const R r = load_row<F>(t, inode);
-        const RowX x = load_rowx<F>(t, inode);
-        const int4 xx = make_int4(x.ae0, x.re0, x.ae1, x.re1);
-        rows[threadIdx.x] = r;
-        if (EXT) rowsx[threadIdx.x] = xx;
-        slotnode[threadIdx.x] = inode;
-        stage[threadIdx.x] = ST{r, xx, inode, threadIdx.x, -1, 0u};
-    }
-    // this lane's pod for scoring: pod j = lane & 31 (both halves of every wave)
-    const uint32_t pj = (uint32_t)lane & 31u;
-    const PD mp = pods[s0 + (pj < kend ? pj : 0u)];
-    __syncthreads();
-    if (threadIdx.x < nd0) taken[inode] = 1;
-    if (threadIdx.x == 63) taken[n] = 1;  // the dummy node: never clean
-    // wave-0 state: committed slots nd, next pod s, rows that won pods in this window, the row
-    // whose reservation is pending (applied while staging it next round), results (lane = pod)
-    uint32_t nd = nd0, s = 0, pend_row = kRunNone, pend_pod = 0;
-    uint64_t won = 0, res_key = 0, res_stamp = 0;
-    bool first = true;
-    if (DIAG) tprev = diag_stamp();
-    while (true) {
-        uint32_t e = s, np = 0;
-        uint32_t mypk = 0;  // wave 0, lane j: pod j's pick, 32-bit key (0 = none)
-        uint32_t mynode = 0;
-        if (wv == 0) {
-            // ---- picks of pods s .. e-1: pod s+h's pick is its first list entry whose node is not
-            // taken (dirty at round start, or picked by an earlier pod of the round).  Its first
-            // eight entries clean at round start are enough (at most h <= 7 earlier picks), so
-            // they are compacted into lanes 8h .. 8h+7 and the chain runs on masks: per pod one
-            // andn2, ff1, readlane, compare and or.
-            e = min(s + kRunH, kend);
-            uint32_t nn[kRunH], ek[kRunH];
-#pragma unroll
-            for (uint32_t h = 0; h < kRunH; ++h) {
-                const uint32_t j = min(s + h, 31u);
-                nn[h] = wln[j * 64 + lane];
-                ek[h] = wlk[j * 64 + lane];
-                if (s + h >= e) nn[h] = n;  // n: the always-taken dummy
-            }
-            // the pending row (won a pod last round): lane 63 reads it now, reserves it below
-            const bool pl = pend_row != kRunNone && lane == 63;
-            R prr = empty_row<F>();
-            int4 prx = make_int4(0, 0, 0, 0);
-            PD ppd{};
-            if (pl) {
-                prr = rows[pend_row];
-                if (EXT) prx = rowsx[pend_row];
-                ppd = wpods[pend_pod];
-            }
-            cand_n[lane] = n;
-            uint32_t tk[kRunH];
-#pragma unroll
-            for (uint32_t h = 0; h < kRunH; ++h) tk[h] = taken[nn[h]];
-#pragma unroll
-            for (uint32_t h = 0; h < kRunH; ++h) {
-                const bool cl = tk[h] == 0;
-                const uint64_t m = __ballot(cl);
-                const uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-                if (cl && rank < 8u) {
-                    cand_n[h * 8 + rank] = nn[h];
-                    cand_k[h * 8 + rank] = ek[h];
-                }
-            }
-            const uint32_t cn = cand_n[lane], ck = cand_k[lane];
-            // every candidate's row, loaded now: the chain below hides the latency, and the
-            // picked lanes stage their rows themselves afterwards
-            R crow = load_row<F>(t, cn < n ? cn : 0u);
-            RowX cx = load_rowx<F>(t, cn < n ? cn : 0u);
-            if (lane < 32) dmax[lane] = 0;
-            if (DIAG) { const uint64_t t_ = diag_stamp(); dsub[0] += t_ - tprev; }
-            uint64_t killed = __ballot(cn == n), pm = 0;
-            uint32_t pk_lane[kRunH], pk_node[kRunH];
-#pragma unroll
-            for (uint32_t h = 0; h < kRunH; ++h) {
-                const uint64_t avail = (0xFFull << (8 * h)) & ~killed;
-                const uint32_t l = avail ? (uint32_t)__builtin_ctzll(avail) : 64u;
-                const uint32_t x = avail ? (uint32_t)__builtin_amdgcn_readlane((int)cn, (int)l) : n;
-                killed |= __ballot(cn == x);
-                pm |= avail ? (1ull << l) : 0ull;
-                pk_lane[h] = l;
-                pk_node[h] = avail ? x : kRunNone;
-                np += avail ? 1u : 0u;
-            }
-#pragma unroll
-            for (uint32_t h = 0; h < kRunH; ++h)
-                if (pk_lane[h] < 64u) {
-                    const uint32_t pk = (uint32_t)__builtin_amdgcn_readlane((int)ck, (int)pk_lane[h]);
-                    if ((uint32_t)lane == s + h) { mypk = pk; mynode = pk_node[h]; }
-                }
-            if (DIAG) { const uint64_t t_ = diag_stamp(); dsub[1] += t_ - tprev; }
-            // pick rows: each picked candidate lane reserves its row with its pod (pod s + lane/8)
-            // at the slot index it would take (picks are in pod order = lane order), and stages it
-            // after the pending row
-            const uint32_t sbase = (first ? nd0 : 0u) + (pend_row != kRunNone ? 1u : 0u);
-            if ((pm >> lane) & 1ull) {
-                const uint32_t pod = s + ((uint32_t)lane >> 3);
-                const uint32_t rank = (uint32_t)__popcll(pm & ((1ull << lane) - 1ull));
-                const uint32_t idx = nd + rank;
-                reserve(crow, cx, wpods[pod], +1);
-                const int4 xx = make_int4(cx.ae0, cx.re0, cx.ae1, cx.re1);
-                rows[idx] = crow;
-                if (EXT) rowsx[idx] = xx;
-                slotnode[idx] = cn;
-                stage[sbase + rank] = ST{crow, xx, cn, idx, (int32_t)pod, 0u};
-            }
-            if (pl) {
-                RowX x{};
-                x.ae0 = prx.x; x.re0 = prx.y; x.ae1 = prx.z; x.re1 = prx.w;
-                reserve(prr, x, ppd, +1);
-                const int4 xx = make_int4(x.ae0, x.re0, x.ae1, x.re1);
-                rows[pend_row] = prr;
-                if (EXT) rowsx[pend_row] = xx;
-                stage[sbase - 1] = ST{prr, xx, slotnode[pend_row], pend_row, (int32_t)pend_pod, 0u};
-            }
-            if (DIAG) { const uint64_t t_ = diag_stamp(); dsub[2] += t_ - tprev; }
-            if (lane == 0) {
-                plan[0] = s >= kend ? 1u : 0u;
-                plan[1] = sbase + np;
-                plan[2] = first ? 0u : nd;  // rows < plan[2] (but the pending one) are unchanged
-                plan[3] = pend_row;
-            }
-            pend_row = kRunNone;  // applied above (also on the final pass, s == kend)
-            first = false;
-            if (DIAG) { const uint64_t t_ = diag_stamp(); dph[0] += t_ - tprev; tprev = t_; }
-        }
-        __syncthreads();  // B1: picks, staged rows and the plan are visible
-        // ---- score: pass q covers staged rows 2q (lanes 0-31) and 2q+1 (lanes 32-63); every
-        // wave half also takes the max over a sixteenth of the unchanged rows
-        {
-            uint32_t q = (wv + kRunWaves - 1) % kRunWaves;  // wave 0 (which verifies next) last
-            uint32_t qi = 2 * q + half;
-            const uint32_t done = plan[0], ns = plan[1], nu = plan[2], pr = plan[3];
-            ST st = stage[qi < kRunStage ? qi : 0u];
-            if (done) break;
-            uint32_t pm = 0;
-#pragma unroll
-            for (uint32_t m = 0; m < kRunRows / 16; ++m) {
-                const uint32_t r = 2 * wv + half + 16 * m;
-                if (r < nu && r != pr) pm = max(pm, keym[r * 32 + pj]);
-            }
-            while (qi < ns) {
-                RowX x{};
-                if (EXT) { x.ae0 = st.x.x; x.re0 = st.x.y; x.ae1 = st.x.z; x.re1 = st.x.w; }
-                uint32_t key = 0;
-                if ((int32_t)pj > st.from && pj < kend && feasible<F>(st.row, x, mp, px)) {
-                    const uint32_t tot = node_total<F>(st.row, x, mp, px, c, 0, 0.0, 0, 0.0, nullptr);
-                    key = ((tot + 1) << 22) | (0x3FFFFFu - st.node);
-                }
-                keym[st.ridx * 32 + pj] = key;
-                pm = max(pm, key);
-                q += kRunWaves;
-                qi = 2 * q + half;
-                if (qi < ns) st = stage[qi];
-            }
-            __hip_atomic_fetch_max(&dmax[pj], pm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        if (DIAG && wv == 0) { const uint64_t t_ = diag_stamp(); dph[1] += t_ - tprev; tprev = t_; }
-        __syncthreads();  // B2: partial maxima complete
-        if (wv == 0) {
-            if (DIAG) { const uint64_t t_ = diag_stamp(); dph[2] += t_ - tprev; tprev = t_; }
-            // ---- verify: pod j's dirty maximum over every row
-            const uint32_t dm = dmax[pj];
-            const bool inr = lane < 32 && (uint32_t)lane >= s && (uint32_t)lane < e;
-            const uint64_t fm = __ballot(inr && dm > mypk);
-            const uint32_t f = fm ? (uint32_t)__builtin_ctzll(fm) : e;
-            // commit pods s .. f-1 on their picks (rows nd .. nd + nc - 1 in pod order)
-            const uint32_t nc = (uint32_t)__popcll(__ballot(inr && (uint32_t)lane < f && mypk != 0));
-            won |= nc ? ((nc == 64 ? ~0ull : ((1ull << nc) - 1ull)) << nd) : 0ull;
-            nd += nc;
-            const uint64_t now = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
-            if (inr && (uint32_t)lane < f) {
-                res_key = key64(mypk);
-                res_stamp = now;
-                if (mypk) taken[mynode] = 1;  // committed picks are dirty from now on
-            }
-            if (f < e) {
-                // pod f takes its dirty maximum: a committed slot or a pick row of pods < f
-                const uint32_t wk = (uint32_t)__builtin_amdgcn_readlane((int)dm, (int)f);
-                const uint32_t wn = 0x3FFFFFu - (wk & 0x3FFFFFu);
-                if ((uint32_t)lane == f) { res_key = key64(wk); res_stamp = now; }
-                const uint32_t sn = (uint32_t)lane < nd ? slotnode[lane] : kRunNone;
-                const uint32_t rs = (uint32_t)__builtin_ctzll(__ballot(sn == wn));
-                won |= 1ull << rs;
-                pend_row = rs;
-                pend_pod = f;
-
-                s = f + 1;
-                if (DIAG) ++dfail;
-            } else {
-                s = e;
-            }
-            if (DIAG) {
-                const uint64_t t_ = diag_stamp();
-                dph[3] += t_ - tprev;
-                tprev = t_;
-                ++drounds;
-            }
-        }
-    }
-    if (wv != 0) return;
-    if (DIAG && lane == 0) {
-        for (int k = 0; k < 4; ++k) atomicAdd((unsigned long long *)&diag[k], (unsigned long long)dph[k]);
-        atomicAdd((unsigned long long *)&diag[4], (unsigned long long)dfail);
-        atomicAdd((unsigned long long *)&diag[5], (unsigned long long)kend);
-        atomicAdd((unsigned long long *)&diag[6], (unsigned long long)drounds);
-        for (int k = 0; k < 3; ++k) atomicAdd((unsigned long long *)&diag[7 + k], (unsigned long long)dsub[k]);
-    }
-    if ((uint32_t)lane < kend) {
-        const uint32_t sp = s0 + lane;
-        out_node[sp] = res_key ? (int32_t)key_node(res_key) : -1;
-        if (out_key) out_key[sp] = res_key;
-        if (stamps) stamps[sp] = res_stamp;
-    }
-    const bool w = (uint32_t)lane < nd && ((won >> lane) & 1ull);
-    if (w) {
-        const uint32_t node = slotnode[lane];
-        store_dyn<F>(t, node, rows[lane]);
-        if (EXT) {
-            const int4 ee = rowsx[lane];
-            RowX x{};
-            x.ae0 = ee.x; x.re0 = ee.y; x.ae1 = ee.z; x.re1 = ee.w;
-            store_dynx<F>(t, node, x);
-        }
-    }
-    if (dcur) {  // nodes won in this window, for the next (overlapped) window
-        const uint64_t wm = __ballot(w);
-        if (w) dcur[1 + __popcll(wm & ((1ull << lane) - 1ull))] = slotnode[lane];
-        if (lane == 0) dcur[0] = (uint32_t)__popcll(wm);
-    }
-}
-
-template <uint32_t F>
-static hipError_t run_prepare_f() {
-    static const hipError_t a1 = hipFuncSetAttribute((const void *)k_la_resolve_run<F, false>,
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    static const hipError_t a2 = hipFuncSetAttribute((const void *)k_la_resolve_run<F, true>,
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    return a1 != hipSuccess ? a1 : a2;
+    return per;
 }
 
 // =============================================================================================
@@ -3165,31 +2510,6 @@ static hipError_t la_window_f(const DevTable &t, const void *pods_, const DPodX 
         const uint64_t *lists = bf.lists;
         const uint32_t *dprev = bf.dprev;
         uint32_t *dcur = bf.dcur;
-        if (geo.spec == 2) {  // speculative-run resolver (unsharded sorted lists, 32-bit keys)
-            if (geo.epl != 1 || geo.W != 1 || !geo.k32 || K > 32) return hipErrorInvalidValue;
-            const size_t ldsr = run_lds_bytes<F>(t.n);
-            if (diag)
-                hipLaunchKernelGGL((k_la_resolve_run<F, true>), dim3(1), dim3(64 * kRunWaves), ldsr, stream, t, pods, c, s0, P,
-                                   K, GLp, lists, on, ok, st, dprev, dcur, diag);
-            else
-                hipLaunchKernelGGL((k_la_resolve_run<F, false>), dim3(1), dim3(64 * kRunWaves), ldsr, stream, t, pods, c, s0, P,
-                                   K, GLp, lists, on, ok, st, dprev, dcur, nullptr);
-            return hipGetLastError();
-        }
-        if (geo.spec) {  // speculative batch resolver (unsharded sorted lists)
-            if (geo.epl != 1 || geo.W != 1) return hipErrorInvalidValue;
-            const size_t ldss = spec_lds_bytes<F>(t.n);
-            if (diag && geo.k32)
-                hipLaunchKernelGGL((k_la_resolve_spec<F, true, true>), dim3(1), dim3(64 * kSpecM), ldss, stream, t, pods, c, s0, P,
-                                   K, GLp, lists, on, ok, st, dprev, dcur, diag);
-            else if (geo.k32)
-                hipLaunchKernelGGL((k_la_resolve_spec<F, true, false>), dim3(1), dim3(64 * kSpecM), ldss, stream, t, pods, c, s0, P,
-                                   K, GLp, lists, on, ok, st, dprev, dcur, nullptr);
-            else
-                hipLaunchKernelGGL((k_la_resolve_spec<F, false, false>), dim3(1), dim3(64 * kSpecM), ldss, stream, t, pods, c, s0, P,
-                                   K, GLp, lists, on, ok, st, dprev, dcur, nullptr);
-            return hipGetLastError();
-        }
         const size_t lds = bm + sizeof(RowT<F>) + sizeof(RowX);
         const size_t lds4 = bm + 5 * 2 * 64 * 8 + 2 * 64 * (sizeof(RowT<F>) + sizeof(int4)) + 2 * sizeof(ResPub) + 64 * 4 + 64 * sizeof(PodT<F>);
         switch (geo.epl) {
@@ -3241,8 +2561,6 @@ hipError_t wide_la_window(const DevTable &t, const void *pods, const DPodX *podx
                           int32_t *on, uint64_t *ok, uint64_t *st, uint64_t *diag,
                           hipStream_t stream, int part);
 hipError_t wide_batch_claim_prepare();
-hipError_t wide_spec_prepare();
-hipError_t wide_run_prepare();
 hipError_t wide_batch_claim(const DevTable &t, const void *pods, const uint64_t *lists, uint32_t *ctrl,
                             uint32_t *bidx, uint32_t P, uint32_t B, int32_t *on, uint64_t *ok,
                             size_t lds, hipStream_t stream);

@@ -42,10 +42,6 @@ hipError_t wide_la_window(const DevTable &t, const void *pods, const DPodX *podx
 
 hipError_t wide_batch_claim_prepare() { return batch_claim_prepare_f<kWideFit>(); }
 
-hipError_t wide_spec_prepare() { return spec_prepare_f<kWideFit>(); }
-
-hipError_t wide_run_prepare() { return run_prepare_f<kWideFit>(); }
-
 hipError_t wide_batch_claim(const DevTable &t, const void *pods, const uint64_t *lists, uint32_t *ctrl,
                             uint32_t *bidx, uint32_t P, uint32_t B, int32_t *on, uint64_t *ok,
                             size_t lds, hipStream_t stream) {

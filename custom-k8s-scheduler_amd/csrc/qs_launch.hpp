@@ -30,13 +30,9 @@ struct HostRow {
 // every shard has the same G/E/chunk and eplr = 2^lr entries per lane per pod; this process
 // selects shards [v0, v0 + nv) (nv = W for virtual shards in one process, 1 per rank with RCCL).
 // epl (total entries per resolver lane, power of two) >= W * eplr.
-// spec = resolver variant for non-normalizing profiles on unsharded lists: 0 the four-wave
-// pipelined resolver, 1 the speculative batch resolver (k_la_resolve_spec), 2 the speculative-run
-// resolver (k_la_resolve_run: 32-bit keys, K <= 32).
 struct LaGeom {
     uint32_t K, L, G, E, chunk, epl, waves, k32;
     uint32_t W, v0, nv, eplr, lr;
-    uint32_t spec;
 };
 // Kernel-side shard view of the lists: [W][K][GLp] uint64 keys, RS = K * GLp.
 struct LaShard {
@@ -76,10 +72,6 @@ struct LaBufs {
     // normalizing profiles, four-wave resolver: the stop record it hands to the resume kernel
     uint32_t *rec = nullptr;
 };
-// The speculative resolver keeps the dirty bitmap of the whole table in LDS (<= 64 KB here).
-bool spec_resolver_fits(uint32_t n);
-hipError_t spec_prepare();  // dynamic-LDS limit of the speculative resolver (call outside capture)
-bool run_resolver_fits(uint32_t n);
 // In-kernel window hand-off (DevCfg::ready): publish a window's lists (value = run << 32 | w + 1).
 hipError_t launch_ready_set(uint64_t *ready, uint64_t value, hipStream_t stream);
 
@@ -90,12 +82,13 @@ hipError_t launch_ready_set(uint64_t *ready, uint64_t value, hipStream_t stream)
 // per-window path (lwords / cwords per parity).
 LaGeom la_stream_res_plan(const LaGeom &geo, uint32_t feat, uint32_t n, uint32_t cus);  // G = 0: unsupported
 size_t la_stream_res_ctl_bytes();
+// Workgroups of that launch guaranteed co-resident on `cus` CUs (occupancy query, one per CU of margin).
+uint32_t la_stream_res_max_blocks(const LaGeom &geo, uint32_t feat, uint32_t n, uint32_t cus);
 hipError_t launch_la_stream_res(const DevTable &t, const void *pods, const DevCfg &c, uint32_t P, const LaGeom &geo,
                                 uint64_t *lists0, uint64_t *clists0, uint32_t lwords, uint32_t cwords, uint32_t *dio,
                                 int32_t *on, uint64_t *ok, uint64_t *st, void *ctl, uint32_t sel_blocks,
                                 uint64_t *rdiag, hipStream_t stream);
 
-hipError_t run_prepare();
 hipError_t launch_la_window(const DevTable &t, const void *pods, const DPodX *podx, uint32_t s0,
                             uint32_t P, const DevCfg &c, const LaGeom &geo, const LaBufs &bufs,
                             int32_t *out_node, uint64_t *out_key, uint64_t *stamps, uint64_t *diag,

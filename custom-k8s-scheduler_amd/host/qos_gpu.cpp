@@ -57,7 +57,7 @@ Status GpuBackend::load_all(const Handle &h) {
         th[i] = r.taint_hard; ts[i] = r.taint_soft; lb[2 * i] = r.label_bits[0]; lb[2 * i + 1] = r.label_bits[1];
     }
     qs_node_soa soa{ac.data(), am.data(), ae.data(), mp.data(), rc.data(), rm.data(), re.data(),
-                    zc.data(), zm.data(), np.data(), th.data(), ts.data(), lb.data()};
+                    zc.data(), zm.data(), np.data(), th.data(), ts.data(), lb.data(), nullptr};
     if (qs_nodes_load(ctx_, &soa, (uint32_t)n) != QS_OK) return Status::AsError(err("qs_nodes_load"));
     gen_.resize(n);
     for (size_t i = 0; i < n; ++i) gen_[i] = nodes[i].generation;

@@ -51,7 +51,8 @@ typedef enum qs_status {
     QS_OK = 0,
     QS_EINVAL = 1,   /* bad argument / input outside the device layout's range */
     QS_EDEVICE = 2,  /* HIP or RCCL failure (message in qs_last_error) */
-    QS_ETIMEOUT = 3, /* a resolver's in-kernel wait for its lookahead window's lists hit its ~2 s bound */
+    QS_ETIMEOUT = 3, /* an in-kernel wait (lookahead lists, resident hand-off, mailbox peer) hit its
+                        0.5 s bound; the run is void and the device table rebuilt from the mirror */
     QS_ENOMEM = 4,
     QS_ESTATE = 5 /* call out of order (e.g. no nodes loaded) */
 } qs_status;
@@ -197,7 +198,10 @@ QS_API qs_status qs_dist_unique_id(uint8_t out[128]);
  * lookahead window every rank then writes its list block (and, for TaintToleration/NodeAffinity
  * profiles, its partial maxima) straight into every peer's mailbox over xGMI and raises a flag
  * there (one hop), instead of an RCCL all-gather; a peer that never posts makes the run return
- * QS_ETIMEOUT after 0.5 s.  All ranks must run the same streams in the same order.
+ * QS_ETIMEOUT (bound: 5 s for a run's first window, 0.5 s for the others).  All ranks must run the
+ * same streams in the same order.  After QS_ETIMEOUT the ranks are out of step: every later run
+ * returns QS_ESTATE until every rank has called qs_dist_mailbox_connect again (the caller places a
+ * barrier of its own before and after that call on every rank), which restarts all mailboxes empty.
  * Replaces (with qs_open_shard) the per-pod ncclAllReduce exchange of SURVEY.md §8(e). */
 QS_API qs_status qs_dist_mailbox_export(qs_ctx *ctx, uint8_t handle[64]);
 QS_API qs_status qs_dist_mailbox_connect(qs_ctx *ctx, const uint8_t *handles /* world x 64 bytes */);

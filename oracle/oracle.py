@@ -117,6 +117,8 @@ def lib():
         L.or_balanced.argtypes = [ctypes.c_int64] * 4
         L.or_schedule.restype = None
         L.or_schedule.argtypes = [ctypes.c_void_p] * 6 + [ctypes.c_int]
+        L.or_schedule_incremental.restype = ctypes.c_int
+        L.or_schedule_incremental.argtypes = [ctypes.c_void_p] * 6 + [ctypes.c_int, ctypes.c_uint64]
         L.or_score_pod.restype = None
         L.or_score_pod.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint32] + [ctypes.c_void_p] * 2
         L.or_reserve.restype = None
@@ -183,6 +185,23 @@ def schedule(nodes, pods, cfg=None, nthreads=1):
     sn, sp, sc = _mk_nodes(nodes), _mk_pods(pods), _mk_cfg(cfg)
     lib().or_schedule(ctypes.byref(sc), ctypes.byref(sn), ctypes.byref(sp), _ptr(placement),
                       _ptr(best), _ptr(order), ctypes.c_int(nthreads))
+    return placement, best, order
+
+
+def schedule_incremental(nodes, pods, cfg=None, nthreads=1, max_bytes=8 << 30):
+    """or_schedule_incremental: the exact stream with a per-pod-type incremental argmax (same
+    results as ``schedule``; Fit + Balanced (+ ext) profiles).  Mutates ``nodes``.  Raises
+    ValueError when the profile normalizes or the trees exceed ``max_bytes``."""
+    p = len(pods["req_cpu"])
+    placement = np.empty(p, np.int32)
+    best = np.empty(p, np.uint64)
+    order = np.empty(p, np.uint32)
+    sn, sp, sc = _mk_nodes(nodes), _mk_pods(pods), _mk_cfg(cfg)
+    rc = lib().or_schedule_incremental(ctypes.byref(sc), ctypes.byref(sn), ctypes.byref(sp), _ptr(placement),
+                                       _ptr(best), _ptr(order), ctypes.c_int(nthreads),
+                                       ctypes.c_uint64(max_bytes))
+    if rc != 0:
+        raise ValueError("or_schedule_incremental: normalizing profile or tree memory bound exceeded")
     return placement, best, order
 
 

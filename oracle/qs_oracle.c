@@ -246,6 +246,127 @@ void or_schedule(const or_config *cfg, or_nodes *nd, const or_pods *pd, int32_t 
     free(order);
 }
 
+/* ---------------- exact stream, incremental argmax (same semantics as or_schedule) ----------
+ * For profiles without NormalizeScore plugins (TaintToleration / NodeAffinity off) a node's key
+ * for pod j depends only on the node's row and on the pod's "type" — its requests, non-zero
+ * requests, extended requests and QoS class (weights) — and a Reserve changes exactly one row.
+ * So instead of re-scoring all N nodes per pod, keep per pod type a max segment tree over the
+ * nodes' packed keys (node_key(), the very function or_schedule evaluates; keys are unique and
+ * embed ~index, so the root is spec S7's selectHost), and after each Reserve re-score only the
+ * reserved node, once per type seen so far.  Identical placements, keys and final table to
+ * or_schedule (tests/test_oracle_incremental.py checks that, bit for bit); used where the
+ * brute-force oracle would take minutes (config 3: 50,000 nodes x 1,000,000 pods).
+ * Returns 0, or -1 when the profile normalizes or the per-type trees would exceed `max_bytes`. */
+typedef struct {
+    int64_t f[7]; /* req_cpu, req_mem, req_ext[0], req_ext[1], nz_cpu, nz_mem, qos */
+    uint32_t rep; /* a pod of this type (its arrival index) */
+    uint64_t *tree; /* [2M] max tree, leaves at M + n */
+} or_type;
+
+static void type_fields(const or_pods *pd, uint32_t j, int64_t f[7]) {
+    f[0] = pd->req_cpu[j]; f[1] = pd->req_mem[j];
+    f[2] = pd->req_ext[j * OR_MAX_EXT]; f[3] = pd->req_ext[j * OR_MAX_EXT + 1];
+    f[4] = pd->nz_cpu[j]; f[5] = pd->nz_mem[j]; f[6] = pd->qos[j];
+}
+
+static uint64_t type_hash(const int64_t f[7]) {
+    uint64_t h = 0x9E3779B97F4A7C15ULL;
+    for (int i = 0; i < 7; i++) {
+        h ^= (uint64_t)f[i] + 0x9E3779B97F4A7C15ULL + (h << 6) + (h >> 2);
+        h *= 0xBF58476D1CE4E5B9ULL;
+    }
+    return h ^ (h >> 31);
+}
+
+int or_schedule_incremental(const or_config *cfg, or_nodes *nd, const or_pods *pd, int32_t *placement,
+                            uint64_t *best_key, uint32_t *order_out, int nthreads, uint64_t max_bytes) {
+    if (cfg->enable_taint || cfg->enable_affinity) return -1;
+    const uint32_t P = pd->p, N = nd->n;
+    if (nthreads < 1) nthreads = 1;
+    uint32_t M = 1;
+    while (M < (N ? N : 1)) M <<= 1;
+    const size_t tree_bytes = sizeof(uint64_t) * 2 * (size_t)M;
+    uint32_t *order = (uint32_t *)malloc(sizeof(uint32_t) * (P ? P : 1));
+    order_pods(cfg, pd, order);
+    uint32_t cap = 0, T = 0, hcap = 1024;
+    or_type *types = NULL;
+    int32_t *htab = (int32_t *)malloc(sizeof(int32_t) * hcap); /* open addressing -> type index */
+    for (uint32_t i = 0; i < hcap; i++) htab[i] = -1;
+    int rc = 0;
+    for (uint32_t s = 0; s < P; s++) {
+        const uint32_t j = order[s];
+        int64_t f[7];
+        type_fields(pd, j, f);
+        uint32_t h = (uint32_t)type_hash(f) & (hcap - 1);
+        int32_t t = -1;
+        while (htab[h] >= 0) {
+            if (memcmp(types[htab[h]].f, f, sizeof f) == 0) { t = htab[h]; break; }
+            h = (h + 1) & (hcap - 1);
+        }
+        if (t < 0) { /* a new type: its tree over the current table */
+            if ((uint64_t)(T + 1) * tree_bytes > max_bytes) { rc = -1; break; }
+            if (T == cap) {
+                cap = cap ? 2 * cap : 64;
+                types = (or_type *)realloc(types, sizeof(or_type) * cap);
+            }
+            if (2 * (T + 1) > hcap) { /* grow the hash table (load <= 1/2) */
+                uint32_t nh = 2 * hcap;
+                int32_t *nt = (int32_t *)malloc(sizeof(int32_t) * nh);
+                for (uint32_t i = 0; i < nh; i++) nt[i] = -1;
+                for (uint32_t u = 0; u < T; u++) {
+                    uint32_t g = (uint32_t)type_hash(types[u].f) & (nh - 1);
+                    while (nt[g] >= 0) g = (g + 1) & (nh - 1);
+                    nt[g] = (int32_t)u;
+                }
+                free(htab);
+                htab = nt;
+                hcap = nh;
+                h = (uint32_t)type_hash(f) & (hcap - 1);
+                while (htab[h] >= 0) h = (h + 1) & (hcap - 1);
+            }
+            or_type *ty = &types[T];
+            memcpy(ty->f, f, sizeof f);
+            ty->rep = j;
+            ty->tree = (uint64_t *)calloc(2 * (size_t)M, sizeof(uint64_t));
+            uint64_t *tr = ty->tree;
+            int64_t n_ = N;
+#pragma omp parallel for num_threads(nthreads) if (nthreads > 1)
+            for (int64_t n = 0; n < n_; n++) tr[M + n] = node_key(cfg, nd, pd, (uint32_t)n, j, 0, 0, NULL);
+            for (uint32_t v = M - 1; v >= 1; v--) tr[v] = tr[2 * v] > tr[2 * v + 1] ? tr[2 * v] : tr[2 * v + 1];
+            htab[h] = (int32_t)T;
+            t = (int32_t)T++;
+        }
+        const uint64_t best = types[t].tree[1];
+        if (best_key) best_key[j] = best;
+        if (best == 0) {
+            placement[j] = -1;
+            continue;
+        }
+        const uint32_t n = 0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFu);
+        placement[j] = (int32_t)n;
+        or_reserve(nd, pd, j, n, +1);
+        /* the reserved node's key changes for every type: re-score it and fix the tree paths */
+        int64_t T_ = T;
+#pragma omp parallel for num_threads(nthreads) if (nthreads > 1 && T_ >= 64)
+        for (int64_t u = 0; u < T_; u++) {
+            uint64_t *tr = types[u].tree;
+            uint32_t v = M + n;
+            tr[v] = node_key(cfg, nd, pd, n, types[u].rep, 0, 0, NULL);
+            for (v >>= 1; v >= 1; v >>= 1) {
+                const uint64_t m = tr[2 * v] > tr[2 * v + 1] ? tr[2 * v] : tr[2 * v + 1];
+                if (tr[v] == m) break; /* unchanged from here up */
+                tr[v] = m;
+            }
+        }
+    }
+    if (order_out) memcpy(order_out, order, sizeof(uint32_t) * P);
+    for (uint32_t u = 0; u < T; u++) free(types[u].tree);
+    free(types);
+    free(htab);
+    free(order);
+    return rc;
+}
+
 /* ---------------- spec S11: batched mode ---------------- */
 #define OR_LIST 64
 #define OR_APPS 1024

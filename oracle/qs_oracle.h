@@ -58,6 +58,13 @@ void or_score_pod(const or_config *cfg, const or_nodes *nodes, const or_pods *po
 void or_schedule(const or_config *cfg, or_nodes *nodes, const or_pods *pods, int32_t *placement,
                  uint64_t *best_key, uint32_t *order_out, int nthreads);
 
+/* The same exact stream with an incremental argmax (per pod type a max tree over the nodes'
+ * keys; only the reserved node is re-scored per pod): identical results, for profiles without
+ * TaintToleration / NodeAffinity.  Returns -1 (nothing usable) for normalizing profiles or when
+ * the trees would need more than max_bytes; nodes are then partially updated: pass a copy. */
+int or_schedule_incremental(const or_config *cfg, or_nodes *nodes, const or_pods *pods, int32_t *placement,
+                            uint64_t *best_key, uint32_t *order_out, int nthreads, uint64_t max_bytes);
+
 /* Batched mode (spec S11): batches of `batch` (<= 64) pods; each pod's 64 best keys against the
  * batch-start table (required anti-affinity to its app per hostname / zone included), claims in
  * batch order (best key whose node, and for zone anti-affinity whose (app, zone), no earlier pod of

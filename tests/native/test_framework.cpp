@@ -388,13 +388,13 @@ static void test_gpu_schedule_one_loop_parity() {
     std::vector<int64_t> ae(2 * n), re(2 * n);
     std::vector<uint64_t> th(n), ts(n), lb(2 * n);
     qs_node_soa_out out{col[0].data(), col[1].data(), ae.data(), col[2].data(), col[3].data(), col[4].data(),
-                        re.data(), col[5].data(), col[6].data(), col[7].data(), th.data(), ts.data(), lb.data()};
+                        re.data(), col[5].data(), col[6].data(), col[7].data(), th.data(), ts.data(), lb.data(), nullptr};
     std::vector<qs_pod> recs(p);
     CHECK_EQ((int)qs_synth_generate(4, seed, n, p, &out, recs.data()), (int)QS_OK);
     qs_ctx *ctx = nullptr;
     CHECK_EQ((int)qs_open(&cfg, 0, &ctx), (int)QS_OK);
     qs_node_soa in{col[0].data(), col[1].data(), ae.data(), col[2].data(), col[3].data(), col[4].data(),
-                   re.data(), col[5].data(), col[6].data(), col[7].data(), th.data(), ts.data(), lb.data()};
+                   re.data(), col[5].data(), col[6].data(), col[7].data(), th.data(), ts.data(), lb.data(), nullptr};
     CHECK_EQ((int)qs_nodes_load(ctx, &in, n), (int)QS_OK);
     std::vector<int32_t> stream(p);
     qs_stats stats;
@@ -407,12 +407,12 @@ static void test_gpu_schedule_one_loop_parity() {
     std::vector<int64_t> oae(2 * n), ore(2 * n);
     std::vector<uint64_t> oth(n), ots(n), olb(2 * n);
     or_nodes on{n, o[0].data(), o[1].data(), oae.data(), o[2].data(), o[3].data(), o[4].data(), ore.data(),
-                o[5].data(), o[6].data(), o[7].data(), oth.data(), ots.data(), olb.data()};
+                o[5].data(), o[6].data(), o[7].data(), oth.data(), ots.data(), olb.data(), nullptr};
     std::vector<int64_t> prc(p), prm(p), pre(2 * p), pzc(p), pzm(p);
     std::vector<int32_t> pq(p), ppr(p), pnr(p), pnp(p), ppw(4 * p);
     std::vector<uint64_t> pth(p), pts(p), psel(2 * p), prt(8 * p), ppt(8 * p);
     or_pods op{p, prc.data(), prm.data(), pre.data(), pzc.data(), pzm.data(), pq.data(), ppr.data(), pth.data(),
-               pts.data(), psel.data(), pnr.data(), pnp.data(), prt.data(), ppt.data(), ppw.data()};
+               pts.data(), psel.data(), pnr.data(), pnp.data(), prt.data(), ppt.data(), ppw.data(), nullptr, nullptr};
     or_generate(4, seed, &on, &op);
     or_config oc{1, 1, {1, 2, 3}, {1, 1, 1}, 3, 2, 1, 1, 0, 1};
     std::vector<int32_t> oracle(p);

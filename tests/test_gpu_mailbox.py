@@ -114,3 +114,99 @@ def test_sharded_context_needs_a_transport():
         with pytest.raises(QschedError, match="transport"):
             st.run()
         st.free()
+
+
+def _rank_timeout(rank, world, qin, qout, n, p):
+    """Rank 0 runs a stream rank 1 never joins (QS_ETIMEOUT after the first window's 5 s bound),
+    then runs fail with QS_ESTATE until both ranks reconnect; then both run the serial-window
+    stream (lookahead_serial: the path whose timeout word was never cleared)."""
+    import sys
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "custom-k8s-scheduler_amd")]
+    import qsched
+
+    try:
+        nodes, pods = qsched.synth_generate(2, n, p)
+        cfg = dict(engine="lookahead", lookahead_serial=1)
+        with qsched.Scheduler(cfg, device=0, shard=(rank, world, None)) as s:
+            qout.put(("h", rank, s.mailbox_export()))
+            handles = qin.get(timeout=120)
+            s.mailbox_connect(handles)
+            s.load_nodes(nodes)
+            st = s.prepare(pods)
+            codes = []
+            if rank == 0:
+                try:
+                    st.run()
+                    codes.append("ok")
+                except qsched.QschedError as e:
+                    codes.append(e.status)
+                try:
+                    st.run()
+                    codes.append("ok")
+                except qsched.QschedError as e:
+                    codes.append(e.status)
+            qout.put(("b", rank, codes))  # barrier: both ranks idle, then reconnect
+            qin.get(timeout=120)
+            s.mailbox_connect(handles)
+            qout.put(("b2", rank, None))
+            qin.get(timeout=120)
+            s.load_nodes(nodes)
+            st = s.prepare(pods)
+            st.run()
+            pl, keys = st.results()
+            st.free()
+        qout.put(("r", rank, pl, keys, codes))
+    except Exception as e:  # reported to the parent instead of hanging it
+        qout.put(("e", rank, repr(e)))
+
+
+def test_mailbox_timeout_then_reconnect(oracle):
+    import torch.multiprocessing as mp
+    from qsched import pods_from_struct, synth_generate
+
+    n, p = 1500, 3000
+    ctx = mp.get_context("spawn")
+    qout = ctx.Queue()
+    qins = [ctx.Queue() for _ in range(2)]
+    procs = [ctx.Process(target=_rank_timeout, args=(r, 2, qins[r], qout, n, p)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    got = {}
+    try:
+        hs = {}
+        while len(hs) < 2:
+            m = qout.get(timeout=180)
+            assert m[0] != "e", m
+            hs[m[1]] = m[2]
+        for q in qins:
+            q.put([hs[0], hs[1]])
+        for tag in ("b", "b2"):
+            seen = {}
+            while len(seen) < 2:
+                m = qout.get(timeout=180)
+                assert m[0] != "e", m
+                assert m[0] == tag, m
+                seen[m[1]] = m[2]
+            if tag == "b":
+                codes = seen[0]
+            for q in qins:
+                q.put(True)
+        while len(got) < 2:
+            m = qout.get(timeout=300)
+            assert m[0] != "e", m
+            got[m[1]] = m[2:]
+    finally:
+        for pr in procs:
+            pr.join(60)
+            if pr.is_alive():
+                pr.kill()
+    assert codes[0] == 3, codes  # QS_ETIMEOUT (rank 1 never posted)
+    assert codes[1] == 5, codes  # QS_ESTATE until every rank reconnects
+    nodes, pods = synth_generate(2, n, p)
+    on = {k: v.copy() for k, v in nodes.items()}
+    o_pl, o_keys, _ = oracle.schedule(on, pods_from_struct(pods), {}, nthreads=16)
+    for rank in range(2):
+        pl, keys, _ = got[rank]
+        assert np.array_equal(pl, o_pl) and np.array_equal(keys, o_keys), rank

@@ -165,15 +165,3 @@ def test_balanced_skip_besteffort(oracle):
     g = run_gpu(nodes, pods, dict(balanced_skip_besteffort=1), "lookahead")
     o = run_oracle(oracle, nodes, pods, dict(balanced_skip_besteffort=1))
     assert_same(g[:2], o[:2], g[2], o[2])
-
-
-@pytest.mark.parametrize("resolver", ["run", "spec"])
-@pytest.mark.parametrize("config,n,p", [(1, 100, 1000), (2, 700, 9000), (2, 5000, 3000), (2, 1500, 20000)])
-def test_speculative_resolvers(oracle, monkeypatch, resolver, config, n, p):
-    """The opt-in speculative resolvers (QS_RESOLVER=run|spec) on the overlapped
-    lookahead windows: placements, keys and the final table bit-exact vs the oracle."""
-    monkeypatch.setenv("QS_RESOLVER", resolver)
-    nodes, pods = synth_generate(config, n, p)
-    g = run_gpu(nodes, pods, {}, "lookahead")
-    o = run_oracle(oracle, nodes, pods, {})
-    assert_same(g[:2], o[:2], g[2], o[2])
