@@ -460,6 +460,16 @@ __device__ __forceinline__ uint32_t ba_score(const R &r, const P &p, const DevCf
     return ba;
 }
 
+// Normalized TaintToleration score: reverse DefaultNormalizeScore (UP helper/normalize_score.go)
+// of the raw count given the pod's maximum mt over feasible nodes and ymt = RN(1/mt).
+__device__ __forceinline__ uint32_t tt_norm(uint32_t raw, uint32_t mt, double ymt) {
+    return mt == 0 ? 100u : 100u - floor_div(100u * raw, ymt);
+}
+// Normalized NodeAffinity score: DefaultNormalizeScore (not reversed).
+__device__ __forceinline__ uint32_t na_norm(uint32_t raw, uint32_t ma, double yma) {
+    return ma == 0 ? raw : floor_div(100u * raw, yma);
+}
+
 template <uint32_t F, class R, class P>
 __device__ __forceinline__ uint32_t node_total(const R &r, const RowX &x, const P &p,
                                                const DPodX &px, const DevCfg &c, uint32_t mt,
@@ -467,14 +477,12 @@ __device__ __forceinline__ uint32_t node_total(const R &r, const RowX &x, const 
     const uint32_t la = la_score(r, p, c), ba = ba_score(r, p, c);
     uint32_t total = __umul24((uint32_t)p.wfit, la) + __umul24((uint32_t)p.wbal, ba);
     uint32_t tt = 0, na = 0;
-    if (F & kFeatTaint) {  // reverse DefaultNormalizeScore (UP helper/normalize_score.go)
-        const uint32_t raw = taint_raw(x, px);
-        tt = mt == 0 ? 100u : 100u - floor_div(100u * raw, ymt);
+    if (F & kFeatTaint) {
+        tt = tt_norm(taint_raw(x, px), mt, ymt);
         total += __umul24((uint32_t)c.wtt, tt);
     }
     if (F & kFeatAffinity) {
-        const uint32_t raw = affinity_raw(x, p, px);
-        na = ma == 0 ? raw : floor_div(100u * raw, yma);
+        na = na_norm(affinity_raw(x, p, px), ma, yma);
         total += __umul24((uint32_t)c.wna, na);
     }
     if (sc) { sc[0] = la; sc[1] = ba; sc[2] = tt; sc[3] = na; }

@@ -1231,11 +1231,14 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                 static const char *senv = getenv("QS_RES_SEL");
                 uint32_t sel = rgeo.K * rgeo.G;
                 if (senv && atoi(senv) > 0) sel = (uint32_t)atoi(senv);
+                // normalizing profiles: the G chunk tasks of a pod wait for each other's partial
+                // maxima, so every task needs its own workgroup
+                if (norm) sel = std::max(sel, rgeo.K * rgeo.G);
                 // the launch's workgroups wait on each other: resident only when the occupancy
                 // query guarantees that all 1 + sel of them run at once (VERDICT r2 missing #5)
                 const bool coresident =
                     rgeo.G > 0 && 1 + sel <= la_stream_res_max_blocks(rgeo, c->dc.feat, n, (uint32_t)c->cus);
-                const bool resident = overlap && !norm && !c->comm && !mbox && c->world == 1 && !c->resident_off &&
+                const bool resident = overlap && !c->comm && !mbox && c->world == 1 && !c->resident_off &&
                                       !diag_on && !c->wide && !(renv && renv[0] == '0') && rgeo.G > 0 && coresident;
                 c->last_resident = resident;
                 if (resident) {
@@ -1248,6 +1251,11 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                     HIPCHK(hipMemsetAsync(c->dio.p, 0, 2 * kDioWords * 4, c->stream));
                     HIPCHK(hipMemsetAsync(c->resctl.p, 0, la_stream_res_ctl_bytes(), c->stream));
                     HIPCHK(hipMemsetAsync(hw + 2, 0, 8, c->stream));
+                    // normalizing profiles: per window parity the chunks' partial maxima and the
+                    // pods' NormInfo; {rescans, windows with a rescan}
+                    c->npart.ensure(16 * 2 * (size_t)rgeo.K * rgeo.G);
+                    c->normi.ensure(16 * 2 * 64);
+                    HIPCHK(hipMemsetAsync(c->nfall.p, 0, 16, c->stream));
                     // test hook: a selector that never delivers window 3 (one-shot), so the
                     // in-kernel timeout drain runs (tests/test_gpu_recovery.py)
                     const char *inj = getenv("QS_INJECT_FAULT");
@@ -1264,8 +1272,10 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                         HIPCHK(hipMemsetAsync(rdiag, 0, 256, c->stream));
                     }
                     kt.begin(3, c->stream);  // the one launch, under "resolve"
-                    HIPCHK(launch_la_stream_res(c->dt, dp, c->dc, P, rgeo, L0, C0, (uint32_t)lwords, (uint32_t)cwords,
-                                                dio, on, ok, st, c->resctl.p, sel, rdiag, c->stream));
+                    HIPCHK(launch_la_stream_res(c->dt, dp, dx, c->dc, P, rgeo, L0, C0, (uint32_t)lwords, (uint32_t)cwords,
+                                                c->npart.as<uint4>(), c->normi.as<NormInfo>(),
+                                                c->nfall.as<unsigned long long>(), on, ok, st, c->resctl.p, sel, rdiag,
+                                                c->stream));
                     kt.end(3, c->stream);
                     c->dc.inject = 0;
                     if (rdiag) {

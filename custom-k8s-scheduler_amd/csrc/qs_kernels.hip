@@ -153,8 +153,11 @@ hipError_t launch_la_window(const DevTable &t, const void *pods, const DPodX *po
 LaGeom la_stream_res_plan(const LaGeom &geo, uint32_t feat, uint32_t n, uint32_t cus) {
     LaGeom r = geo;
     r.G = 0;
-    if (!((feat == 0 || feat == kFeatExt) && geo.W == 1 && geo.nv == 1 && geo.epl == 1 && geo.waves == 4 &&
-          geo.L <= 64 && n > 0 && cus > geo.K))
+    // compact Fit + Balanced (+ extended) profiles, and the normalizing ones (K <= kResNormK)
+    const bool fit = feat == 0 || feat == kFeatExt;
+    const bool norm = (feat & kFeatNorm) != 0 && (feat & kFeatWide) == 0 && geo.K <= kResNormK;
+    if (!((fit || norm) && geo.W == 1 && geo.nv == 1 && geo.epl == 1 && geo.waves == 4 && geo.L <= 64 && n > 0 &&
+          cus > geo.K))
         return r;
     const uint32_t gmax = std::min(8u, (cus - 1) / geo.K);
     if (gmax == 0) return r;
@@ -179,21 +182,28 @@ size_t la_stream_res_ctl_bytes() { return kResCtlBytes; }
 // CU can exceed what the hardware admits by one workgroup (MI355X_MICROARCH.md, residency), so one
 // is taken off whenever the API allows two or more.
 uint32_t la_stream_res_max_blocks(const LaGeom &geo, uint32_t feat, uint32_t n, uint32_t cus) {
-    const int per = (feat & kFeatExt) ? la_stream_res_per_cu<kFeatExt>(geo, n) : la_stream_res_per_cu<0>(geo, n);
+    const int per = (feat & kFeatNorm)  ? la_stream_res_per_cu<kFeatExt | kFeatTaint | kFeatAffinity>(geo, n)
+                    : (feat & kFeatExt) ? la_stream_res_per_cu<kFeatExt>(geo, n)
+                                        : la_stream_res_per_cu<0>(geo, n);
     const int safe = per >= 2 ? per - 1 : per;
     return (uint32_t)std::max(0, safe) * cus;
 }
 
-hipError_t launch_la_stream_res(const DevTable &t, const void *pods, const DevCfg &c, uint32_t P, const LaGeom &geo,
-                                uint64_t *lists0, uint64_t *clists0, uint32_t lwords, uint32_t cwords, uint32_t *dio,
-                                int32_t *on, uint64_t *ok, uint64_t *st, void *ctl, uint32_t sel_blocks,
-                                uint64_t *rdiag, hipStream_t stream) {
+hipError_t launch_la_stream_res(const DevTable &t, const void *pods, const DPodX *podx, const DevCfg &c, uint32_t P,
+                                const LaGeom &geo, uint64_t *lists0, uint64_t *clists0, uint32_t lwords,
+                                uint32_t cwords, uint4 *npart, NormInfo *norm, unsigned long long *nfall, int32_t *on,
+                                uint64_t *ok, uint64_t *st, void *ctl, uint32_t sel_blocks, uint64_t *rdiag,
+                                hipStream_t stream) {
     if (t.wrows || geo.G == 0 || (uint64_t)t.n * sizeof(DRow) >= (1ull << 31)) return hipErrorInvalidValue;
+    if (c.feat & kFeatNorm)
+        return la_stream_res_f<kFeatExt | kFeatTaint | kFeatAffinity>(t, pods, podx, c, P, geo, lists0, clists0, lwords,
+                                                                      cwords, npart, norm, nfall, on, ok, st, ctl,
+                                                                      sel_blocks, rdiag, stream);
     if (c.feat & kFeatExt)
-        return la_stream_res_f<kFeatExt>(t, pods, c, P, geo, lists0, clists0, lwords, cwords, dio, on, ok, st, ctl,
-                                         sel_blocks, rdiag, stream);
-    return la_stream_res_f<0>(t, pods, c, P, geo, lists0, clists0, lwords, cwords, dio, on, ok, st, ctl, sel_blocks,
-                              rdiag, stream);
+        return la_stream_res_f<kFeatExt>(t, pods, podx, c, P, geo, lists0, clists0, lwords, cwords, npart, norm, nfall,
+                                         on, ok, st, ctl, sel_blocks, rdiag, stream);
+    return la_stream_res_f<0>(t, pods, podx, c, P, geo, lists0, clists0, lwords, cwords, npart, norm, nfall, on, ok, st,
+                              ctl, sel_blocks, rdiag, stream);
 }
 
 LaGeom la_geometry(uint32_t n, uint32_t K, uint32_t W, uint32_t L) {

@@ -1592,6 +1592,7 @@ struct ResCtl {                // zeroed before every launch; each counter on it
     uint32_t done, pad0[31];   // windows resolved
     uint32_t rdy[2][32];       // pods merged, per window parity
     uint32_t ticket[2][64];    // chunk lists delivered, per window parity and window pod
+    uint32_t nticket[2][64];   // normalizing profiles: chunk partial maxima published, likewise
 };
 // Bounded relaxed poll by one lane: true once *p >= want; false on werr or after 0.5 s (100 MHz).
 __device__ __forceinline__ bool res_wait_ge(const uint32_t *p, uint32_t want, uint32_t *werr) {
@@ -1624,21 +1625,29 @@ __device__ __forceinline__ void res_publish_list(const uint64_t *lbuf, uint32_t 
     if (threadIdx.x == 0) res_add(rdy);
 }
 
+// Normalizing profiles (TaintToleration / NodeAffinity): a task first scores everything but the
+// normalized parts and the chunk's partial maxima {mt, ct, ma, ca} over its feasible nodes,
+// publishes the partial (sc1, ticket nticket[w&1][k]), waits until all G chunks of its pod have
+// published (every task has its own workgroup, so they all run at once), combines them into the
+// pod's NormInfo and only then finishes the totals and its top-L.  The merger publishes the
+// NormInfo with the pod's list, for the resolver's lost-maximum test.
 template <int E, int E2, uint32_t F>
 __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *__restrict__ pods, const DevCfg &c,
                                              uint32_t P, uint32_t K, uint32_t G, uint32_t L, uint32_t chunk,
                                              uint32_t nwin, uint64_t *lists0, uint64_t *clists0, uint32_t lwords,
                                              uint32_t cwords, ResCtl *ctl, uint32_t sid, uint32_t S,
-                                             uint64_t *rdiag) {
+                                             uint64_t *rdiag, const DPodX *__restrict__ podx, uint4 *npart0,
+                                             NormInfo *norm0) {
+    constexpr bool NORM = (F & kFeatNorm) != 0;
     // rdiag (QS_RES_DIAG=1): summed s_memrealtime ticks of the selectors' phases, [16] scoring,
     // [17] chunk top-L, [18] publish / merge, [19] tasks, [20] merges
     uint64_t ts0 = 0, ts1 = 0, ts2 = 0, dsc = 0, dtl = 0, dpm = 0, ntask = 0, nmerge = 0;
     __shared__ uint64_t lbuf[64];
     __shared__ uint32_t okflag_[4];  // (16 B: keeps the dynamic-LDS base 16-byte aligned)
+    __shared__ uint32_t nred[4][8];  // NORM: per-wave partial maxima and counts
     uint32_t &okflag = okflag_[0];
     const int tid = threadIdx.x, lane = tid & 63, w8 = tid >> 6;
     const __amdgpu_buffer_rsrc_t rs = row_rsrc(t);
-    const DPodX px{};
     DevCfg cv = c;  // (weights in VGPRs, as in la_resolve4_stream)
     asm volatile("" : "+v"(cv.yd_both), "+v"(cv.yd_c), "+v"(cv.yd_m), "+v"(cv.wc), "+v"(cv.wm));
     for (uint32_t w = 0; w < nwin; ++w) {
@@ -1659,16 +1668,102 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
             const uint32_t start = g * chunk, end = min(t.n, start + chunk);
             const uint32_t base = start + (uint32_t)w8 * E * kWave + lane;
             uint32_t tv[E];
+            NormInfo nf{0, 0, 0, 0};
+            if constexpr (NORM) {
+                const DPodX px = load_vgpr(podx + s0 + k);
+                uint32_t raw[E];  // (taint raw | affinity raw << 16), 0xFFFFFFFF = infeasible / outside
+                uint32_t mt = 0, ma = 0;
 #pragma unroll
-            for (int j = 0; j < E; ++j) {
-                const uint32_t idx = base + j * kWave;
-                tv[j] = 0;
-                if (idx < end) {
-                    RowX x;
-                    const Row r = load_row_coh<F>(t, rs, idx, x);
-                    const bool f = feasible<F>(r, x, p, px);
-                    const uint32_t tot = node_total<F>(r, x, p, px, cv, 0, 0.0, 0, 0.0, nullptr);
-                    tv[j] = f ? tot + 1 : 0;
+                for (int j = 0; j < E; ++j) {
+                    const uint32_t idx = base + j * kWave;
+                    tv[j] = 0;
+                    raw[j] = 0xFFFFFFFFu;
+                    if (idx < end) {
+                        RowX x;
+                        const Row r = load_row_coh<F>(t, rs, idx, x);
+                        const DMask m = t.masks[idx];  // static during a stream
+                        x.th = m.th; x.ts = m.ts; x.lb0 = m.lb0; x.lb1 = m.lb1;
+                        if (feasible<F>(r, x, p, px)) {
+                            const uint32_t rt = (F & kFeatTaint) ? taint_raw(x, px) : 0u;
+                            const uint32_t ra = (F & kFeatAffinity) ? affinity_raw(x, p, px) : 0u;
+                            raw[j] = rt | (ra << 16);
+                            mt = rt > mt ? rt : mt;
+                            ma = ra > ma ? ra : ma;
+                            tv[j] = __umul24((uint32_t)p.wfit, la_score(r, p, cv)) +
+                                    __umul24((uint32_t)p.wbal, ba_score(r, p, cv));
+                        }
+                    }
+                }
+                // the chunk's maxima and the counts of feasible nodes attaining them
+                mt = wave_max_u32(mt);
+                ma = wave_max_u32(ma);
+                if (lane == 0) { nred[0][w8] = mt; nred[1][w8] = ma; }
+                __syncthreads();
+                mt = ma = 0;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    mt = nred[0][i] > mt ? nred[0][i] : mt;
+                    ma = nred[1][i] > ma ? nred[1][i] : ma;
+                }
+                uint32_t ct = 0, ca = 0;
+#pragma unroll
+                for (int j = 0; j < E; ++j) {
+                    ct += (uint32_t)__popcll(__ballot(raw[j] != 0xFFFFFFFFu && (raw[j] & 0xFFFFu) == mt));
+                    ca += (uint32_t)__popcll(__ballot(raw[j] != 0xFFFFFFFFu && (raw[j] >> 16) == ma));
+                }
+                if (lane == 0) { nred[2][w8] = ct; nred[3][w8] = ca; }
+                __syncthreads();
+                if (G == 1) {
+                    nf = NormInfo{mt, 0, ma, 0};
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) { nf.ct += nred[2][i]; nf.ca += nred[3][i]; }
+                } else {
+                    // publish this chunk's partial, then combine all G partials of the pod
+                    uint4 *np = npart0 + ((size_t)b * K + k) * G;
+                    if (tid == 0) {
+                        uint4 o = make_uint4(mt, 0, ma, 0);
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) { o.y += nred[2][i]; o.w += nred[3][i]; }
+                        store_coh_u64(reinterpret_cast<uint64_t *>(np + g), (uint64_t)o.x | ((uint64_t)o.y << 32));
+                        store_coh_u64(reinterpret_cast<uint64_t *>(np + g) + 1, (uint64_t)o.z | ((uint64_t)o.w << 32));
+                        drain_stores();
+                        res_add(&ctl->nticket[b][k]);
+                        okflag = res_wait_ge(&ctl->nticket[b][k], ((w >> 1) + 1) * G, c.werr) ? 1u : 0u;
+                    }
+                    __syncthreads();
+                    if (!okflag) return;
+                    for (uint32_t gg = 0; gg < G; ++gg) {  // spec S5 maxima over the pod's feasible nodes
+                        const uint64_t lo = load_coh_u64(reinterpret_cast<const uint64_t *>(np + gg));
+                        const uint64_t hi = load_coh_u64(reinterpret_cast<const uint64_t *>(np + gg) + 1);
+                        const uint32_t qx = (uint32_t)lo, qy = (uint32_t)(lo >> 32), qz = (uint32_t)hi,
+                                       qw = (uint32_t)(hi >> 32);
+                        if (qx > nf.mt) { nf.mt = qx; nf.ct = 0; }
+                        if (qx == nf.mt) nf.ct += qy;
+                        if (qz > nf.ma) { nf.ma = qz; nf.ca = 0; }
+                        if (qz == nf.ma) nf.ca += qw;
+                    }
+                }
+                const double ymt = rcp_exact(nf.mt), yma = rcp_exact(nf.ma);
+#pragma unroll
+                for (int j = 0; j < E; ++j) {
+                    uint32_t tot = tv[j];
+                    if (F & kFeatTaint) tot += __umul24((uint32_t)cv.wtt, tt_norm(raw[j] & 0xFFFFu, nf.mt, ymt));
+                    if (F & kFeatAffinity) tot += __umul24((uint32_t)cv.wna, na_norm(raw[j] >> 16, nf.ma, yma));
+                    tv[j] = raw[j] != 0xFFFFFFFFu ? tot + 1 : 0u;
+                }
+            } else {
+                const DPodX px{};
+#pragma unroll
+                for (int j = 0; j < E; ++j) {
+                    const uint32_t idx = base + j * kWave;
+                    tv[j] = 0;
+                    if (idx < end) {
+                        RowX x;
+                        const Row r = load_row_coh<F>(t, rs, idx, x);
+                        const bool f = feasible<F>(r, x, p, px);
+                        const uint32_t tot = node_total<F>(r, x, p, px, cv, 0, 0.0, 0, 0.0, nullptr);
+                        tv[j] = f ? tot + 1 : 0;
+                    }
                 }
             }
             if (rdiag) { __syncthreads(); ts1 = __builtin_amdgcn_s_memrealtime(); }
@@ -1676,7 +1771,16 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
             __syncthreads();  // lbuf complete
             if (rdiag) ts2 = __builtin_amdgcn_s_memrealtime();
             uint64_t *out = lists + (size_t)k * 64;
+            // NORM: the pod's NormInfo goes out with its list (written before the list's signal)
+            auto put_norm = [&]() {
+                if (NORM && tid == 0) {
+                    NormInfo *no = norm0 + (size_t)b * 64 + k;
+                    store_coh_u64(reinterpret_cast<uint64_t *>(no), (uint64_t)nf.mt | ((uint64_t)nf.ct << 32));
+                    store_coh_u64(reinterpret_cast<uint64_t *>(no) + 1, (uint64_t)nf.ma | ((uint64_t)nf.ca << 32));
+                }
+            };
             if (G == 1) {
+                put_norm();
                 res_publish_list(lbuf, L, out, &ctl->rdy[b][0]);
             } else {
                 uint64_t *cl = clists + (size_t)k * G * L;
@@ -1698,6 +1802,7 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
                     __syncthreads();  // every wave is done reading lbuf
                     block_topl<kResBS, E2>(te, L, lbuf, [&](int j) { return e[j]; });
                     __syncthreads();
+                    put_norm();
                     res_publish_list(lbuf, L, out, &ctl->rdy[b][0]);
                     ++nmerge;
                 }
@@ -1718,19 +1823,37 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
     }
 }
 
-// Resident four-wave resolver: la_resolve4_block's pipeline (non-normalizing profiles, one list
-// entry per lane) run over every window of the stream without leaving the kernel.  Nothing crosses
-// a window boundary through global memory: the slots won in window w (window w+1's inherited dirty
-// set, §4.1 item 4) are compacted in place through LDS (rows stay on chip), dropped slots' dirty
-// bits are cleared, wave D loads window w+1's pod records at the start of window w, and wave C
-// polls window w+1's lists five pods before the end of window w and prefetches the entries of its
-// first three pods and the candidate rows of its first pod.  Wave A stores the rows won in window
-// w write-through and, two pods into window w+1 (long drained by then), signals done = w + 1.
+// Resident four-wave resolver: la_resolve4_block's pipeline (one list entry per lane) run over every
+// window of the stream without leaving the kernel.  Nothing crosses a window boundary through
+// global memory: the slots won in window w (window w+1's inherited dirty set, §4.1 item 4) are
+// compacted in place through LDS (rows stay on chip), dropped slots' dirty bits are cleared, wave D
+// loads window w+1's pod records at the start of window w, and wave C polls window w+1's lists five
+// pods before the end of window w and prefetches the entries of its first three pods and the
+// candidate rows of its first pod.  Wave A stores the rows won in window w write-through and, two
+// pods into window w+1 (long drained by then), signals done = w + 1.
 // Per window and wave: one prologue barrier, one barrier per pod, two boundary barriers.
+//
+// Normalizing profiles (NORM: TaintToleration / NodeAffinity, config 4): list keys
+// and slot keys are normalized with the selection-time maxima of each pod (NormInfo, published by
+// the selectors with the lists), and waves A/B/C return two "lost holder" flags per key (infeasible
+// now and raw score = the maximum), which wave D counts before its argmax, exactly as
+// la_resolve4_block does.  When a maximum may be lost at pod i, D publishes STOP; after that step's
+// barrier ALL EIGHT waves of the workgroup (the four pipeline waves and the four that otherwise
+// only keep the barrier count) rescan the table exactly for pod i (slot rows from LDS, every other
+// row from HBM), D publishes the winner as an ordinary result — a new slot always with source lane 0,
+// whose staged row, key and flags for pod i+1 wave C writes there — and the pipeline continues with
+// pod i+1, whose precomputed keys cover every outcome of pod i.  Per window one more prologue
+// barrier (B0: the window's NormInfo in LDS before wave A's first keys), four per rescan.  The four
+// extra waves also stage the next window's pod extension records (176 B each) in LDS.
+constexpr uint32_t kResNormK = 32;  // window pods whose NORM records are staged per parity (K <= 32)
 template <uint32_t F>
 constexpr size_t res_stream_lds_bytes(uint32_t n) {
-    return ((((size_t)n + 31) / 32 + 3) & ~(size_t)3) * 4 + 4 * 2 * 64 * 8 + 2 * 64 * (sizeof(RowT<F>) + sizeof(int4)) +
-           2 * sizeof(ResPub) + 3 * 64 * 4 + 64 * (sizeof(RowT<F>) + sizeof(int4)) + 2 * 64 * sizeof(PodT<F>);
+    size_t b = ((((size_t)n + 31) / 32 + 3) & ~(size_t)3) * 4 + 4 * 2 * 64 * 8 + 2 * 64 * (sizeof(RowT<F>) + sizeof(int4)) +
+               2 * sizeof(ResPub) + 3 * 64 * 4 + 64 * (sizeof(RowT<F>) + sizeof(int4)) + 2 * 64 * sizeof(PodT<F>);
+    if ((F & kFeatNorm) != 0)
+        b += 2 * kResNormK * (sizeof(DPodX) + sizeof(NormInfo) + sizeof(double2)) + 2 * 64 * sizeof(RowX) +
+             64 * sizeof(RowX) + 64 * (sizeof(RowT<F>) + sizeof(RowX)) + 2 * 64 * 4 + 64 * 4 + 16 * 4 + 8 * 8 + 16;
+    return b;
 }
 // QS_RES_DIAG_BLOCK build (experiments): per-role busy shader cycles per pod step, barrier exit
 // to barrier entry, into rdiag[8 + role] (D, A, B, C) with the step count in rdiag[12].
@@ -1746,8 +1869,11 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                                                    const DevCfg &c, uint32_t P, uint32_t K, uint32_t nwin,
                                                    const uint64_t *lists0, uint32_t lwords,
                                                    int32_t *__restrict__ out_node, uint64_t *__restrict__ out_key,
-                                                   uint64_t *__restrict__ stamps, ResCtl *ctl, uint64_t *rdiag) {
-    static_assert((F & (kFeatNorm | kFeatWide)) == 0, "compact, non-normalizing profiles");
+                                                   uint64_t *__restrict__ stamps, ResCtl *ctl, uint64_t *rdiag,
+                                                   const DPodX *__restrict__ podx, const NormInfo *norm0,
+                                                   unsigned long long *nfall) {
+    constexpr bool NORM = (F & kFeatNorm) != 0;
+    static_assert((F & kFeatWide) == 0, "compact layout");
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t nwords = (t.n + 31) / 32;
@@ -1765,7 +1891,20 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
     uint32_t *dnode = (uint32_t *)base; base += 64 * 4;  // rank -> node
     RowT<F> *carry = (RowT<F> *)base; base += 64 * sizeof(RowT<F>);
     int4 *carryx = (int4 *)base; base += 64 * sizeof(int4);
-    PodT<F>(*wpods2)[64] = (PodT<F>(*)[64])base;  // window pod records, by window parity
+    PodT<F>(*wpods2)[64] = (PodT<F>(*)[64])base; base += 2 * 64 * sizeof(PodT<F>);  // window pod records, by window parity
+    // NORM only (the host sizes the LDS accordingly)
+    DPodX(*wpodx2)[kResNormK] = (DPodX(*)[kResNormK])base; base += 2 * kResNormK * sizeof(DPodX);
+    NormInfo(*wnorm2)[kResNormK] = (NormInfo(*)[kResNormK])base; base += 2 * kResNormK * sizeof(NormInfo);
+    double2(*wrcp2)[kResNormK] = (double2(*)[kResNormK])base; base += 2 * kResNormK * sizeof(double2);
+    RowX(*stagexN)[64] = (RowX(*)[64])base; base += 2 * 64 * sizeof(RowX);  // full candidate RowX (masks)
+    RowX *carryxN = (RowX *)base; base += 64 * sizeof(RowX);
+    RowT<F> *srow = (RowT<F> *)base; base += 64 * sizeof(RowT<F>);  // rescan: slot rows
+    RowX *sxr = (RowX *)base; base += 64 * sizeof(RowX);
+    uint32_t(*flagC)[64] = (uint32_t(*)[64])base; base += 2 * 64 * 4;  // C's lost-holder flags
+    uint32_t *sidx = (uint32_t *)base; base += 64 * 4;                // rescan: slot lane -> node
+    uint32_t *red_m = (uint32_t *)base; base += 16 * 4;
+    uint64_t *red_k = (uint64_t *)base; base += 8 * 8;
+    uint32_t *snd = (uint32_t *)base;                                  // rescan: slot count
     const ResPub none{0, 0xFFFFFFFFu, -1, -1, 0, {0, 0}};
     const DPodX px{};
     // the LeastAllocated weights and weight-sum reciprocals held in VGPRs: the score's per-lane
@@ -1778,7 +1917,88 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
     for (uint32_t i = threadIdx.x; i < nwords; i += 256) dirty[i] = 0;
     if (threadIdx.x < min(K, P)) wpods2[0][threadIdx.x] = pods[threadIdx.x];
     if (threadIdx.x == 0) pub[1] = none;
+    if constexpr (NORM) {  // window 0's pod extension records
+        constexpr uint32_t q = sizeof(DPodX) / 16;
+        for (uint32_t j = threadIdx.x; j < min(K, P) * q; j += kResBS)
+            reinterpret_cast<int4 *>(&wpodx2[0][0])[j] = reinterpret_cast<const int4 *>(podx)[j];
+    }
     __syncthreads();
+
+    // NORM: exact rescan of window pod i at the current state by all eight waves (wave D has staged
+    // its slot nodes in sidx / snd and wave A the slot rows in srow / sxr before the call).  Rows of
+    // dirty nodes come from the slots, every other row from HBM, where it is current (only slots
+    // change during a window).  Returns the pod's packed key (0 = unschedulable), the same in every
+    // wave.  Three barriers.
+    auto rescan_pass = [&](uint32_t i, uint32_t wb) -> uint64_t {
+        __syncthreads();  // R1: slots staged
+        const uint32_t n = t.n, nds = *snd;
+        const PodT<F> p = wpods2[wb][i];
+        const DPodX pxi = wpodx2[wb][i];
+        constexpr uint32_t U = 4;
+        auto rows_at = [&](uint32_t b0, RowT<F>(&r)[U], RowX(&x)[U]) {
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) {
+                const uint32_t idx = b0 + 64 * u < n ? b0 + 64 * u : 0u;
+                r[u] = load_row<F>(t, idx);
+                x[u] = load_rowx<F>(t, idx);
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) {
+                const uint32_t idx = b0 + 64 * u;
+                if (idx < n && ((dirty[idx >> 5] >> (idx & 31)) & 1u)) {
+                    uint32_t j = 0;
+                    while (j + 1 < nds && sidx[j] != idx) ++j;  // dirty <=> held by a slot
+                    r[u] = srow[j];
+                    x[u] = sxr[j];
+                }
+            }
+        };
+        const uint32_t wid = (uint32_t)wv;
+        uint32_t mt = 0, ma = 0;
+        for (uint32_t b0 = wid * 64 * U + lane; b0 < n; b0 += 8 * 64 * U) {
+            RowT<F> r[U];
+            RowX x[U];
+            rows_at(b0, r, x);
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) {
+                if (b0 + 64 * u < n && feasible<F>(r[u], x[u], p, pxi)) {
+                    const uint32_t a = (F & kFeatTaint) ? taint_raw(x[u], pxi) : 0u;
+                    const uint32_t b2 = (F & kFeatAffinity) ? affinity_raw(x[u], p, pxi) : 0u;
+                    mt = a > mt ? a : mt;
+                    ma = b2 > ma ? b2 : ma;
+                }
+            }
+        }
+        mt = wave_max_u32(mt);
+        ma = wave_max_u32(ma);
+        if (lane == 0) { red_m[2 * wid] = mt; red_m[2 * wid + 1] = ma; }
+        __syncthreads();  // R2
+#pragma unroll
+        for (uint32_t q = 0; q < 8; ++q) {
+            mt = red_m[2 * q] > mt ? red_m[2 * q] : mt;
+            ma = red_m[2 * q + 1] > ma ? red_m[2 * q + 1] : ma;
+        }
+        const double ymt = rcp_exact(mt), yma = rcp_exact(ma);
+        uint64_t best = 0;
+        for (uint32_t b0 = wid * 64 * U + lane; b0 < n; b0 += 8 * 64 * U) {
+            RowT<F> r[U];
+            RowX x[U];
+            rows_at(b0, r, x);
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) {
+                const uint32_t idx = b0 + 64 * u;
+                const uint32_t tv = node_total<F>(r[u], x[u], p, pxi, cv, mt, ymt, ma, yma, nullptr);
+                const uint64_t key = (idx < n && feasible<F>(r[u], x[u], p, pxi)) ? pack_key(tv + 1, idx) : 0ull;
+                best = key > best ? key : best;
+            }
+        }
+        uint64_t ks = wave_max_u64(best);
+        if (lane == 0) red_k[wid] = ks;
+        __syncthreads();  // R3
+#pragma unroll
+        for (uint32_t q = 0; q < 8; ++q) ks = red_k[q] > ks ? red_k[q] : ks;
+        return ks;
+    };
 
     if (wv == 0) {
         // ---- D: pod i's winner from the precomputed keys (la_resolve4_block's wave D) -----------
@@ -1794,14 +2014,27 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
             const int4 npa = pq[0], npb = pq[1];
             uint64_t res_key = 0, res_stamp = 0;
             ResPub pv = none;
+            bool stopped = false;  // NORM: a rescan ran in this window
+            if (NORM) __syncthreads();  // B0
             __syncthreads();  // B1
             for (uint32_t i = 0; i < kend; ++i) {
                 QS_RSTAMP_BEGIN()
                 const int par = i & 1, pp = par ^ 1;
                 const uint64_t a = keyA[pp][lane], b = keyB[pp][lane], cl = keyC[pp][lane];
                 const uint64_t e1 = C1[pp][lane];
+                uint32_t fcl = 0;
+                NormInfo nf{0, 0, 0, 0};
+                if (NORM) {
+                    fcl = flagC[pp][lane];
+                    nf = wnorm2[w & 1][i];
+                }
                 const bool pnew = pv.ks != 0 && pv.slot < 0;
-                const uint64_t sc = (lane == pv.slot) ? b : a;
+                uint64_t sc = (lane == pv.slot) ? b : a;
+                uint32_t fl = 0;  // NORM: lost-holder flags of this slot (bit 0 taint, bit 1 affinity)
+                if (NORM) {
+                    fl = (uint32_t)sc & 3u;
+                    sc &= ~3ull;
+                }
                 uint64_t fk = ((uint32_t)lane < nd && sc) ? (sc | (uint64_t)(0xFFFFFFFFu - didx)) : 0ull;
                 // the new slot's key, read unconditionally (under a branch the compiler sank the
                 // keyC load into it: a second, dependent LDS round trip on D's chain)
@@ -1809,42 +2042,91 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                 const uint64_t cw = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(cl >> 32), srcl) << 32) |
                                     (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)cl, srcl);
                 if (pnew && (uint32_t)lane == pv.nd_old) fk = cw;
-                const uint64_t cand = (pv.ks != 0 && e1 != 0 && key_node(e1) == pv.w) ? 0ull : e1;
-                const uint64_t best = fk > cand ? fk : cand;
-                uint64_t ks;
-                if (K32) {  // (score+1) < 2^10 and n <= 2^22: one 32-bit reduction
-                    const uint32_t tv = (uint32_t)(best >> 32);
-                    const uint32_t k32 = tv ? (tv << 22) | (0x3FFFFFu - key_node(best)) : 0u;
-                    const uint32_t m = wave_max_u32_dpp(k32);
-                    ks = m ? (((uint64_t)(m >> 22) << 32) | (uint64_t)(0xFFFFFFFFu - (0x3FFFFFu - (m & 0x3FFFFFu)))) : 0ull;
+                bool unsafe = false;
+                if (NORM) {
+                    const uint32_t fc = (uint32_t)__builtin_amdgcn_readlane((int)fcl, srcl);
+                    if (pnew && (uint32_t)lane == pv.nd_old) fl = fc;
+                    // do the selection-time maxima still hold for pod i?  A maximum is lost only
+                    // when every node attaining it is dirty and infeasible now
+                    if (F & kFeatTaint)
+                        unsafe |= nf.mt > 0 && (uint32_t)__popcll(__ballot((uint32_t)lane < nd && (fl & 1u))) >= nf.ct;
+                    if (F & kFeatAffinity)
+                        unsafe |= nf.ma > 0 && (uint32_t)__popcll(__ballot((uint32_t)lane < nd && (fl & 2u))) >= nf.ca;
+                }
+                if (NORM && unsafe) {
+                    if (lane == 0) pub[par] = ResPub{0, 0xFFFFFFFFu, -2, -1, nd, {0, 0}};  // STOP
                 } else {
-                    ks = wave_max_u64(best);
-                }
-                ResPub np{ks, ks ? key_node(ks) : 0xFFFFFFFFu, -1, -1, nd, {0, 0}};
-                if (ks) {
-                    const uint64_t own = __ballot((uint32_t)lane < nd && didx == np.w);
-                    if (own) {
-                        np.slot = (int32_t)__builtin_ctzll(own);
-                        won |= lane == np.slot;
+                    const uint64_t cand = (pv.ks != 0 && e1 != 0 && key_node(e1) == pv.w) ? 0ull : e1;
+                    const uint64_t best = fk > cand ? fk : cand;
+                    uint64_t ks;
+                    if (K32) {  // (score+1) < 2^10 and n <= 2^22: one 32-bit reduction
+                        const uint32_t tv = (uint32_t)(best >> 32);
+                        const uint32_t k32 = tv ? (tv << 22) | (0x3FFFFFu - key_node(best)) : 0u;
+                        const uint32_t m = wave_max_u32_dpp(k32);
+                        ks = m ? (((uint64_t)(m >> 22) << 32) | (uint64_t)(0xFFFFFFFFu - (0x3FFFFFu - (m & 0x3FFFFFu)))) : 0ull;
                     } else {
-                        np.src = (int32_t)__builtin_ctzll(__ballot(cand == ks));
-                        if ((uint32_t)lane == nd) { didx = np.w; won = true; }
-                        ++nd;
-                        if (lane == 0)  // dirty from now on: wave C's next dirty-word reads see it
-                            __hip_atomic_fetch_or(&dirty[np.w >> 5], 1u << (np.w & 31), __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+                        ks = wave_max_u64(best);
                     }
-                }
-                pv = np;
-                if (lane == 0) pub[par] = np;
-                if ((uint32_t)lane == i) {
-                    res_key = ks;
-                    if (stamps) res_stamp = __builtin_amdgcn_s_memrealtime();
+                    ResPub np{ks, ks ? key_node(ks) : 0xFFFFFFFFu, -1, -1, nd, {0, 0}};
+                    if (ks) {
+                        const uint64_t own = __ballot((uint32_t)lane < nd && didx == np.w);
+                        if (own) {
+                            np.slot = (int32_t)__builtin_ctzll(own);
+                            won |= lane == np.slot;
+                        } else {
+                            np.src = (int32_t)__builtin_ctzll(__ballot(cand == ks));
+                            if ((uint32_t)lane == nd) { didx = np.w; won = true; }
+                            ++nd;
+                            if (lane == 0)  // dirty from now on: wave C's next dirty-word reads see it
+                                __hip_atomic_fetch_or(&dirty[np.w >> 5], 1u << (np.w & 31), __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+                        }
+                    }
+                    pv = np;
+                    if (lane == 0) pub[par] = np;
+                    if ((uint32_t)lane == i) {
+                        res_key = ks;
+                        if (stamps) res_stamp = __builtin_amdgcn_s_memrealtime();
+                    }
                 }
                 QS_RSTAMP_END()
                 __syncthreads();
+                if (NORM && unsafe) {
+                    // the exact rescan of pod i (every wave), then pod i's result as usual; a new
+                    // slot takes source lane 0, whose staged row / key / flags wave C rewrites
+                    if ((uint32_t)lane < nd) sidx[lane] = didx;
+                    if (lane == 0) *snd = nd;
+                    const uint64_t ks = rescan_pass(i, w & 1);
+                    ResPub np{ks, ks ? key_node(ks) : 0xFFFFFFFFu, -1, -1, nd, {0, 0}};
+                    if (ks) {
+                        const uint64_t own = __ballot((uint32_t)lane < nd && didx == np.w);
+                        if (own) {
+                            np.slot = (int32_t)__builtin_ctzll(own);
+                            won |= lane == np.slot;
+                        } else {
+                            np.src = 0;
+                            if ((uint32_t)lane == nd) { didx = np.w; won = true; }
+                            ++nd;
+                            if (lane == 0)
+                                __hip_atomic_fetch_or(&dirty[np.w >> 5], 1u << (np.w & 31), __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+                        }
+                    }
+                    pv = np;
+                    if (lane == 0) {
+                        pub[par] = np;
+                        if (nfall) atomicAdd(nfall, 1ull);  // pods resolved by an exact rescan
+                    }
+                    if ((uint32_t)lane == i) {
+                        res_key = ks;
+                        if (stamps) res_stamp = __builtin_amdgcn_s_memrealtime();
+                    }
+                    stopped = true;
+                    __syncthreads();  // R5
+                }
             }
             steps_ += kend;
+            if (NORM && stopped && lane == 0 && nfall) atomicAdd(nfall + 1, 1ull);  // windows with a rescan
             if ((uint32_t)lane < kend) {
                 out_node[s0 + lane] = res_key ? (int32_t)key_node(res_key) : -1;
                 if (out_key) out_key[s0 + lane] = res_key;
@@ -1885,10 +2167,27 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
         uint32_t nd = 0;
         uint32_t pend = 0;  // wave A: windows whose rows are stored but not yet signalled (done value)
         const __amdgpu_buffer_rsrc_t rs = row_rsrc(t);
-        auto slot_key = [&](const RowT<F> &r, const RowX &x, const PodT<F> &q) -> uint64_t {
+        // NORM: pod k's extension record, maxima and reciprocals (LDS, read one step ahead)
+        struct PodN {
+            DPodX x;
+            NormInfo nf;
+            double2 yr;
+        };
+        auto slot_key = [&](const RowT<F> &r, const RowX &x, const PodT<F> &q, const PodN &pn) -> uint64_t {
+            const bool act = (uint32_t)lane < nd;
+            if constexpr (NORM) {
+                const bool f = feasible<F>(r, x, q, pn.x);
+                const uint32_t tot = node_total<F>(r, x, q, pn.x, cv, pn.nf.mt, pn.yr.x, pn.nf.ma, pn.yr.y, nullptr);
+                uint32_t fl = 0;
+                if (act && !f) {
+                    if (F & kFeatTaint) fl |= taint_raw(x, pn.x) == pn.nf.mt ? 1u : 0u;
+                    if (F & kFeatAffinity) fl |= affinity_raw(x, q, pn.x) == pn.nf.ma ? 2u : 0u;
+                }
+                return ((act && f) ? ((uint64_t)(tot + 1) << 32) : 0ull) | fl;
+            }
             const bool f = feasible<F>(r, x, q, px);
             const uint32_t tot = node_total<F>(r, x, q, px, cv, 0, 0.0, 0, 0.0, nullptr);
-            return ((uint32_t)lane < nd && f) ? ((uint64_t)(tot + 1) << 32) : 0ull;
+            return (act && f) ? ((uint64_t)(tot + 1) << 32) : 0ull;
         };
         auto apply = [&](const ResPub &pv, int pp, const PodT<F> &pprev) {
             if (pv.ks == 0) return;
@@ -1897,7 +2196,9 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
             } else {
                 if ((uint32_t)lane == pv.nd_old) {
                     S = stage[pp][pv.src];
-                    if (F & kFeatExt) {
+                    if constexpr (NORM) {
+                        SX = stagexN[pp][pv.src];
+                    } else if (F & kFeatExt) {
                         const int4 e = stagex[pp][pv.src];
                         SX.ae0 = e.x; SX.re0 = e.y; SX.ae1 = e.z; SX.re1 = e.w;
                     }
@@ -1906,19 +2207,37 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                 ++nd;
             }
         };
+        // NORM: D stopped at window pod j: stage the slot rows (wave A), rescan with every wave
+        auto rescan_ab = [&](uint32_t j, uint32_t wb) {
+            if (wv == 1 && (uint32_t)lane < nd) { srow[lane] = S; sxr[lane] = SX; }
+            (void)rescan_pass(j, wb);
+            __syncthreads();  // R5
+        };
         for (uint32_t w = 0; w < nwin; ++w) {
             const uint32_t s0 = w * K, kend = min(K, P - s0);
             const PodT<F> *wp = wpods2[w & 1];
-            if (wv == 1 && nd > 0) keyA[1][lane] = slot_key(S, SX, wp[0]);  // pod 0, inherited slots
+            auto podn = [&](uint32_t k) -> PodN {
+                PodN r{};
+                if constexpr (NORM)
+                    if (k < kend) r = PodN{wpodx2[w & 1][k], wnorm2[w & 1][k], wrcp2[w & 1][k]};
+                return r;
+            };
+            if (NORM) __syncthreads();  // B0 (the window's NormInfo is in LDS)
+            if (wv == 1 && nd > 0) keyA[1][lane] = slot_key(S, SX, wp[0], podn(0));  // pod 0, inherited slots
             __syncthreads();  // B1
             const uint32_t isig = min(2u, kend - 1);
             PodT<F> pprev = wp[0], pcur = wp[0];  // pods i-1 and i (pod i+1's record is read each step)
+            PodN pnx = podn(1);                   // NORM: pod i+1's record at step i
             for (uint32_t i = 0; i < kend; ++i) {
                 QS_RSTAMP_BEGIN()
                 const int par = i & 1, pp = par ^ 1;
-                const ResPub pv = read_pub(&pub[pp]);
+                ResPub pv = read_pub(&pub[pp]);
                 const PodT<F> pn1 = wp[i + 1];
                 __builtin_amdgcn_sched_barrier(0);  // both LDS reads go out before the pub's wait
+                if (NORM && i > 0 && pv.slot == -2) {  // D stopped at pod i-1
+                    rescan_ab(i - 1, w & 1);
+                    pv = read_pub(&pub[pp]);
+                }
                 if (i > 0) apply(pv, pp, pprev);
                 if (wv == 1 && pend && i == isig) {
                     // the previous window's rows went out write-through a window boundary ago
@@ -1927,16 +2246,19 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                     pend = 0;
                 }
                 if (i + 1 < kend) {
+                    const PodN pnc = pnx;
+                    if (NORM) pnx = podn(i + 2);  // next step's record: its LDS reads overlap this score
                     RowT<F> s2 = S;
                     RowX x2s = SX;
                     if (wv == 2) reserve(s2, x2s, pcur, +1);
-                    (wv == 1 ? keyA : keyB)[par][lane] = slot_key(s2, x2s, pn1);
+                    (wv == 1 ? keyA : keyB)[par][lane] = slot_key(s2, x2s, pn1, pnc);
                 }
                 pprev = pcur;
                 pcur = pn1;
                 QS_RSTAMP_END()
                 __syncthreads();
             }
+            if (NORM && read_pub(&pub[(kend - 1) & 1]).slot == -2) rescan_ab(kend - 1, w & 1);
             apply(read_pub(&pub[(kend - 1) & 1]), (kend - 1) & 1, pprev);
             __syncthreads();  // B2 (D's slot ranks and nodes)
             const uint32_t rk = xrank[lane];
@@ -1944,15 +2266,20 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
             if (wv == 1 && keep) {
                 store_row_coh<F>(t, rs, xnode[lane], S, SX);
                 carry[rk] = S;
-                carryx[rk] = make_int4(SX.ae0, SX.re0, SX.ae1, SX.re1);
+                if constexpr (NORM) carryxN[rk] = SX;
+                else carryx[rk] = make_int4(SX.ae0, SX.re0, SX.ae1, SX.re1);
             }
             if (wv == 1) pend = w + 1;
             __syncthreads();  // B3
             nd = (uint32_t)__popcll(__ballot(keep));
             if ((uint32_t)lane < nd) {
                 S = carry[lane];
-                const int4 e = carryx[lane];
-                SX.ae0 = e.x; SX.re0 = e.y; SX.ae1 = e.z; SX.re1 = e.w;
+                if constexpr (NORM) {
+                    SX = carryxN[lane];
+                } else {
+                    const int4 e = carryx[lane];
+                    SX.ae0 = e.x; SX.re0 = e.y; SX.ae1 = e.z; SX.re1 = e.w;
+                }
             } else {
                 S = empty_row<F>();
                 SX = RowX{};
@@ -1962,17 +2289,24 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
             drain_stores();
             if (lane == 0) __hip_atomic_store((gu32 *)&ctl->done, pend, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-    } else {
+    } else if (wv == 3) {
         // ---- C: candidate rows, C keys, the next pod's best clean entry; next-window prefetch -----
         uint64_t eX = 0, eY = 0, c1 = 0;
         RowT<F> r1 = empty_row<F>();
         RowX x1{};
         bool pref = false;  // window w's first entries and first candidate rows already loaded
         uint64_t pe0 = 0, pe1 = 0, pe2 = 0;
+        uint64_t pn0 = 0, pn1w = 0;  // NORM: the next window's NormInfo of this lane's pod (prefetched)
         uint32_t rdyv = 0, nfallback = 0;
         auto dirty_bit = [&](uint64_t e) -> bool {
             const uint32_t nidx = e ? key_node(e) : 0u;
             return (dirty[nidx >> 5] >> (nidx & 31)) & 1u;
+        };
+        // NORM: NormInfo of lane `lane`'s pod into the window's LDS arrays (+ the reciprocals)
+        auto put_norm = [&](uint32_t wb, uint64_t lo, uint64_t hi) {
+            const NormInfo nf{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+            wnorm2[wb][lane] = nf;
+            wrcp2[wb][lane] = make_double2(rcp_exact(nf.mt), rcp_exact(nf.ma));
         };
         for (uint32_t w = 0; w < nwin; ++w) {
             const uint32_t s0 = w * K, kend = min(K, P - s0);
@@ -1985,6 +2319,42 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
             auto ent = [&](const uint64_t *l, uint32_t pod, uint32_t kk) -> uint64_t {
                 return pod < kk ? load_coh_u64(l + (size_t)pod * 64 + lane) : 0ull;
             };
+            // NORM: D stopped at window pod j: rescan with every wave, then (a new slot) pod j's
+            // winner as source lane 0 of step j's staging: its row before pod j, and its key and
+            // lost-holder flags for pod j+1 after pod j
+            auto rescan_c = [&](uint32_t j) {
+                const uint64_t ks = rescan_pass(j, w & 1);
+                if (ks && j + 1 < kend) {
+                    const uint32_t W = key_node(ks);
+                    const bool slot = __ballot((uint32_t)lane < *snd && sidx[lane] == W) != 0;
+                    if (!slot) {
+                        const int pj = j & 1;
+                        const RowT<F> rw = load_row<F>(t, W);
+                        const RowX xw = load_rowx<F>(t, W);
+                        RowT<F> cr = rw;
+                        RowX crx = xw;
+                        reserve(cr, crx, wp[j], +1);
+                        const PodT<F> q1 = wp[j + 1];
+                        const DPodX qx = wpodx2[w & 1][j + 1];
+                        const NormInfo nf = wnorm2[w & 1][j + 1];
+                        const double2 yr = wrcp2[w & 1][j + 1];
+                        const bool f = feasible<F>(cr, crx, q1, qx);
+                        const uint32_t tot = node_total<F>(cr, crx, q1, qx, cv, nf.mt, yr.x, nf.ma, yr.y, nullptr);
+                        uint32_t fl = 0;
+                        if (!f) {
+                            if (F & kFeatTaint) fl |= taint_raw(crx, qx) == nf.mt ? 1u : 0u;
+                            if (F & kFeatAffinity) fl |= affinity_raw(crx, q1, qx) == nf.ma ? 2u : 0u;
+                        }
+                        if (lane == 0) {
+                            stage[pj][0] = rw;
+                            stagexN[pj][0] = xw;
+                            keyC[pj][0] = f ? pack_key(tot + 1, W) : 0ull;
+                            flagC[pj][0] = fl;
+                        }
+                    }
+                }
+                __syncthreads();  // R5
+            };
             uint64_t e0;
             if (pref) {
                 e0 = pe0; eX = pe1; eY = pe2;
@@ -1995,6 +2365,12 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                 e0 = ent(lists, 0, kend);
                 eX = ent(lists, 1, kend);
                 eY = ent(lists, 2, kend);
+                if constexpr (NORM) {
+                    if ((uint32_t)lane < kend) {
+                        const uint64_t *nq = reinterpret_cast<const uint64_t *>(norm0 + (size_t)(w & 1) * 64 + lane);
+                        put_norm(w & 1, load_coh_u64(nq), load_coh_u64(nq + 1));
+                    }
+                }
             }
             c1 = (e0 != 0 && !dirty_bit(e0)) ? e0 : 0ull;
             C1[1][lane] = c1;
@@ -2003,6 +2379,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                 x1 = load_rowx<F>(t, c1 ? key_node(c1) : 0u);
             }  // else r1 / x1 hold e0's row (loaded at the previous window's last pod)
             pref = false;
+            if (NORM) __syncthreads();  // B0
             __syncthreads();  // B1
             const bool pfw = hasnext && kend >= 6;  // prefetch the next window during this one
             PodT<F> pcur = wp[0];  // pod i's record (pod i+1's is read each step)
@@ -2015,19 +2392,41 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                 // C never reads the published winner: a candidate taken by pod i-1's winner is
                 // masked by D, which then never names that lane as a new slot's source.
                 const uint32_t en_node = en ? key_node(en) : 0u;
-                const uint32_t dword = dirty[en_node >> 5];
+                uint32_t dword = dirty[en_node >> 5];
                 const PodT<F> pn1 = wp[i + 1];
+                const uint32_t kn = min(i + 1, kend - 1);
+                DPodX qx{};
+                NormInfo nf{0, 0, 0, 0};
+                double2 yr = make_double2(0.0, 0.0);
+                int32_t stop = 0;
+                if constexpr (NORM) {
+                    qx = wpodx2[w & 1][kn];
+                    nf = wnorm2[w & 1][kn];
+                    yr = wrcp2[w & 1][kn];
+                    stop = pub[par ^ 1].slot;  // NORM only: a STOP of pod i-1 is read here
+                }
                 __builtin_amdgcn_sched_barrier(0);  // both LDS reads go out before their waits
+                if (NORM && i > 0 && stop == -2) {
+                    rescan_c(i - 1);
+                    dword = dirty[en_node >> 5];  // pod i-1's rescanned winner is dirty now
+                }
                 // keyC's score (candidate c1's row + pod i, scored for pod i+1) needs no pub
                 RowT<F> cr = r1;
                 RowX crx = x1;
                 reserve(cr, crx, pcur, +1);
-                const bool f = feasible<F>(cr, crx, pn1, px);
-                const uint32_t tot = node_total<F>(cr, crx, pn1, px, cv, 0, 0.0, 0, 0.0, nullptr);
+                const bool f = feasible<F>(cr, crx, pn1, NORM ? qx : px);
+                const uint32_t tot = node_total<F>(cr, crx, pn1, NORM ? qx : px, cv, nf.mt, yr.x, nf.ma, yr.y, nullptr);
+                uint32_t fl = 0;
+                if (NORM && !f) {
+                    if (F & kFeatTaint) fl |= taint_raw(crx, qx) == nf.mt ? 1u : 0u;
+                    if (F & kFeatAffinity) fl |= affinity_raw(crx, pn1, qx) == nf.ma ? 2u : 0u;
+                }
                 stage[par][lane] = r1;
-                if (F & kFeatExt) stagex[par][lane] = make_int4(x1.ae0, x1.re0, x1.ae1, x1.re1);
+                if constexpr (NORM) stagexN[par][lane] = x1;
+                else if (F & kFeatExt) stagex[par][lane] = make_int4(x1.ae0, x1.re0, x1.ae1, x1.re1);
                 if (i + 1 < kend) {
                     keyC[par][lane] = (c1 != 0 && f) ? pack_key(tot + 1, key_node(c1)) : 0ull;
+                    if (NORM) flagC[par][lane] = fl;
                     const bool dirt = ((dword >> (en_node & 31)) & 1u) != 0;
                     c1 = (en != 0 && !dirt) ? en : 0ull;  // pod i+1 against the dirty set through pod i-1
                     C1[par][lane] = c1;
@@ -2050,6 +2449,12 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                             pe0 = ent(listsn, 0, knext);
                             pe1 = ent(listsn, 1, knext);
                             pe2 = ent(listsn, 2, knext);
+                            if constexpr (NORM) {
+                                const uint64_t *nq =
+                                    reinterpret_cast<const uint64_t *>(norm0 + (size_t)((w + 1) & 1) * 64 + lane);
+                                pn0 = (uint32_t)lane < knext ? load_coh_u64(nq) : 0ull;
+                                pn1w = (uint32_t)lane < knext ? load_coh_u64(nq + 1) : 0ull;
+                            }
                         }
                     }
                 }
@@ -2069,12 +2474,41 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                 step(hooked, i + 1, eY);
             }
             if (i < kend) step(hooked, i, eX);
+            if (NORM && pub[(kend - 1) & 1].slot == -2) rescan_c(kend - 1);
+            if (NORM && pref && (uint32_t)lane < knext) put_norm((w + 1) & 1, pn0, pn1w);
             __syncthreads();  // B2
             __syncthreads();  // B3 (D cleared the dropped slots' dirty bits before B2)
         }
         if (rdiag && lane == 0) rdiag[4] = nfallback;
+    } else if constexpr (NORM) {
+        // ---- waves 4-7: the rescans' extra hands; stage the next window's pod extension records --
+        constexpr uint32_t q = sizeof(DPodX) / 16;
+        for (uint32_t w = 0; w < nwin; ++w) {
+            const uint32_t s0 = w * K, kend = min(K, P - s0);
+            const uint32_t knext = w + 1 < nwin ? min(K, P - s0 - K) : 0u;
+            const uint32_t id0 = (uint32_t)(wv - 4) * 64 + lane, id1 = id0 + 256;
+            const bool h0 = id0 < knext * q, h1 = id1 < knext * q;
+            const int4 *src = reinterpret_cast<const int4 *>(podx + (size_t)s0 + K);
+            int4 q0 = make_int4(0, 0, 0, 0), q1 = make_int4(0, 0, 0, 0);
+            if (h0) q0 = src[id0];
+            if (h1) q1 = src[id1];
+            __syncthreads();  // B0
+            __syncthreads();  // B1
+            for (uint32_t i = 0; i < kend; ++i) {
+                __syncthreads();
+                if (pub[i & 1].slot == -2) {
+                    (void)rescan_pass(i, w & 1);
+                    __syncthreads();  // R5
+                }
+            }
+            int4 *dst = reinterpret_cast<int4 *>(&wpodx2[(w + 1) & 1][0]);
+            if (h0) dst[id0] = q0;
+            if (h1) dst[id1] = q1;
+            __syncthreads();  // B2
+            __syncthreads();  // B3
+        }
     }
-    if (kResDiag && rdiag && lane == 0) {
+    if (kResDiag && rdiag && lane == 0 && wv < 4) {
         rdiag[8 + wv] = busy_;
         if (wv == 0) rdiag[12] = steps_;
     }
@@ -2087,31 +2521,34 @@ __global__ __launch_bounds__(kResBS) void k_la_stream_res(DevTable t, const PodT
                                                        uint32_t P, uint32_t K, uint32_t G, uint32_t L,
                                                        uint32_t chunk, uint32_t nwin, uint64_t *lists0,
                                                        uint64_t *clists0, uint32_t lwords, uint32_t cwords,
-                                                       uint32_t *dio, int32_t *__restrict__ out_node,
+                                                       int32_t *__restrict__ out_node,
                                                        uint64_t *__restrict__ out_key,
                                                        uint64_t *__restrict__ stamps, ResCtl *ctl,
-                                                       uint64_t *__restrict__ rdiag) {
+                                                       uint64_t *__restrict__ rdiag, const DPodX *__restrict__ podx,
+                                                       uint4 *npart0, NormInfo *norm0, unsigned long long *nfall) {
     if (blockIdx.x != 0) {
         res_selector<E, E2, F>(t, pods, c, P, K, G, L, chunk, nwin, lists0, clists0, lwords, cwords, ctl,
-                               blockIdx.x - 1, gridDim.x - 1, rdiag);
+                               blockIdx.x - 1, gridDim.x - 1, rdiag, podx, npart0, norm0);
         return;
     }
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    if (threadIdx.x >= 256) {  // not a pipeline wave: the same barrier count (1 + per window kend + 3)
+    if ((F & kFeatNorm) == 0 && threadIdx.x >= 256) {
+        // not a pipeline wave: the same barrier count (1 + per window kend + 3)
         __syncthreads();
         for (uint32_t w = 0; w < nwin; ++w)
             for (uint32_t j = 0, nb = min(K, P - w * K) + 3; j < nb; ++j) __syncthreads();
         return;
     }
     const uint64_t t0 = rdiag ? __builtin_amdgcn_s_memrealtime() : 0ull;
-    la_resolve4_stream<F, K32>(lds, t, pods, c, P, K, nwin, lists0, lwords, out_node, out_key, stamps, ctl, rdiag);
+    la_resolve4_stream<F, K32>(lds, t, pods, c, P, K, nwin, lists0, lwords, out_node, out_key, stamps, ctl, rdiag,
+                               podx, norm0, nfall);
     if (rdiag && threadIdx.x == 0) { rdiag[1] = __builtin_amdgcn_s_memrealtime() - t0; rdiag[3] = nwin; }
-    (void)dio;
 }
 
 template <uint32_t F>
-static hipError_t la_stream_res_f(const DevTable &t, const void *pods, const DevCfg &c, uint32_t P, const LaGeom &geo,
-                                  uint64_t *lists0, uint64_t *clists0, uint32_t lwords, uint32_t cwords, uint32_t *dio,
+static hipError_t la_stream_res_f(const DevTable &t, const void *pods, const DPodX *podx, const DevCfg &c, uint32_t P,
+                                  const LaGeom &geo, uint64_t *lists0, uint64_t *clists0, uint32_t lwords,
+                                  uint32_t cwords, uint4 *npart0, NormInfo *norm0, unsigned long long *nfall,
                                   int32_t *on, uint64_t *ok, uint64_t *st, void *ctl, uint32_t sel_blocks,
                                   uint64_t *rdiag, hipStream_t stream) {
     const uint32_t K = geo.K, G = geo.G, L = geo.L, nwin = (P + K - 1) / K;
@@ -2119,12 +2556,17 @@ static hipError_t la_stream_res_f(const DevTable &t, const void *pods, const Dev
     if (G * L > (uint32_t)kResBS) return hipErrorInvalidValue;
     const size_t lds4 = res_stream_lds_bytes<F>(t.n);
     if (lds4 > 64 * 1024) return hipErrorInvalidValue;
+    // NORM: K <= kResNormK staged records per window, and a task per workgroup (the G chunks of a
+    // pod wait for each other's partial maxima)
+    if ((F & kFeatNorm) && (K > kResNormK || sel_blocks < K * G || !podx || !npart0 || !norm0))
+        return hipErrorInvalidValue;
     const dim3 grid(1 + sel_blocks);
     const PodT<F> *pp = (const PodT<F> *)pods;
     ResCtl *rc = (ResCtl *)ctl;
 #define QS_RESK(EE, EE2, KK)                                                                                          \
     hipLaunchKernelGGL((k_la_stream_res<F, EE, EE2, KK>), grid, dim3(kResBS), lds4, stream, t, pp, c, P, K, G, L,       \
-                       geo.chunk, nwin, lists0, clists0, lwords, cwords, dio, on, ok, st, rc, rdiag)
+                       geo.chunk, nwin, lists0, clists0, lwords, cwords, on, ok, st, rc, rdiag, podx, npart0, norm0,   \
+                       nfall)
 #define QS_RESE(EE, EE2) \
     else if (geo.E == EE && E2 == EE2) { if (geo.k32) QS_RESK(EE, EE2, true); else QS_RESK(EE, EE2, false); }
     if (false) {

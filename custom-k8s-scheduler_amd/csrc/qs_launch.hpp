@@ -84,10 +84,14 @@ LaGeom la_stream_res_plan(const LaGeom &geo, uint32_t feat, uint32_t n, uint32_t
 size_t la_stream_res_ctl_bytes();
 // Workgroups of that launch guaranteed co-resident on `cus` CUs (occupancy query, one per CU of margin).
 uint32_t la_stream_res_max_blocks(const LaGeom &geo, uint32_t feat, uint32_t n, uint32_t cus);
-hipError_t launch_la_stream_res(const DevTable &t, const void *pods, const DevCfg &c, uint32_t P, const LaGeom &geo,
-                                uint64_t *lists0, uint64_t *clists0, uint32_t lwords, uint32_t cwords, uint32_t *dio,
-                                int32_t *on, uint64_t *ok, uint64_t *st, void *ctl, uint32_t sel_blocks,
-                                uint64_t *rdiag, hipStream_t stream);
+// Normalizing profiles (TaintToleration / NodeAffinity) also pass the pod extension records (podx),
+// npart (2 x K x G uint4 partial maxima), norm (2 x 64 NormInfo) and nfall ({rescans, windows with
+// a rescan}); they need K <= 32 and sel_blocks >= K * G.
+hipError_t launch_la_stream_res(const DevTable &t, const void *pods, const DPodX *podx, const DevCfg &c, uint32_t P,
+                                const LaGeom &geo, uint64_t *lists0, uint64_t *clists0, uint32_t lwords,
+                                uint32_t cwords, uint4 *npart, NormInfo *norm, unsigned long long *nfall, int32_t *on,
+                                uint64_t *ok, uint64_t *st, void *ctl, uint32_t sel_blocks, uint64_t *rdiag,
+                                hipStream_t stream);
 
 hipError_t launch_la_window(const DevTable &t, const void *pods, const DPodX *podx, uint32_t s0,
                             uint32_t P, const DevCfg &c, const LaGeom &geo, const LaBufs &bufs,

@@ -75,6 +75,7 @@ def test_config4_full_lookahead(oracle, serial):
     o = run_oracle(oracle, nodes, pods, CFG4)
     assert_same(g[:2], o[:2], g[2], o[2])
     assert g[3]["engine_used"] == "lookahead"
+    assert g[3]["resident"] == (1 if serial == 0 else 0)  # overlapped windows: one resident launch
 
 
 @pytest.mark.parametrize("waves", ["4", "1"])
@@ -165,3 +166,24 @@ def test_balanced_skip_besteffort(oracle):
     g = run_gpu(nodes, pods, dict(balanced_skip_besteffort=1), "lookahead")
     o = run_oracle(oracle, nodes, pods, dict(balanced_skip_besteffort=1))
     assert_same(g[:2], o[:2], g[2], o[2])
+
+
+@pytest.mark.parametrize("n,p,K", [(400, 14000, 32), (2000, 6000, 32), (5000, 20000, 32), (9000, 8000, 16),
+                                   (3000, 5000, 7), (600, 4000, 1), (20000, 3000, 32)])
+def test_resident_stream_norm(oracle, monkeypatch, n, p, K):
+    """Normalizing profiles (TaintToleration + NodeAffinity + amd.com/gpu, config 4) as ONE resident
+    launch: selectors publish the chunks' partial maxima and combine them per pod
+    before scoring, the resolver tests the maxima per pod and rescans a pod exactly with all eight
+    waves when one may be lost.  Bit-exact vs the oracle, and identical to the per-window launches;
+    the tight cluster (400 nodes) must take the rescan path."""
+    nodes, pods = synth_generate(4, n, p)
+    g = run_gpu(nodes, pods, CFG4, "lookahead", lookahead=K)
+    assert g[3]["resident"] == 1
+    o = run_oracle(oracle, nodes, pods, CFG4)
+    assert_same(g[:2], o[:2], g[2], o[2])
+    if n == 400:
+        assert g[3]["truncations"] > 0 and g[3]["resumed_windows"] > 0
+    monkeypatch.setenv("QS_RESIDENT", "0")
+    w = run_gpu(nodes, pods, CFG4, "lookahead", lookahead=K)
+    assert w[3]["resident"] == 0
+    assert np.array_equal(w[0], g[0]) and np.array_equal(w[1], g[1])

@@ -10,14 +10,16 @@ cfgno = int(os.environ.get("CFG", 2))
 nodes, pods = qsched.synth_generate(cfgno, n, p)
 ref = None
 for eng, K in [(e.split(":")[0], int(e.split(":")[1])) for e in os.environ.get("RUNS", "lookahead:64").split(",")]:
-    s = qsched.Scheduler({"engine": eng, "lookahead": K})
+    prof = {"enable_taint": 1, "enable_affinity": 1} if cfgno == 4 else {}
+    s = qsched.Scheduler(dict({"engine": eng, "lookahead": K}, **prof))
     s.load_nodes(nodes); s.save_table()
     st = s.prepare(pods)
     walls = []
     for r in range(4):
         s.restore_table()
-        walls.append(st.run()["wall_s"])
+        stats = st.run()
+        walls.append(stats["wall_s"])
     pl, _ = st.results()
     if ref is None: ref = pl
-    print(f"{eng:10s} K={K:3d} ms/stream={1e3*min(walls[1:]):8.2f}  pods/s={p/min(walls[1:]):12.0f} same={np.array_equal(pl, ref)}", flush=True)
+    print(f"{eng:10s} K={K:3d} ms/stream={1e3*min(walls[1:]):8.2f}  pods/s={p/min(walls[1:]):12.0f} same={np.array_equal(pl, ref)} resident={stats['resident']} rescans={stats['truncations']} stopped_windows={stats['resumed_windows']}", flush=True)
     st.free(); s.close()
