@@ -176,7 +176,14 @@ constexpr size_t kMbRanks = 16, kMbSlots = 3, kMbPartPerRank = 4096;
 constexpr size_t kMbFlags = 2 * kMbRanks * 8;
 constexpr size_t kMbListSlot = kMbRanks * 64 * 64 * 8;
 constexpr size_t kMbPartSlot = kMbRanks * kMbPartPerRank * 16;
-constexpr size_t kMbBytes = kMbFlags + kMbSlots * (kMbListSlot + kMbPartSlot);
+// Resident sharded stream, after the per-window regions: hello[16] (each rank's run
+// sequence, the in-launch entry barrier), flags[4 slots][32 pods][16 ranks] and shard lists
+// [4 slots][32 pods][16 ranks][64] u64 (window w uses slot w % 4).
+constexpr size_t kMbResSlots = 4, kMbResPods = 32;
+constexpr size_t kMbResHello = kMbFlags + kMbSlots * (kMbListSlot + kMbPartSlot);
+constexpr size_t kMbResFlags = kMbResHello + 256;
+constexpr size_t kMbResLists = kMbResFlags + kMbResSlots * kMbResPods * kMbRanks * 8;
+constexpr size_t kMbBytes = kMbResLists + kMbResSlots * kMbResPods * kMbRanks * 64 * 8;
 inline uint64_t *mbox_lists(qs_ctx *c, uint32_t slot) {
     return reinterpret_cast<uint64_t *>(static_cast<char *>(c->mbox.p) + kMbFlags + slot * kMbListSlot);
 }

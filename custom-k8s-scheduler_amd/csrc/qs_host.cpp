@@ -66,8 +66,10 @@ DevCfg make_devcfg(const qs_config &c) {
     d.yd_both = rcp(c.fit_weight_cpu + c.fit_weight_mem);
     d.yd_c = rcp(c.fit_weight_cpu);
     d.yd_m = rcp(c.fit_weight_mem);
-    d.wtt = c.w_taint;
-    d.wna = c.w_affinity;
+    // a disabled plugin weighs 0 (the kernels of the normalizing class evaluate both plugins; the
+    // pod records of a disabled plugin are neutral, see compact_pod / compact_podx)
+    d.wtt = c.enable_taint ? c.w_taint : 0;
+    d.wna = c.enable_affinity ? c.w_affinity : 0;
     d.feat = feat_of(c);
     d.ba_skip_be = c.balanced_skip_besteffort ? 1u : 0u;
     return d;
@@ -323,8 +325,12 @@ void check_pod(const qs_pod &p, uint32_t j) {
     if (p.anti_affinity < QS_AA_NONE || p.anti_affinity > QS_AA_ZONE) bad("anti_affinity must be 0..2");
 }
 
-uint32_t pod_flags(const qs_pod &p) {
-    return (uint32_t)p.qos | ((uint32_t)p.n_req_terms << 4) | ((uint32_t)p.n_pref_terms << 8) |
+// NodeAffinity disabled (config.enable_affinity = 0): the pod's required / preferred term counts are
+// recorded as 0, so the normalizing kernels (which evaluate both plugins) neither filter nor score
+// by affinity.
+uint32_t pod_flags(const qs_ctx *c, const qs_pod &p) {
+    const uint32_t aff = c->cfg.enable_affinity ? 1u : 0u;
+    return (uint32_t)p.qos | (aff * (uint32_t)p.n_req_terms << 4) | (aff * (uint32_t)p.n_pref_terms << 8) |
            ((uint32_t)p.anti_affinity << 12) | ((uint32_t)p.app << 16);
 }
 
@@ -344,7 +350,7 @@ void compact_pod(const qs_ctx *c, const qs_pod &p, uint32_t j, int shift, bool w
         d.re1 = (int32_t)p.req_ext[1];
         d.wfit = (uint16_t)c->cfg.w_fit[p.qos];
         d.wbal = (uint16_t)c->cfg.w_bal[p.qos];
-        d.flags = pod_flags(p);
+        d.flags = pod_flags(c, p);
         std::memcpy(dst, &d, sizeof d);
         return;
     }
@@ -359,16 +365,20 @@ void compact_pod(const qs_ctx *c, const qs_pod &p, uint32_t j, int shift, bool w
     d.re1 = (int32_t)p.req_ext[1];
     d.wfit = (uint16_t)c->cfg.w_fit[p.qos];
     d.wbal = (uint16_t)c->cfg.w_bal[p.qos];
-    d.flags = pod_flags(p);
+    d.flags = pod_flags(c, p);
     std::memcpy(dst, &d, sizeof d);
 }
 
-DPodX compact_podx(const qs_pod &p) {
+// A disabled plugin's part of the record is neutral: TaintToleration off -> every taint tolerated
+// (Filter passes, raw score 0); NodeAffinity off -> no nodeSelector (the term counts are 0 in the
+// pod flags).
+DPodX compact_podx(const qs_ctx *c, const qs_pod &p) {
     DPodX x{};
-    x.tol_hard = p.tol_hard;
-    x.tol_soft = p.tol_soft;
-    x.sel0 = p.sel[0];
-    x.sel1 = p.sel[1];
+    const bool taint = c->cfg.enable_taint != 0, aff = c->cfg.enable_affinity != 0;
+    x.tol_hard = taint ? p.tol_hard : ~0ull;
+    x.tol_soft = taint ? p.tol_soft : ~0ull;
+    x.sel0 = aff ? p.sel[0] : 0ull;
+    x.sel1 = aff ? p.sel[1] : 0ull;
     for (int t = 0; t < QS_MAX_TERMS; t++) {
         x.req[t][0] = p.req_terms[t][0];
         x.req[t][1] = p.req_terms[t][1];
@@ -909,7 +919,7 @@ qs_status qs_score_pod(qs_ctx *c, const qs_pod *pod, uint8_t *feas, int32_t *sco
         ensure_layout(c, pod, 1);
         alignas(16) uint8_t dp[sizeof(DPodW)];
         compact_pod(c, *pod, 0, c->shift, c->wide, dp);
-        const DPodX dx = compact_podx(*pod);
+        const DPodX dx = compact_podx(c, *pod);
         c->dc.feat = feat_of(c->cfg) | ((pod->req_ext[0] || pod->req_ext[1]) ? kFeatExt : 0u) |
                      (c->wide ? kFeatWide | kFeatExt : 0u);
         c->one_pod.ensure(sizeof(DPodW));
@@ -962,7 +972,7 @@ qs_status qs_stream_prepare(qs_ctx *c, const qs_pod *pods, uint32_t p, qs_stream
         for (uint32_t k = 0; k < p; k++) {
             const uint32_t j = s->order[k];
             compact_pod(c, pods[j], j, c->shift, c->wide, dp.data() + rb * k);
-            if (needx) dx[k] = compact_podx(pods[j]);
+            if (needx) dx[k] = compact_podx(c, pods[j]);
         }
         const size_t P1 = std::max<uint32_t>(p, 1);
         s->d_pods.ensure(rb * P1);
@@ -1238,8 +1248,12 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                 // query guarantees that all 1 + sel of them run at once (VERDICT r2 missing #5)
                 const bool coresident =
                     rgeo.G > 0 && 1 + sel <= la_stream_res_max_blocks(rgeo, c->dc.feat, n, (uint32_t)c->cus);
-                const bool resident = overlap && !c->comm && !mbox && c->world == 1 && !c->resident_off &&
-                                      !diag_on && !c->wide && !(renv && renv[0] == '0') && rgeo.G > 0 && coresident;
+                // unsharded contexts, and mailbox-sharded ones for Fit + Balanced (+ extended)
+                // profiles: there the selectors exchange every pod's shard list through the peers'
+                // mailboxes inside the launch (RCCL cannot be called in a kernel)
+                const bool res_transport = c->world == 1 ? !mbox && !c->comm : mbox && !norm;
+                const bool resident = overlap && res_transport && !c->resident_off && !diag_on && !c->wide &&
+                                      !(renv && renv[0] == '0') && rgeo.G > 0 && coresident;
                 c->last_resident = resident;
                 if (resident) {
                     c->resctl.ensure(la_stream_res_ctl_bytes());
@@ -1256,6 +1270,14 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                     c->npart.ensure(16 * 2 * (size_t)rgeo.K * rgeo.G);
                     c->normi.ensure(16 * 2 * 64);
                     HIPCHK(hipMemsetAsync(c->nfall.p, 0, 16, c->stream));
+                    // chunk lists of the resident geometry (its chunks differ from the per-window
+                    // select's), double-buffered by window parity
+                    const size_t rcw = std::max<size_t>(1, (size_t)rgeo.K * rgeo.G * rgeo.L);
+                    c->clists.ensure(8 * rcw * 2);
+                    ResShard rsh{1u, 0u, 0ull, nullptr, 0ull, 0ull, 0ull};
+                    if (c->world > 1)
+                        rsh = ResShard{(uint32_t)c->world, (uint32_t)c->rank, seq_run, c->mbox_peers.as<char *>(),
+                                       kMbResHello, kMbResFlags, kMbResLists};
                     // test hook: a selector that never delivers window 3 (one-shot), so the
                     // in-kernel timeout drain runs (tests/test_gpu_recovery.py)
                     const char *inj = getenv("QS_INJECT_FAULT");
@@ -1272,10 +1294,10 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                         HIPCHK(hipMemsetAsync(rdiag, 0, 256, c->stream));
                     }
                     kt.begin(3, c->stream);  // the one launch, under "resolve"
-                    HIPCHK(launch_la_stream_res(c->dt, dp, dx, c->dc, P, rgeo, L0, C0, (uint32_t)lwords, (uint32_t)cwords,
-                                                c->npart.as<uint4>(), c->normi.as<NormInfo>(),
-                                                c->nfall.as<unsigned long long>(), on, ok, st, c->resctl.p, sel, rdiag,
-                                                c->stream));
+                    HIPCHK(launch_la_stream_res(c->dt, dp, dx, c->dc, P, rgeo, L0, c->clists.as<uint64_t>(),
+                                                (uint32_t)lwords, (uint32_t)rcw, c->npart.as<uint4>(),
+                                                c->normi.as<NormInfo>(), c->nfall.as<unsigned long long>(), on, ok,
+                                                st, c->resctl.p, sel, rdiag, rsh, c->stream));
                     kt.end(3, c->stream);
                     c->dc.inject = 0;
                     if (rdiag) {

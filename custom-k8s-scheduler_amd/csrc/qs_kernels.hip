@@ -154,11 +154,13 @@ LaGeom la_stream_res_plan(const LaGeom &geo, uint32_t feat, uint32_t n, uint32_t
     LaGeom r = geo;
     r.G = 0;
     // compact Fit + Balanced (+ extended) profiles, and the normalizing ones (K <= kResNormK)
+    // sharded (geo.W > 1 ranks, one shard each): Fit + Balanced (+ extended) only, W * L <= 512
     const bool fit = feat == 0 || feat == kFeatExt;
     const bool norm = (feat & kFeatNorm) != 0 && (feat & kFeatWide) == 0 && geo.K <= kResNormK;
-    if (!((fit || norm) && geo.W == 1 && geo.nv == 1 && geo.epl == 1 && geo.waves == 4 && geo.L <= 64 && n > 0 &&
-          cus > geo.K))
-        return r;
+    const bool shard_ok = geo.W == 1 ? geo.nv == 1 && geo.epl == 1
+                                     : fit && geo.nv == 1 && geo.K <= 32 && geo.W * geo.L <= (uint32_t)kResBS;
+    if (!((fit || norm) && shard_ok && geo.waves == 4 && geo.L <= 64 && n > 0 && cus > geo.K)) return r;
+    n = (n + geo.W - 1) / geo.W;  // this rank's node range
     const uint32_t gmax = std::min(8u, (cus - 1) / geo.K);
     if (gmax == 0) return r;
     constexpr uint32_t bs = kResBS;  // threads of a selector workgroup
@@ -193,17 +195,17 @@ hipError_t launch_la_stream_res(const DevTable &t, const void *pods, const DPodX
                                 const LaGeom &geo, uint64_t *lists0, uint64_t *clists0, uint32_t lwords,
                                 uint32_t cwords, uint4 *npart, NormInfo *norm, unsigned long long *nfall, int32_t *on,
                                 uint64_t *ok, uint64_t *st, void *ctl, uint32_t sel_blocks, uint64_t *rdiag,
-                                hipStream_t stream) {
+                                const ResShard &rsh, hipStream_t stream) {
     if (t.wrows || geo.G == 0 || (uint64_t)t.n * sizeof(DRow) >= (1ull << 31)) return hipErrorInvalidValue;
     if (c.feat & kFeatNorm)
         return la_stream_res_f<kFeatExt | kFeatTaint | kFeatAffinity>(t, pods, podx, c, P, geo, lists0, clists0, lwords,
                                                                       cwords, npart, norm, nfall, on, ok, st, ctl,
-                                                                      sel_blocks, rdiag, stream);
+                                                                      sel_blocks, rdiag, rsh, stream);
     if (c.feat & kFeatExt)
         return la_stream_res_f<kFeatExt>(t, pods, podx, c, P, geo, lists0, clists0, lwords, cwords, npart, norm, nfall,
-                                         on, ok, st, ctl, sel_blocks, rdiag, stream);
+                                         on, ok, st, ctl, sel_blocks, rdiag, rsh, stream);
     return la_stream_res_f<0>(t, pods, podx, c, P, geo, lists0, clists0, lwords, cwords, npart, norm, nfall, on, ok, st,
-                              ctl, sel_blocks, rdiag, stream);
+                              ctl, sel_blocks, rdiag, rsh, stream);
 }
 
 LaGeom la_geometry(uint32_t n, uint32_t K, uint32_t W, uint32_t L) {

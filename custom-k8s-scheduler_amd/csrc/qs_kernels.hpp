@@ -1625,6 +1625,80 @@ __device__ __forceinline__ void res_publish_list(const uint64_t *lbuf, uint32_t 
     if (threadIdx.x == 0) res_add(rdy);
 }
 
+// Sharded resident stream: the block holding rank `rank`'s shard list of window
+// pod k (lbuf, L keys, node-index order among equal totals) writes it into EVERY rank's mailbox
+// (lists[w % 4][k][rank], system-scope stores over xGMI) and raises flags[w % 4][k][rank] = seq << 32
+// | w + 1 there with a system-scope release after a system fence; then waits (bounded) until all W
+// ranks' flags for pod k have arrived in its own mailbox and reduces the W * L keys, rank-major (so
+// equal totals stay in node-index order), to the pod's top-L in lbuf.  Before its first remote
+// write of a run a block waits for every rank's hello (posted by each rank's resolver block at
+// launch start): a peer still finishing its previous run could otherwise see its slots reused.
+// Slot w % 4 is safe to reuse: a rank writes window w only after resolving window w - 2, which took
+// every rank's lists of window w - 2, produced after those ranks resolved window w - 4, whose
+// cross merges read slot (w - 4) % 4.  Returns false on a timeout (werr raised).
+__device__ __forceinline__ bool res_cross_merge(uint64_t *lbuf, uint32_t L, uint32_t k, uint32_t w,
+                                                const ResShard &rsh, bool &hello_ok, uint32_t &okflag,
+                                                uint32_t *werr) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    const uint32_t W = rsh.W;
+    const uint64_t tag = (rsh.seq << 32) | (uint64_t)(w + 1);
+    const size_t cell = ((size_t)(w & 3) * 32 + k) * 16;  // [slot][pod][rank] index base
+    auto sys_poll = [&](const uint64_t *p, uint64_t want) -> bool {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < want) {
+            __builtin_amdgcn_s_sleep(1);
+            if (load_coh_u32(werr) != 0u) return false;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 50000000ull) {
+                __hip_atomic_store((gu32 *)werr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                return false;
+            }
+        }
+        return true;
+    };
+    const char *own = rsh.peers[rsh.rank];
+    if (!hello_ok) {
+        if (tid == 0) {
+            bool ok = true;
+            for (uint32_t r = 0; r < W && ok; ++r)
+                ok = sys_poll(reinterpret_cast<const uint64_t *>(own + rsh.hello) + r, rsh.seq);
+            okflag = ok ? 1u : 0u;
+        }
+        __syncthreads();
+        if (!okflag) return false;
+        hello_ok = true;
+    }
+    if (tid < 64) {
+        for (uint32_t r = 0; r < W; ++r) {
+            uint64_t *dst = reinterpret_cast<uint64_t *>(rsh.peers[r] + rsh.lists) + (cell + rsh.rank) * 64;
+            if ((uint32_t)lane < L)
+                __hip_atomic_store(dst + lane, lbuf[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        __threadfence_system();
+        if (lane == 0)
+            for (uint32_t r = 0; r < W; ++r)
+                __hip_atomic_store(reinterpret_cast<uint64_t *>(rsh.peers[r] + rsh.flags) + cell + rsh.rank, tag,
+                                   __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (tid == 0) {
+        bool ok = true;
+        for (uint32_t r = 0; r < W && ok; ++r) ok = sys_poll(reinterpret_cast<const uint64_t *>(own + rsh.flags) + cell + r, tag);
+        okflag = ok ? 1u : 0u;
+    }
+    __syncthreads();  // every wave is past its lbuf reads; the flags have been seen
+    if (!okflag) return false;
+    const uint32_t M = W * L;  // <= 512 = one key per thread, rank-major positions
+    const uint32_t pos = (uint32_t)tid;
+    uint64_t e[1];
+    uint32_t te[1];
+    e[0] = pos < M ? __hip_atomic_load(reinterpret_cast<const uint64_t *>(own + rsh.lists) + (cell + pos / L) * 64 + pos % L,
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                   : 0ull;
+    te[0] = (uint32_t)(e[0] >> 32);
+    block_topl<kResBS, 1>(te, L, lbuf, [&](int) { return e[0]; });
+    __syncthreads();  // lbuf complete
+    return true;
+}
+
 // Normalizing profiles (TaintToleration / NodeAffinity): a task first scores everything but the
 // normalized parts and the chunk's partial maxima {mt, ct, ma, ca} over its feasible nodes,
 // publishes the partial (sc1, ticket nticket[w&1][k]), waits until all G chunks of its pod have
@@ -1637,8 +1711,12 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
                                              uint32_t nwin, uint64_t *lists0, uint64_t *clists0, uint32_t lwords,
                                              uint32_t cwords, ResCtl *ctl, uint32_t sid, uint32_t S,
                                              uint64_t *rdiag, const DPodX *__restrict__ podx, uint4 *npart0,
-                                             NormInfo *norm0) {
+                                             NormInfo *norm0, const ResShard &rsh) {
     constexpr bool NORM = (F & kFeatNorm) != 0;
+    // sharded (rsh.W > 1): this rank's node range; the chunks tile it
+    const uint32_t lo = (uint32_t)((uint64_t)rsh.rank * t.n / rsh.W);
+    const uint32_t hi = (uint32_t)((uint64_t)(rsh.rank + 1) * t.n / rsh.W);
+    bool hello_ok = rsh.W == 1;
     // rdiag (QS_RES_DIAG=1): summed s_memrealtime ticks of the selectors' phases, [16] scoring,
     // [17] chunk top-L, [18] publish / merge, [19] tasks, [20] merges
     uint64_t ts0 = 0, ts1 = 0, ts2 = 0, dsc = 0, dtl = 0, dpm = 0, ntask = 0, nmerge = 0;
@@ -1665,7 +1743,7 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
             const uint32_t k = task / G, g = task % G;
             if (rdiag) ts0 = __builtin_amdgcn_s_memrealtime();
             const PodT<F> p = pods[s0 + k];
-            const uint32_t start = g * chunk, end = min(t.n, start + chunk);
+            const uint32_t start = lo + g * chunk, end = min(hi, start + chunk);
             const uint32_t base = start + (uint32_t)w8 * E * kWave + lane;
             uint32_t tv[E];
             NormInfo nf{0, 0, 0, 0};
@@ -1779,9 +1857,18 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
                     store_coh_u64(reinterpret_cast<uint64_t *>(no) + 1, (uint64_t)nf.ma | ((uint64_t)nf.ca << 32));
                 }
             };
+            // lbuf holds this rank's top-L of pod k: publish it (unsharded), or exchange it with
+            // every rank and publish the top-L of the W shard lists (sharded)
+            auto publish = [&]() {
+                if (rsh.W > 1) {
+                    if (!res_cross_merge(lbuf, L, k, w, rsh, hello_ok, okflag, c.werr)) return false;
+                }
+                res_publish_list(lbuf, L, out, &ctl->rdy[b][0]);
+                return true;
+            };
             if (G == 1) {
                 put_norm();
-                res_publish_list(lbuf, L, out, &ctl->rdy[b][0]);
+                if (!publish()) return;
             } else {
                 uint64_t *cl = clists + (size_t)k * G * L;
                 if ((uint32_t)tid < L) store_coh_u64(cl + (size_t)g * L + tid, lbuf[tid]);
@@ -1803,7 +1890,7 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
                     block_topl<kResBS, E2>(te, L, lbuf, [&](int j) { return e[j]; });
                     __syncthreads();
                     put_norm();
-                    res_publish_list(lbuf, L, out, &ctl->rdy[b][0]);
+                    if (!publish()) return;
                     ++nmerge;
                 }
             }
@@ -2324,13 +2411,19 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
             // lost-holder flags for pod j+1 after pod j
             auto rescan_c = [&](uint32_t j) {
                 const uint64_t ks = rescan_pass(j, w & 1);
-                if (ks && j + 1 < kend) {
-                    const uint32_t W = key_node(ks);
-                    const bool slot = __ballot((uint32_t)lane < *snd && sidx[lane] == W) != 0;
-                    if (!slot) {
-                        const int pj = j & 1;
-                        const RowT<F> rw = load_row<F>(t, W);
-                        const RowX xw = load_rowx<F>(t, W);
+                const uint32_t W = ks ? key_node(ks) : 0u;
+                const bool slot = __ballot((uint32_t)lane < *snd && sidx[lane] == W) != 0;
+                if (ks && !slot) {
+                    // the staged row is needed even at the window's last pod (waves A/B apply it
+                    // after the loop); the key and flags only when pod j+1 is in this window
+                    const int pj = j & 1;
+                    const RowT<F> rw = load_row<F>(t, W);
+                    const RowX xw = load_rowx<F>(t, W);
+                    if (lane == 0) {
+                        stage[pj][0] = rw;
+                        stagexN[pj][0] = xw;
+                    }
+                    if (j + 1 < kend) {
                         RowT<F> cr = rw;
                         RowX crx = xw;
                         reserve(cr, crx, wp[j], +1);
@@ -2346,8 +2439,6 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                             if (F & kFeatAffinity) fl |= affinity_raw(crx, q1, qx) == nf.ma ? 2u : 0u;
                         }
                         if (lane == 0) {
-                            stage[pj][0] = rw;
-                            stagexN[pj][0] = xw;
                             keyC[pj][0] = f ? pack_key(tot + 1, W) : 0ull;
                             flagC[pj][0] = fl;
                         }
@@ -2525,12 +2616,17 @@ __global__ __launch_bounds__(kResBS) void k_la_stream_res(DevTable t, const PodT
                                                        uint64_t *__restrict__ out_key,
                                                        uint64_t *__restrict__ stamps, ResCtl *ctl,
                                                        uint64_t *__restrict__ rdiag, const DPodX *__restrict__ podx,
-                                                       uint4 *npart0, NormInfo *norm0, unsigned long long *nfall) {
+                                                       uint4 *npart0, NormInfo *norm0, unsigned long long *nfall,
+                                                       ResShard rsh) {
     if (blockIdx.x != 0) {
         res_selector<E, E2, F>(t, pods, c, P, K, G, L, chunk, nwin, lists0, clists0, lwords, cwords, ctl,
-                               blockIdx.x - 1, gridDim.x - 1, rdiag, podx, npart0, norm0);
+                               blockIdx.x - 1, gridDim.x - 1, rdiag, podx, npart0, norm0, rsh);
         return;
     }
+    if (rsh.W > 1 && threadIdx.x == 0)  // this rank is in its new run: peers may write its mailbox
+        for (uint32_t r = 0; r < rsh.W; ++r)
+            __hip_atomic_store(reinterpret_cast<uint64_t *>(rsh.peers[r] + rsh.hello) + rsh.rank, rsh.seq,
+                               __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     if ((F & kFeatNorm) == 0 && threadIdx.x >= 256) {
         // not a pipeline wave: the same barrier count (1 + per window kend + 3)
@@ -2550,8 +2646,11 @@ static hipError_t la_stream_res_f(const DevTable &t, const void *pods, const DPo
                                   const LaGeom &geo, uint64_t *lists0, uint64_t *clists0, uint32_t lwords,
                                   uint32_t cwords, uint4 *npart0, NormInfo *norm0, unsigned long long *nfall,
                                   int32_t *on, uint64_t *ok, uint64_t *st, void *ctl, uint32_t sel_blocks,
-                                  uint64_t *rdiag, hipStream_t stream) {
+                                  uint64_t *rdiag, const ResShard &rsh, hipStream_t stream) {
     const uint32_t K = geo.K, G = geo.G, L = geo.L, nwin = (P + K - 1) / K;
+    // sharded: Fit + Balanced profiles, W * L <= 512 keys per cross merge, K <= 32 pods per slot
+    if (rsh.W > 1 && ((F & kFeatNorm) || rsh.W * L > (uint32_t)kResBS || K > 32 || rsh.W > 16 || !rsh.peers))
+        return hipErrorInvalidValue;
     const uint32_t E2 = 1;  // a pod's G*L <= 512 chunk keys, one per merging thread
     if (G * L > (uint32_t)kResBS) return hipErrorInvalidValue;
     const size_t lds4 = res_stream_lds_bytes<F>(t.n);
@@ -2566,7 +2665,7 @@ static hipError_t la_stream_res_f(const DevTable &t, const void *pods, const DPo
 #define QS_RESK(EE, EE2, KK)                                                                                          \
     hipLaunchKernelGGL((k_la_stream_res<F, EE, EE2, KK>), grid, dim3(kResBS), lds4, stream, t, pp, c, P, K, G, L,       \
                        geo.chunk, nwin, lists0, clists0, lwords, cwords, on, ok, st, rc, rdiag, podx, npart0, norm0,   \
-                       nfall)
+                       nfall, rsh)
 #define QS_RESE(EE, EE2) \
     else if (geo.E == EE && E2 == EE2) { if (geo.k32) QS_RESK(EE, EE2, true); else QS_RESK(EE, EE2, false); }
     if (false) {

@@ -80,10 +80,22 @@ hipError_t launch_ready_set(uint64_t *ready, uint64_t value, hipStream_t stream)
 // workgroups; ctl = la_stream_res_ctl_bytes() of device memory, zeroed before every launch, and
 // c.werr the timeout word.  lists0 / clists0 / dio: the double-buffered window buffers of the
 // per-window path (lwords / cwords per parity).
-LaGeom la_stream_res_plan(const LaGeom &geo, uint32_t feat, uint32_t n, uint32_t cus);  // G = 0: unsupported
+// G = 0: unsupported.  Sharded contexts (geo.W > 1, Fit + Balanced (+ ext) only) plan their own
+// node range of ceil(n / W) nodes.
+LaGeom la_stream_res_plan(const LaGeom &geo, uint32_t feat, uint32_t n, uint32_t cus);
 size_t la_stream_res_ctl_bytes();
 // Workgroups of that launch guaranteed co-resident on `cus` CUs (occupancy query, one per CU of margin).
 uint32_t la_stream_res_max_blocks(const LaGeom &geo, uint32_t feat, uint32_t n, uint32_t cus);
+// Resident sharded stream: rank `rank` of W selects its node range and exchanges
+// every pod's shard list through the peer-memory mailboxes (peers[r] = rank r's mailbox base as
+// mapped here; hello / flags / lists = byte offsets of the resident regions in every mailbox);
+// seq tags this run's flags.  W = 1: unsharded (peers unused).
+struct ResShard {
+    uint32_t W, rank;
+    uint64_t seq;
+    char *const *peers;
+    uint64_t hello, flags, lists;
+};
 // Normalizing profiles (TaintToleration / NodeAffinity) also pass the pod extension records (podx),
 // npart (2 x K x G uint4 partial maxima), norm (2 x 64 NormInfo) and nfall ({rescans, windows with
 // a rescan}); they need K <= 32 and sel_blocks >= K * G.
@@ -91,7 +103,7 @@ hipError_t launch_la_stream_res(const DevTable &t, const void *pods, const DPodX
                                 const LaGeom &geo, uint64_t *lists0, uint64_t *clists0, uint32_t lwords,
                                 uint32_t cwords, uint4 *npart, NormInfo *norm, unsigned long long *nfall, int32_t *on,
                                 uint64_t *ok, uint64_t *st, void *ctl, uint32_t sel_blocks, uint64_t *rdiag,
-                                hipStream_t stream);
+                                const ResShard &rsh, hipStream_t stream);
 
 hipError_t launch_la_window(const DevTable &t, const void *pods, const DPodX *podx, uint32_t s0,
                             uint32_t P, const DevCfg &c, const LaGeom &geo, const LaBufs &bufs,

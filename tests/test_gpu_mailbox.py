@@ -15,11 +15,12 @@ pytestmark = pytest.mark.gpu
 CFG4 = dict(enable_taint=1, enable_affinity=1)
 
 
-def _rank(rank, world, qin, qout, cfg, config, n, p):
+def _rank(rank, world, qin, qout, cfg, config, n, p, resident="1"):
     import sys
     import os
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [root, os.path.join(root, "custom-k8s-scheduler_amd")]
+    os.environ["QS_RESIDENT"] = resident
     import qsched
 
     try:
@@ -33,18 +34,19 @@ def _rank(rank, world, qin, qout, cfg, config, n, p):
             pl, keys = st.results()
             st.free()
             final = s.read_nodes()
-        qout.put(("r", rank, pl, keys, final, stats["engine_used"]))
+        qout.put(("r", rank, pl, keys, final, stats["engine_used"], stats["resident"]))
     except Exception as e:  # reported to the parent instead of hanging it
         qout.put(("e", rank, repr(e)))
 
 
-def run_world(world, cfg, config, n, p):
+def run_world(world, cfg, config, n, p, resident="1"):
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     qout = ctx.Queue()
     qins = [ctx.Queue() for _ in range(world)]
-    procs = [ctx.Process(target=_rank, args=(r, world, qins[r], qout, cfg, config, n, p)) for r in range(world)]
+    procs = [ctx.Process(target=_rank, args=(r, world, qins[r], qout, cfg, config, n, p, resident))
+             for r in range(world)]
     for pr in procs:
         pr.start()
     handles, results = {}, {}
@@ -67,18 +69,25 @@ def run_world(world, cfg, config, n, p):
     return results
 
 
-@pytest.mark.parametrize("cfg,config,n,p", [({}, 2, 3000, 12000), (CFG4, 4, 2000, 6000)],
-                         ids=["config2", "config4"])
-def test_mailbox_world2_two_processes(oracle, cfg, config, n, p):
+@pytest.mark.parametrize("cfg,config,n,p,resident",
+                         [({}, 2, 3000, 12000, "1"), ({}, 2, 3000, 12000, "0"), ({}, 3, 12000, 20000, "1"),
+                          (CFG4, 4, 2000, 6000, "1")],
+                         ids=["config2-resident", "config2-per-window", "config3-resident", "config4"])
+def test_mailbox_world2_two_processes(oracle, cfg, config, n, p, resident):
+    """Fit + Balanced profiles run the SHARDED RESIDENT stream by default (each
+    rank's selectors score its node range and exchange every pod's shard list through the peers'
+    mailboxes inside the one launch); QS_RESIDENT=0 keeps the per-window mailbox exchange, and the
+    normalizing profile (config 4) always runs per window when sharded."""
     from qsched import pods_from_struct, synth_generate
 
-    res = run_world(2, cfg, config, n, p)
+    res = run_world(2, cfg, config, n, p, resident)
     nodes, pods = synth_generate(config, n, p)
     on = {k: v.copy() for k, v in nodes.items()}
     o_pl, o_keys, _ = oracle.schedule(on, pods_from_struct(pods), cfg, nthreads=16)
     for rank in range(2):
-        pl, keys, final, eng = res[rank]
+        pl, keys, final, eng, res_flag = res[rank]
         assert eng == "lookahead"
+        assert res_flag == (1 if (resident == "1" and not cfg) else 0), rank
         bad = np.nonzero(pl != o_pl)[0]
         assert bad.size == 0, f"rank {rank}: {bad.size} placements differ, first at pod {bad[0]}"
         assert np.array_equal(keys, o_keys), rank

@@ -187,3 +187,19 @@ def test_resident_stream_norm(oracle, monkeypatch, n, p, K):
     w = run_gpu(nodes, pods, CFG4, "lookahead", lookahead=K)
     assert w[3]["resident"] == 0
     assert np.array_equal(w[0], g[0]) and np.array_equal(w[1], g[1])
+
+
+@pytest.mark.parametrize("resident", ["1", "0"])
+@pytest.mark.parametrize("prof", [dict(enable_taint=1), dict(enable_affinity=1)], ids=["taint-only", "affinity-only"])
+def test_single_normalizing_plugin(oracle, monkeypatch, prof, resident):
+    """Only one of TaintToleration / NodeAffinity enabled: the normalizing kernels evaluate both, so
+    the disabled plugin's part of every pod record is neutral (all taints tolerated / no affinity
+    terms) and its weight 0 — placements and keys as the oracle with that plugin off."""
+    monkeypatch.setenv("QS_RESIDENT", resident)
+    nodes, pods = synth_generate(4, 1500, 8000)
+    g = run_gpu(nodes, pods, prof, "lookahead")
+    assert g[3]["resident"] == int(resident)
+    o = run_oracle(oracle, nodes, pods, prof)
+    assert_same(g[:2], o[:2], g[2], o[2])
+    s = run_gpu(nodes, pods, prof, "scan")
+    assert_same(s[:2], o[:2], s[2], o[2])
