@@ -137,6 +137,14 @@ class Ctx:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
+    def min(self, v):
+        if self.dist is None:
+            return v
+        import torch
+        t = torch.tensor([v], dtype=torch.float64, device=self.dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN)
+        return float(t.item())
+
     def shard(self):
         """(rank, world, RCCL unique id) for qs_open_shard; the id is made on rank 0."""
         import torch
@@ -273,32 +281,34 @@ def measure(cx, a, workload, steps, warmup, with_diag=True):
     nodes, pods = qsched.synth_generate(gen, n_nodes, n_pods, seed=seed)
     cfg = dict({"engine": a.engine, "lookahead": a.lookahead}, **PROFILE.get(workload, {}))
     s = open_sched(cx, cfg, sharded)
-    s.load_nodes(nodes)
-    st = s.prepare(pods)  # (may re-lay the table out for the pods' quantities: snapshot after)
-    s.save_table()
+    try:
+        s.load_nodes(nodes)
+        st = s.prepare(pods)  # (may re-lay the table out for the pods' quantities: snapshot after)
+        s.save_table()
 
-    mode = MODE.get(workload, "exact")
+        mode = MODE.get(workload, "exact")
 
-    def step():
-        s.restore_table()
-        return st.run(mode=mode)
+        def step():
+            s.restore_table()
+            return st.run(mode=mode)
 
-    # all ranks enter their first run together: a sharded rank's first window waits (bounded) for
-    # its peers' lists, and a one-sided timeout would void only that rank's run
-    cx.barrier()
-    for _ in range(warmup):
-        step()
-    cx.barrier()
-    t0 = time.perf_counter()
-    last = None
-    for _ in range(steps):
-        last = step()
-    cx.barrier()
-    elapsed = cx.max(time.perf_counter() - t0)
-    placement, keys = st.results()
-    final = s.read_nodes()  # the table after the last timed step (which started from the snapshot)
-    st.free()
-    s.close()
+        # all ranks enter their first run together: a sharded rank's first window waits (bounded)
+        # for its peers' lists, and a one-sided timeout would void only that rank's run
+        cx.barrier()
+        for _ in range(warmup):
+            step()
+        cx.barrier()
+        t0 = time.perf_counter()
+        last = None
+        for _ in range(steps):
+            last = step()
+        cx.barrier()
+        elapsed = cx.max(time.perf_counter() - t0)
+        placement, keys = st.results()
+        final = s.read_nodes()  # the table after the last timed step (which started from the snapshot)
+        st.free()
+    finally:
+        s.close()
     ranks_work = cx.world if (cx.world > 1 and not sharded) else 1  # replicas multiply the work
     value = n_pods * steps * ranks_work / elapsed
     out = {"value": value, "ms_per_step": elapsed / steps * 1e3, "engine": last["engine_used"],
@@ -312,6 +322,36 @@ def measure(cx, a, workload, steps, warmup, with_diag=True):
         out["p50"], out["p99"], out["kp"] = diag_runs(cx, nodes, pods, cfg, sharded)
         out["wall_fallback"] = last["wall_s"]
     return out
+
+
+def measure_sharded(cx, a, workload):
+    """N > 1 config 3: the requested transport (default: the peer-memory mailbox, which runs the
+    sharded RESIDENT stream), falling back to the RCCL all-gather when any rank fails or the ranks'
+    placements disagree.  Every rank takes the same decision (all-reduces of an ok flag and of the
+    placement checksum), so a fallback never leaves ranks out of step."""
+    import zlib
+
+    tried = []
+    order = [a.transport] + (["rccl"] if a.transport != "rccl" else [])
+    for name in order:
+        TRANSPORT["name"] = name
+        m, err = None, None
+        try:
+            m = measure(cx, a, workload, a.steps, a.warmup)
+        except Exception as e:  # a timed-out or failed exchange on this rank
+            err = repr(e)[:300]
+        ok = cx.min(1.0 if m is not None else 0.0) > 0
+        if ok:
+            crc = float(zlib.crc32(np.ascontiguousarray(m["placement"]).tobytes()))
+            ok = cx.min(crc) == cx.max(crc)
+            if not ok:
+                err = "placements differ across ranks"
+        if ok:
+            m["transport"] = name
+            m["transport_tried"] = tried
+            return m
+        tried.append({"transport": name, "error": err or "failed on another rank"})
+    raise SystemExit(f"bench.py: every transport failed: {tried}")
 
 
 def check_stream(m):
@@ -498,7 +538,10 @@ def main():
         return subprocess.run(plan["argv"]).returncode
     cx = Ctx()
     workload = a.workload if a.workload != "auto" else ("config2" if cx.world == 1 else "config3")
-    m = measure(cx, a, workload, a.steps, a.warmup)
+    if cx.world > 1 and workload == "config3":
+        m = measure_sharded(cx, a, workload)
+    else:
+        m = measure(cx, a, workload, a.steps, a.warmup)
     c3 = c4 = c5 = scan = None
     if cx.world == 1 and workload == "config2" and not a.no_config3:
         c3 = measure(cx, a, "config3", 1, 1, with_diag=False)
@@ -514,8 +557,10 @@ def main():
     if cx.rank == 0:
         rl = roofline(m["kp"], m["n_nodes"], m["n_pods"], m["wall_fallback"])
         if m["sharded"]:
-            how = "RCCL all-gather" if TRANSPORT["name"] == "rccl" else "peer-memory mailbox"
-            par, scaling = f"node-sharded x{cx.world} ({how} per window)", "strong"
+            how = ("RCCL all-gather per window" if TRANSPORT["name"] == "rccl" else
+                   "peer-memory mailbox, shard lists exchanged in-launch" if m["launch"] == "resident" else
+                   "peer-memory mailbox per window")
+            par, scaling = f"node-sharded x{cx.world} ({how})", "strong"
         elif cx.world > 1:
             par, scaling = f"replicas x{cx.world}", "weak"
         else:
@@ -536,6 +581,10 @@ def main():
             "roofline": rl,
             "kernels_us_per_step": {k: round(v["s"] * 1e6, 1) for k, v in m["kp"].items()},
         }
+        if m.get("transport"):
+            out["config"]["transport"] = m["transport"]
+            if m["transport_tried"]:
+                out["config"]["transport_fallback_from"] = m["transport_tried"]
         if m["sharded"] or (cx.world == 1 and not a.no_cpu):
             out["check"] = check_stream(m)
         if c3 is not None:

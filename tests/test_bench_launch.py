@@ -92,3 +92,51 @@ def test_world2_gloo_rank_plumbing():
         assert uid == bytes(range(128))  # rank 1 received rank 0's id
         assert top == 1.5                # max over ranks
         assert status == 2               # QS_EDEVICE: no HIP device in this container
+
+
+def _rank_fallback(rank, port, q, mode):
+    """bench.measure_sharded's decision at world 2 (gloo), with measure() stubbed: the mailbox
+    transport fails on one rank only (mode "raise") or gives different placements on the two ranks
+    (mode "differ"); both ranks must then fall back to RCCL together."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE="2",
+                      LOCAL_RANK=str(rank))
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "custom-k8s-scheduler_amd")]
+    import numpy as np
+
+    import bench
+
+    cx = bench.Ctx(backend="gloo")
+    a = bench.parse(["--gpus", "2"])
+
+    def fake_measure(cx_, a_, workload, steps, warmup, with_diag=True):
+        name = bench.TRANSPORT["name"]
+        if name == "mailbox":
+            if mode == "raise" and rank == 1:
+                raise RuntimeError("QS_ETIMEOUT: mailbox exchange timed out")
+            if mode == "differ":
+                return {"placement": np.full(4, rank, np.int32)}
+        return {"placement": np.arange(4, dtype=np.int32)}
+
+    bench.measure = fake_measure
+    m = bench.measure_sharded(cx, a, "config3")
+    cx.dist.destroy_process_group()
+    q.put((rank, m["transport"], [t["transport"] for t in m["transport_tried"]]))
+
+
+@pytest.mark.parametrize("mode", ["raise", "differ"])
+def test_world2_transport_fallback(mode):
+    import torch.multiprocessing as mp
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank_fallback, args=(r, port, q, mode)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert res == [(0, "rccl", ["mailbox"]), (1, "rccl", ["mailbox"])]
