@@ -517,11 +517,26 @@ def framework_leg(cx, n_nodes=5000, n_pods=2000):
     on = {k: v.copy() for k, v in nodes.items()}
     ref, _, _ = O.schedule(on, qsched.pods_from_struct(pods), {"qos_sort": 0}, nthreads=16)
     us = lat * 1e6
-    return {"workload": f"{n_nodes:,} nodes x {n_pods:,} pods, qs_score_pod + qs_reserve per pod "
-                        "(Python ctypes caller, arrival order)",
-            "p50_us": round(float(np.percentile(us, 50)), 2), "p99_us": round(float(np.percentile(us, 99)), 2),
-            "mean_us": round(float(us.mean()), 2), "pods_per_s": round(n_pods / lat.sum(), 1),
-            "placements_match": bool(np.array_equal(placement, ref))}
+    out = {"workload": f"{n_nodes:,} nodes x {n_pods:,} pods, qs_score_pod + qs_reserve per pod, arrival "
+                       "order; p50/p99 from the C++ caller (tools/fw_latency.cpp, every per-node output "
+                       "copied out), python_ctypes = the same loop through the ctypes binding",
+           "python_ctypes": {"p50_us": round(float(np.percentile(us, 50)), 2),
+                             "p99_us": round(float(np.percentile(us, 99)), 2),
+                             "mean_us": round(float(us.mean()), 2), "pods_per_s": round(n_pods / lat.sum(), 1),
+                             "placements_match": bool(np.array_equal(placement, ref))}}
+    import subprocess
+    exe = os.path.join(ROOT, "custom-k8s-scheduler_amd", "fw_latency")
+    for outputs, key in ((1, "native"), (0, "native_best_only")):
+        try:
+            r = subprocess.run([exe, str(n_nodes), str(n_pods), str(outputs)], capture_output=True, text=True,
+                               timeout=120)
+            out[key] = json.loads(r.stdout.strip().splitlines()[-1])
+        except Exception as e:  # reported, not fatal: the ctypes numbers stand
+            out[key] = {"error": repr(e)[:200]}
+    nat = out.get("native", {})
+    for k in ("p50_us", "p99_us", "mean_us", "pods_per_s", "placements_match"):
+        out[k] = nat.get(k, out["python_ctypes"][k])
+    return out
 
 
 def main():

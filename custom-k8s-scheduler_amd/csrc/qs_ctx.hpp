@@ -127,6 +127,11 @@ struct qs_ctx {
     uint64_t device_faults = 0; // QS_EDEVICE results so far (each one drops the device table)
     qs_host::DevBuf diag;
     qs_host::DevBuf scratch, lists, clists, dio, npart, normi, nfall, nrec, bctrl, one_pod, one_podx, out_feas, out_score, out_total;
+    void *pin = nullptr;   // qs_score_pod's packed outputs, written by the kernel (pinned host memory)
+    size_t pin_bytes = 0;
+    uint64_t score_seq = 0;  // the kernel's done word for the call in flight
+    uint32_t pend = 0xFFFFFFFFu;  // a qs_reserve / qs_unreserve row not yet written to the device:
+                                  // the next qs_score_pod writes it, every other call first flushes it
     qs_host::DevBuf hand;  // window hand-off words: {unused, ready, timeout flag} (u64 each)
     bool handoff_off = false;  // a hand-off timed out once: cross-stream events from then on
     qs_host::DevBuf resctl;    // resident stream's hand-off counters

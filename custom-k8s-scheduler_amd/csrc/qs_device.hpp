@@ -354,18 +354,30 @@ __device__ __forceinline__ bool fits(const R &r, const RowX &x, const P &p) {
 __device__ __forceinline__ bool subset128(uint64_t m0, uint64_t m1, uint64_t b0, uint64_t b1) {
     return ((m0 & ~b0) | (m1 & ~b1)) == 0;
 }
+// Every caller evaluates ONE pod per wave (the pod record is wave-uniform), so the pod's term counts
+// and its nodeSelector are read into scalars and the terms a pod does not have are skipped by
+// scalar branches instead of being evaluated under a select (config 4: at most one required and
+// two preferred terms per pod, most pods none).
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
 template <uint32_t F, class R, class P>
 __device__ __forceinline__ bool feasible(const R &r, const RowX &x, const P &p, const DPodX &px) {
     bool ok = fits<F>(r, x, p);
     if (F & kFeatTaint) ok &= (x.th & ~px.tol_hard) == 0;  // UP tainttoleration#Filter
     if (F & kFeatAffinity) {                                 // UP nodeaffinity#Filter
-        ok &= subset128(px.sel0, px.sel1, x.lb0, x.lb1);
-        const uint32_t nt = (p.flags >> 4) & 7u;
-        bool any = nt == 0;
+        const uint64_t s0 = uniform64(px.sel0), s1 = uniform64(px.sel1);
+        if (s0 | s1) ok &= subset128(s0, s1, x.lb0, x.lb1);
+        const uint32_t nt = (uint32_t)__builtin_amdgcn_readfirstlane((int)((p.flags >> 4) & 7u));
+        if (nt != 0) {
+            bool any = false;
 #pragma unroll
-        for (uint32_t k = 0; k < 4; ++k)
-            any |= (k < nt) & subset128(px.req[k][0], px.req[k][1], x.lb0, x.lb1);
-        ok &= any;
+            for (uint32_t k = 0; k < 4; ++k)
+                if (k < nt) any |= subset128(px.req[k][0], px.req[k][1], x.lb0, x.lb1);
+            ok &= any;
+        }
     }
     return ok;
 }
@@ -376,11 +388,11 @@ __device__ __forceinline__ uint32_t taint_raw(const RowX &x, const DPodX &px) {
 // raw NodeAffinity score: weights of matching preferred terms (UP nodeaffinity#Score)
 template <class P>
 __device__ __forceinline__ uint32_t affinity_raw(const RowX &x, const P &p, const DPodX &px) {
-    const uint32_t nt = (p.flags >> 8) & 7u;
+    const uint32_t nt = (uint32_t)__builtin_amdgcn_readfirstlane((int)((p.flags >> 8) & 7u));
     uint32_t s = 0;
 #pragma unroll
     for (uint32_t k = 0; k < 4; ++k)
-        s += ((k < nt) & subset128(px.pref[k][0], px.pref[k][1], x.lb0, x.lb1)) ? (uint32_t)px.pw[k] : 0u;
+        if (k < nt) s += subset128(px.pref[k][0], px.pref[k][1], x.lb0, x.lb1) ? (uint32_t)px.pw[k] : 0u;
     return s;
 }
 

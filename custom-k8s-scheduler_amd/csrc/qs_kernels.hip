@@ -50,27 +50,7 @@ hipError_t launch_batch_claim(const DevTable &t, const void *pods, const uint64_
 // =============================================================================================
 __global__ void k_set_row(DevTable t, uint32_t i, HostRow v, uint32_t feat) {
     (void)feat;
-    t.masks[i] = DMask{v.th, v.ts, v.lb0, v.lb1};
-    if (t.zone) t.zone[i] = v.zone;
-    if (t.wrows) {  // wide layout: memory columns in f64 bytes
-        DRowW w;
-        w.ac = v.ac; w.rc = v.rc; w.zc = v.zc; w.np = v.np;
-        w.am = v.wam; w.rm = v.wrm; w.zm = v.wzm; w.ym = v.ym;
-        w.yc = v.yc; w.mp = v.mp; w.pad = 0;
-        w.ae0 = v.ae0; w.re0 = v.re0; w.ae1 = v.ae1; w.re1 = v.re1;
-        t.wrows[i] = w;
-        return;
-    }
-    DRow r;
-    r.ac = v.ac; r.am = v.am; r.rc = v.rc; r.rm = v.rm; r.zc = v.zc; r.zm = v.zm;
-    r.np = v.np; r.mp = v.mp; r.yc = v.yc; r.ym = v.ym;
-    r.ae0 = v.ae0; r.re0 = v.re0; r.ae1 = v.ae1; r.re1 = v.re1;
-    t.rows[i] = r;
-    if (t.soa.c[0]) {
-        const int32_t f[kSCols] = {v.ac, v.am, v.rc, v.rm, v.zc, v.zm, v.np, v.mp, v.ae0, v.re0, v.ae1, v.re1};
-#pragma unroll
-        for (int k = 0; k < kSCols; ++k) t.soa.c[k][i] = f[k];
-    }
+    set_row(t, i, v);
 }
 
 // =============================================================================================
@@ -122,6 +102,19 @@ hipError_t launch_scan_pod(const DevTable &t, const void *pods, const DPodX *pod
 }
 
 size_t scan_scratch_bytes() { return sizeof(ScanScratch); }
+
+uint32_t score_pod1_max_nodes() { return kScorePod1Max; }
+size_t score_pod1_pack_bytes(uint32_t n) { return score_pack_bytes(n); }
+hipError_t launch_score_pod1(const DevTable &t, const void *pod, const DPodX *podx, const DevCfg &c, uint8_t *hout,
+                             uint64_t seq, uint32_t pidx, const HostRow &prow, hipStream_t stream) {
+    if (t.wrows) return wide_score_pod1(t, pod, podx, c, hout, seq, pidx, prow, stream);
+    switch (feat_class(c.feat)) {
+        case 0: return score_pod1_f<0>(t, pod, podx, c, hout, seq, pidx, prow, stream);
+        case kFeatExt: return score_pod1_f<kFeatExt>(t, pod, podx, c, hout, seq, pidx, prow, stream);
+        default:
+            return score_pod1_f<kFeatExt | kFeatTaint | kFeatAffinity>(t, pod, podx, c, hout, seq, pidx, prow, stream);
+    }
+}
 
 // Window hand-off: publishes window w's lists (ready = run << 32 | w + 1) once the
 // select chain's kernels before it on the stream have finished; the release store orders them.

@@ -17,6 +17,7 @@
 //               which is always inside the top-L lists).  Bit-exact; SURVEY.md §7 H4 option 3.
 #pragma once
 #include <algorithm>
+#include <cstring>
 
 #include "qs_device.hpp"
 #include "qs_launch.hpp"
@@ -293,6 +294,126 @@ __global__ __launch_bounds__(256) void k_scan_commit(DevTable t, const PodT<F> *
     out_node[s] = ks ? (int32_t)key_node(ks) : -1;
     if (out_key) out_key[s] = ks;
     if (stamps) stamps[s] = __builtin_amdgcn_s_memrealtime();
+}
+
+// One node row written from the host mirror (qs_node_upsert / qs_reserve / qs_unreserve; k_set_row
+// and the pending-row write of k_score_pod1): row (compact or wide), masks, zone, SoA copy.
+__device__ __forceinline__ void set_row(const DevTable &t, uint32_t i, const HostRow &v) {
+    t.masks[i] = DMask{v.th, v.ts, v.lb0, v.lb1};
+    if (t.zone) t.zone[i] = v.zone;
+    if (t.wrows) {  // wide layout: memory columns in f64 bytes
+        DRowW w;
+        w.ac = v.ac; w.rc = v.rc; w.zc = v.zc; w.np = v.np;
+        w.am = v.wam; w.rm = v.wrm; w.zm = v.wzm; w.ym = v.ym;
+        w.yc = v.yc; w.mp = v.mp; w.pad = 0;
+        w.ae0 = v.ae0; w.re0 = v.re0; w.ae1 = v.ae1; w.re1 = v.re1;
+        t.wrows[i] = w;
+        return;
+    }
+    DRow r;
+    r.ac = v.ac; r.am = v.am; r.rc = v.rc; r.rm = v.rm; r.zc = v.zc; r.zm = v.zm;
+    r.np = v.np; r.mp = v.mp; r.yc = v.yc; r.ym = v.ym;
+    r.ae0 = v.ae0; r.re0 = v.re0; r.ae1 = v.ae1; r.re1 = v.re1;
+    t.rows[i] = r;
+    if (t.soa.c[0]) {
+        const int32_t f[kSCols] = {v.ac, v.am, v.rc, v.rm, v.zc, v.zm, v.np, v.mp, v.ae0, v.re0, v.ae1, v.re1};
+#pragma unroll
+        for (int k = 0; k < kSCols; ++k) t.soa.c[k][i] = f[k];
+    }
+}
+// The same row as the kernels' register form.
+template <uint32_t F>
+__device__ __forceinline__ void host_row_regs(const HostRow &v, RowT<F> &r, RowX &x) {
+    if constexpr ((F & kFeatWide) != 0) {
+        r.ac = v.ac; r.rc = v.rc; r.zc = v.zc; r.np = v.np; r.mp = v.mp;
+        r.am = v.wam; r.rm = v.wrm; r.zm = v.wzm; r.yc = v.yc; r.ym = v.ym;
+    } else {
+        r.ac = v.ac; r.am = v.am; r.rc = v.rc; r.rm = v.rm; r.zc = v.zc; r.zm = v.zm;
+        r.np = v.np; r.mp = v.mp; r.yc = v.yc; r.ym = v.ym;
+    }
+    x.ae0 = x.re0 = x.ae1 = x.re1 = 0;
+    x.th = x.ts = x.lb0 = x.lb1 = 0;
+    if (F & kFeatExt) { x.ae0 = v.ae0; x.re0 = v.re0; x.ae1 = v.ae1; x.re1 = v.re1; }
+    if (F & (kFeatTaint | kFeatAffinity)) { x.th = v.th; x.ts = v.ts; x.lb0 = v.lb0; x.lb1 = v.lb1; }
+}
+
+// qs_score_pod for tables up to kScorePod1Max nodes (the framework-embedded path, one call per pod,
+// DESIGN.md §4.6): ONE 1024-thread workgroup, the pod record and its extension passed by value (no
+// H2D), the normalize maxima and the keys in the same launch (two passes over the L2-resident rows,
+// separated by a barrier), and every output written straight into pinned host memory (no D2H
+// command): [best key u64 | done u64 | total i32 x n (-1 = infeasible) | plugin scores u8 x 4n];
+// `done` = seq, stored last with a system-scope release after every thread's system fence, is what
+// the host polls.  A pending row (the previous qs_reserve / qs_unreserve, folded into this launch)
+// is written to the table by thread 0 and used from the argument by the thread that scores it.
+constexpr uint32_t kScorePod1Max = 16384;
+__host__ __device__ constexpr size_t score_pack_bytes(uint32_t n) { return 16 + 4 * (size_t)n + 4 * (size_t)n; }
+template <uint32_t F>
+__global__ __launch_bounds__(1024) void k_score_pod1(DevTable t, PodT<F> p, DPodX px, DevCfg c, uint8_t *hout,
+                                                     uint64_t seq, uint32_t pidx, HostRow prow) {
+    constexpr int NW = 1024 / kWave;
+    __shared__ uint32_t red[2][NW];
+    __shared__ uint64_t redk[NW];
+    const uint32_t n = t.n, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    int32_t *total = reinterpret_cast<int32_t *>(hout + 16);
+    uint32_t *score = reinterpret_cast<uint32_t *>(hout + 16 + 4 * (size_t)n);
+    RowT<F> pr;
+    RowX prx;
+    host_row_regs<F>(prow, pr, prx);
+    if (tid == 0 && pidx < n) set_row(t, pidx, prow);
+    auto row_at = [&](uint32_t i, RowT<F> &r, RowX &x) {
+        r = load_row<F>(t, i);
+        x = load_rowx<F>(t, i);
+        if (i == pidx) { r = pr; x = prx; }
+    };
+    uint32_t mt = 0, ma = 0;
+    if constexpr ((F & kFeatNorm) != 0) {  // NormalizeScore maxima over the feasible nodes (spec S5)
+        for (uint32_t i = tid; i < n; i += 1024) {
+            RowT<F> r;
+            RowX x;
+            row_at(i, r, x);
+            if (feasible<F>(r, x, p, px)) {
+                const uint32_t a = taint_raw(x, px), b = affinity_raw(x, p, px);
+                mt = a > mt ? a : mt;
+                ma = b > ma ? b : ma;
+            }
+        }
+        mt = wave_max_u32(mt);
+        ma = wave_max_u32(ma);
+        if (lane == 0) { red[0][wv] = mt; red[1][wv] = ma; }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < NW; ++q) {
+            mt = red[0][q] > mt ? red[0][q] : mt;
+            ma = red[1][q] > ma ? red[1][q] : ma;
+        }
+    }
+    const double ymt = rcp_exact(mt), yma = rcp_exact(ma);
+    uint64_t best = 0;
+    for (uint32_t i = tid; i < n; i += 1024) {
+        RowT<F> r;
+        RowX x;
+        row_at(i, r, x);
+        const bool f = feasible<F>(r, x, p, px);
+        uint32_t sco[4];
+        const uint32_t tot = node_total<F>(r, x, p, px, c, mt, ymt, ma, yma, sco);
+        const uint64_t key = f ? pack_key(tot + 1, i) : 0ull;
+        best = key > best ? key : best;
+        // plugin scores are 0..100: one byte each
+        total[i] = f ? (int32_t)tot : -1;
+        score[i] = f ? (sco[0] | (sco[1] << 8) | (sco[2] << 16) | (sco[3] << 24)) : 0u;
+    }
+    best = wave_max_u64(best);
+    if (lane == 0) redk[wv] = best;
+    __threadfence_system();  // every thread's host-memory stores before the barrier ...
+    __syncthreads();
+    if (tid == 0) {
+#pragma unroll
+        for (int q = 0; q < NW; ++q) best = redk[q] > best ? redk[q] : best;
+        *reinterpret_cast<volatile uint64_t *>(hout) = best;
+        __threadfence_system();
+        // ... and the done word last: the host polls it
+        __hip_atomic_store(reinterpret_cast<uint64_t *>(hout + 8), seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // =============================================================================================
@@ -2978,6 +3099,18 @@ static hipError_t scan_pod_f(const DevTable &t, const void *pods_, const DPodX *
 }
 
 template <uint32_t F>
+static hipError_t score_pod1_f(const DevTable &t, const void *pod, const DPodX *podx, const DevCfg &c, uint8_t *hout,
+                               uint64_t seq, uint32_t pidx, const HostRow &prow, hipStream_t stream) {
+    if (t.n > kScorePod1Max) return hipErrorInvalidValue;
+    PodT<F> p;
+    std::memcpy(&p, pod, sizeof p);
+    DPodX px{};
+    if ((F & kFeatNorm) && podx) px = *podx;
+    hipLaunchKernelGGL((k_score_pod1<F>), dim3(1), dim3(1024), 0, stream, t, p, px, c, hout, seq, pidx, prow);
+    return hipGetLastError();
+}
+
+template <uint32_t F>
 static hipError_t la_window_f(const DevTable &t, const void *pods_, const DPodX *podx, uint32_t s0,
                               uint32_t P, const DevCfg &c, const LaGeom &geo, const LaBufs &bf,
                               int32_t *on, uint64_t *ok, uint64_t *st, uint64_t *diag,
@@ -3102,6 +3235,8 @@ hipError_t wide_la_window(const DevTable &t, const void *pods, const DPodX *podx
                           int32_t *on, uint64_t *ok, uint64_t *st, uint64_t *diag,
                           hipStream_t stream, int part);
 hipError_t wide_batch_claim_prepare();
+hipError_t wide_score_pod1(const DevTable &t, const void *pod, const DPodX *podx, const DevCfg &c, uint8_t *hout,
+                           uint64_t seq, uint32_t pidx, const HostRow &prow, hipStream_t stream);
 hipError_t wide_batch_claim(const DevTable &t, const void *pods, const uint64_t *lists, uint32_t *ctrl,
                             uint32_t *bidx, uint32_t P, uint32_t B, int32_t *on, uint64_t *ok,
                             size_t lds, hipStream_t stream);

@@ -203,12 +203,17 @@ class Scheduler:
         self._chk(self.lib.qs_unreserve(self.ctx, node, _ptr(p)))
 
     # ---- one pod, all nodes ----
-    def score_pod(self, pod):
+    def score_pod(self, pod, outputs=True):
+        """qs_score_pod: {"best"} and, with outputs, the per-node "feasible" / "scores" / "total"
+        arrays (fresh copies).  outputs=False asks the library for the best node only."""
         p = np.array([pod], POD_DTYPE) if isinstance(pod, np.void) else pods_to_struct(pod)[:1]
+        best = ctypes.c_int32(-2)
+        if not outputs:
+            self._chk(self.lib.qs_score_pod(self.ctx, _ptr(p), None, None, None, ctypes.byref(best)))
+            return dict(best=best.value)
         feas = np.zeros(self.n, np.uint8)
         score = np.zeros((self.n, 4), np.int32)
         total = np.zeros(self.n, np.int32)
-        best = ctypes.c_int32(-2)
         self._chk(self.lib.qs_score_pod(self.ctx, _ptr(p), _ptr(feas), _ptr(score), _ptr(total),
                                         ctypes.byref(best)))
         return dict(feasible=feas.astype(bool), scores=score, total=total, best=best.value)

@@ -1,0 +1,90 @@
+// fw_latency.cpp — latency of the framework-embedded path (SURVEY.md §3.4, §5 p99 definition) timed
+// from C++ over the C ABI, as a kube-scheduler plugin calls it once per pod: qs_score_pod
+// (PreFilter..NormalizeScore for every node, per-node feasible / plugin scores / totals copied out)
+// followed by qs_reserve of the chosen node.  Arrival order on a spec/synth.md config-2 cluster;
+// placements diffed against the CPU oracle (test infrastructure: oracle/liboracle.so).
+//
+//   fw_latency [nodes] [pods] [outputs: 1 all arrays, 0 best only]  ->  one JSON line
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "../include/qsched.h"
+extern "C" {
+#include "../oracle/qs_oracle.h"
+}
+
+int main(int argc, char **argv) {
+    const uint32_t n = argc > 1 ? (uint32_t)atoi(argv[1]) : 5000;
+    const uint32_t p = argc > 2 ? (uint32_t)atoi(argv[2]) : 2000;
+    const bool outputs = argc > 3 ? atoi(argv[3]) != 0 : true;
+    std::vector<int64_t> col[10];
+    for (auto &v : col) v.assign(n, 0);
+    std::vector<int64_t> ae(2 * n), re(2 * n);
+    std::vector<uint64_t> th(n), ts(n), lb(2 * n);
+    std::vector<int32_t> zone(n);
+    qs_node_soa_out out{col[0].data(), col[1].data(), ae.data(), col[2].data(), col[3].data(), col[4].data(),
+                        re.data(), col[5].data(), col[6].data(), col[7].data(), th.data(), ts.data(), lb.data(),
+                        zone.data()};
+    std::vector<qs_pod> pods(p);
+    if (qs_synth_generate(2, 0x5EED0002ull, n, p, &out, pods.data()) != QS_OK) return 2;
+    qs_config cfg;
+    qs_config_default(&cfg);
+    qs_ctx *ctx = nullptr;
+    if (qs_open(&cfg, 0, &ctx) != QS_OK) return 3;
+    qs_node_soa in{col[0].data(), col[1].data(), ae.data(), col[2].data(), col[3].data(), col[4].data(),
+                   re.data(), col[5].data(), col[6].data(), col[7].data(), th.data(), ts.data(), lb.data(),
+                   zone.data()};
+    if (qs_nodes_load(ctx, &in, n) != QS_OK) return 4;
+    std::vector<uint8_t> feas(n);
+    std::vector<int32_t> score(4 * (size_t)n), total(n), placement(p);
+    std::vector<double> lat(p);
+    using clk = std::chrono::steady_clock;
+    for (uint32_t j = 0; j < p; ++j) {
+        const auto t0 = clk::now();
+        int32_t best = -2;
+        if (qs_score_pod(ctx, &pods[j], outputs ? feas.data() : nullptr, outputs ? score.data() : nullptr,
+                         outputs ? total.data() : nullptr, &best) != QS_OK) {
+            std::fprintf(stderr, "qs_score_pod: %s\n", qs_last_error(ctx));
+            return 5;
+        }
+        if (best >= 0 && qs_reserve(ctx, (uint32_t)best, &pods[j]) != QS_OK) {
+            std::fprintf(stderr, "qs_reserve: %s\n", qs_last_error(ctx));
+            return 6;
+        }
+        lat[j] = std::chrono::duration<double, std::micro>(clk::now() - t0).count();
+        placement[j] = best;
+    }
+    qs_close(ctx);
+    // oracle, arrival order (qos_sort = 0)
+    std::vector<int64_t> o[10];
+    for (auto &v : o) v.assign(n, 0);
+    std::vector<int64_t> oae(2 * n), ore(2 * n);
+    std::vector<uint64_t> oth(n), ots(n), olb(2 * n);
+    std::vector<int32_t> ozone(n);
+    or_nodes on{n, o[0].data(), o[1].data(), oae.data(), o[2].data(), o[3].data(), o[4].data(), ore.data(),
+                o[5].data(), o[6].data(), o[7].data(), oth.data(), ots.data(), olb.data(), ozone.data()};
+    std::vector<int64_t> prc(p), prm(p), pre(2 * p), pzc(p), pzm(p);
+    std::vector<int32_t> pq(p), ppr(p), pnr(p), pnp(p), ppw(4 * p), papp(p), paa(p);
+    std::vector<uint64_t> pth(p), pts(p), psel(2 * p), prt(8 * p), ppt(8 * p);
+    or_pods op{p, prc.data(), prm.data(), pre.data(), pzc.data(), pzm.data(), pq.data(), ppr.data(), pth.data(),
+               pts.data(), psel.data(), pnr.data(), pnp.data(), prt.data(), ppt.data(), ppw.data(), papp.data(),
+               paa.data()};
+    or_generate(2, 0x5EED0002ull, &on, &op);
+    or_config oc{1, 1, {1, 2, 3}, {1, 1, 1}, 3, 2, 0, 0, 0, 0};
+    std::vector<int32_t> ref(p);
+    or_schedule(&oc, &on, &op, ref.data(), nullptr, nullptr, 16);
+    const bool match = std::equal(ref.begin(), ref.end(), placement.begin());
+    std::vector<double> s = lat;
+    std::sort(s.begin(), s.end());
+    auto pct = [&](double q) { return s[std::min(s.size() - 1, (size_t)(q * (double)(s.size() - 1) + 0.5))]; };
+    double sum = 0;
+    for (double v : lat) sum += v;
+    std::printf("{\"nodes\": %u, \"pods\": %u, \"outputs\": %s, \"p50_us\": %.2f, \"p99_us\": %.2f, \"mean_us\": %.2f, "
+                "\"max_us\": %.2f, \"pods_per_s\": %.1f, \"placements_match\": %s}\n",
+                n, p, outputs ? "\"feasible+scores+totals\"" : "\"best only\"", pct(0.5), pct(0.99), sum / p, s.back(),
+                p / (sum * 1e-6), match ? "true" : "false");
+    return match ? 0 : 1;
+}
