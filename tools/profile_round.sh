@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 rm -rf $OUT; mkdir -p $OUT profiles
 ARGS="--steps 2 --warmup 1 --no-cpu --no-config3"
-PMC_ARGS="--steps 1 --warmup 1 --no-cpu --no-config3 --no-scan --no-extra"
+PMC_ARGS="--steps 1 --warmup 1 --no-cpu --no-config3 --no-extra"  # the scan leg too: k_scan_soa traffic
 # heartbeat for the GPU pool's silence watchdog (counter passes print nothing for minutes)
 ( while sleep 45; do date >> $OUT/heartbeat; done ) &
 HB=$!
