@@ -396,6 +396,29 @@ __device__ __forceinline__ uint32_t affinity_raw(const RowX &x, const P &p, cons
     return s;
 }
 
+// The state-independent part of one (node, pod) evaluation of the normalizing plugins, packed in
+// 32 bits (resident config-4 stream): bit 0 = the taint / nodeSelector /
+// required-term filters pass, bits 1-7 = taint_raw (<= 64), bits 8-31 = affinity_raw.  Node masks
+// and pod records never change during a stream, so it can be computed anywhere ahead of use; the
+// resolver's slot and candidate keys then only add fits / LeastAllocated / BalancedAllocation and
+// the two normalizations.  Same predicates as feasible / taint_raw / affinity_raw, with per-lane
+// term counts (one pod per lane is allowed here).
+__device__ __forceinline__ uint32_t static_raw(uint64_t th, uint64_t ts, uint64_t lb0, uint64_t lb1, uint32_t flags,
+                                               const DPodX &px) {
+    // branch-free (the callers run one pod per lane: per-lane branches cost exec-mask juggling)
+    const uint32_t nr = (flags >> 4) & 7u, np = (flags >> 8) & 7u;
+    uint32_t ok = (uint32_t)((th & ~px.tol_hard) == 0) & (uint32_t)(((px.sel0 | px.sel1) == 0) | subset128(px.sel0, px.sel1, lb0, lb1));
+    uint32_t any = (uint32_t)(nr == 0), ra = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+        any |= (uint32_t)(k < nr) & (uint32_t)subset128(px.req[k][0], px.req[k][1], lb0, lb1);
+        const uint32_t hit = (uint32_t)(k < np) & (uint32_t)subset128(px.pref[k][0], px.pref[k][1], lb0, lb1);
+        ra += (0u - hit) & (uint32_t)px.pw[k];
+    }
+    const uint32_t rt = (uint32_t)__popcll(ts & ~px.tol_soft);
+    return (ok & any) | (rt << 1) | (ra << 8);
+}
+
 // ---- exact small divisions (spec S10) -------------------------------------------------------
 // floor(n / d) for n < 2^32, 1 <= d < 2^29 and n / d <= ~1000, given y = RN_f64(1/d):
 // n*y is within 2^-52 relative of n/d, whose fractional part is 0 or in [1/d, 1 - 1/d]; a 2^-30
@@ -499,6 +522,26 @@ __device__ __forceinline__ uint32_t node_total(const R &r, const RowX &x, const 
     }
     if (sc) { sc[0] = la; sc[1] = ba; sc[2] = tt; sc[3] = na; }
     return total;
+}
+
+// node_total of a normalizing profile with the node's static part given as static_raw (resident
+// stream's waves A/B/C): the same sums in the same order.
+template <uint32_t F, class R, class P>
+__device__ __forceinline__ uint32_t norm_total(const R &r, const P &p, const DevCfg &c, uint32_t st, uint32_t mt,
+                                               double ymt, uint32_t ma, double yma) {
+    uint32_t total = __umul24((uint32_t)p.wfit, la_score(r, p, c)) + __umul24((uint32_t)p.wbal, ba_score(r, p, c));
+    if (F & kFeatTaint) total += __umul24((uint32_t)c.wtt, tt_norm((st >> 1) & 127u, mt, ymt));
+    if (F & kFeatAffinity) total += __umul24((uint32_t)c.wna, na_norm(st >> 8, ma, yma));
+    return total;
+}
+// The resolver's lost-holder flags of an infeasible node (bit 0: its taint raw score is the pod's
+// selection-time maximum, bit 1: its affinity raw score is), from static_raw.
+template <uint32_t F>
+__device__ __forceinline__ uint32_t holder_flags(uint32_t st, uint32_t mt, uint32_t ma) {
+    uint32_t fl = 0;
+    if (F & kFeatTaint) fl |= ((st >> 1) & 127u) == mt ? 1u : 0u;
+    if (F & kFeatAffinity) fl |= (st >> 8) == ma ? 2u : 0u;
+    return fl;
 }
 
 // Normalization facts of one pod at selection time (LOOKAHEAD with TaintToleration /

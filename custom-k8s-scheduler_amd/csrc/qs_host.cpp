@@ -1355,6 +1355,7 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                     // pods' NormInfo; {rescans, windows with a rescan}
                     c->npart.ensure(16 * 2 * (size_t)rgeo.K * rgeo.G);
                     c->normi.ensure(16 * 2 * 64);
+                    c->nstat.ensure(4 * 2 * 128 * (size_t)rgeo.K);  // entry statics of the lists
                     HIPCHK(hipMemsetAsync(c->nfall.p, 0, 16, c->stream));
                     // chunk lists of the resident geometry (its chunks differ from the per-window
                     // select's), double-buffered by window parity
@@ -1382,7 +1383,8 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                     kt.begin(3, c->stream);  // the one launch, under "resolve"
                     HIPCHK(launch_la_stream_res(c->dt, dp, dx, c->dc, P, rgeo, L0, c->clists.as<uint64_t>(),
                                                 (uint32_t)lwords, (uint32_t)rcw, c->npart.as<uint4>(),
-                                                c->normi.as<NormInfo>(), c->nfall.as<unsigned long long>(), on, ok,
+                                                c->normi.as<NormInfo>(), c->nstat.as<uint32_t>(),
+                                                c->nfall.as<unsigned long long>(), on, ok,
                                                 st, c->resctl.p, sel, rdiag, rsh, c->stream));
                     kt.end(3, c->stream);
                     c->dc.inject = 0;
@@ -1401,6 +1403,10 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                             fprintf(stderr, "QS_RES_DIAG busy cycles/step: D %.0f A %.0f B %.0f C %.0f (steps %llu)\n",
                                     h[8] / (double)h[12], h[9] / (double)h[12], h[10] / (double)h[12],
                                     h[11] / (double)h[12], (unsigned long long)h[12]);
+                        if (h[12])
+                            fprintf(stderr, "QS_RES_DIAG step marks: D argmax %.0f | A pub+reads %.0f applied %.0f | C reads %.0f keyC %.0f loads %.0f\n",
+                                    h[26] / (double)h[12], h[21] / (double)h[12], h[22] / (double)h[12],
+                                    h[23] / (double)h[12], h[24] / (double)h[12], h[25] / (double)h[12]);
                     }
                 } else if (use_graph) {
                     std::vector<uint8_t> key;

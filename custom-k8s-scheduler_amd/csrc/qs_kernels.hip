@@ -186,19 +186,19 @@ uint32_t la_stream_res_max_blocks(const LaGeom &geo, uint32_t feat, uint32_t n, 
 
 hipError_t launch_la_stream_res(const DevTable &t, const void *pods, const DPodX *podx, const DevCfg &c, uint32_t P,
                                 const LaGeom &geo, uint64_t *lists0, uint64_t *clists0, uint32_t lwords,
-                                uint32_t cwords, uint4 *npart, NormInfo *norm, unsigned long long *nfall, int32_t *on,
-                                uint64_t *ok, uint64_t *st, void *ctl, uint32_t sel_blocks, uint64_t *rdiag,
+                                uint32_t cwords, uint4 *npart, NormInfo *norm, uint32_t *stat, unsigned long long *nfall,
+                                int32_t *on, uint64_t *ok, uint64_t *st, void *ctl, uint32_t sel_blocks, uint64_t *rdiag,
                                 const ResShard &rsh, hipStream_t stream) {
     if (t.wrows || geo.G == 0 || (uint64_t)t.n * sizeof(DRow) >= (1ull << 31)) return hipErrorInvalidValue;
     if (c.feat & kFeatNorm)
         return la_stream_res_f<kFeatExt | kFeatTaint | kFeatAffinity>(t, pods, podx, c, P, geo, lists0, clists0, lwords,
-                                                                      cwords, npart, norm, nfall, on, ok, st, ctl,
+                                                                      cwords, npart, norm, stat, nfall, on, ok, st, ctl,
                                                                       sel_blocks, rdiag, rsh, stream);
     if (c.feat & kFeatExt)
-        return la_stream_res_f<kFeatExt>(t, pods, podx, c, P, geo, lists0, clists0, lwords, cwords, npart, norm, nfall,
-                                         on, ok, st, ctl, sel_blocks, rdiag, rsh, stream);
-    return la_stream_res_f<0>(t, pods, podx, c, P, geo, lists0, clists0, lwords, cwords, npart, norm, nfall, on, ok, st,
-                              ctl, sel_blocks, rdiag, rsh, stream);
+        return la_stream_res_f<kFeatExt>(t, pods, podx, c, P, geo, lists0, clists0, lwords, cwords, npart, norm, stat,
+                                         nfall, on, ok, st, ctl, sel_blocks, rdiag, rsh, stream);
+    return la_stream_res_f<0>(t, pods, podx, c, P, geo, lists0, clists0, lwords, cwords, npart, norm, stat, nfall, on,
+                              ok, st, ctl, sel_blocks, rdiag, rsh, stream);
 }
 
 LaGeom la_geometry(uint32_t n, uint32_t K, uint32_t W, uint32_t L) {

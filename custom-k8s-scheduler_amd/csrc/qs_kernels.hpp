@@ -1745,6 +1745,35 @@ __device__ __forceinline__ void res_publish_list(const uint64_t *lbuf, uint32_t 
     __syncthreads();
     if (threadIdx.x == 0) res_add(rdy);
 }
+// Normalizing profiles: the same, plus the static parts (static_raw) of the pod's sorted entries
+// against the next two stream pods, sout[0][lane] vs pod s + 1 and sout[1][lane] vs pod s + 2 (the
+// resolver's wave C scores a candidate entry for the next pod, waves A/B a new slot taken from it
+// for the pod after that).  Waves 0 and 1, one pod each; published before the list's signal.
+template <class PodRec>
+__device__ __forceinline__ void res_publish_list_norm(uint64_t *lbuf, uint32_t L, uint64_t *out, uint32_t *rdy,
+                                                      const DevTable &t, const PodRec *__restrict__ pods,
+                                                      const DPodX *__restrict__ podx, uint32_t s, uint32_t P,
+                                                      uint32_t *sout) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (wv == 0) {
+        uint64_t v = (uint32_t)lane < L ? lbuf[lane] : 0ull;
+        v = wave_sort_desc(v, lane);
+        if ((uint32_t)lane < L) store_coh_u64(out + lane, v);
+        lbuf[lane] = v;
+    }
+    __syncthreads();
+    if (wv < 2) {
+        const uint32_t q = min(s + 1 + (uint32_t)wv, P - 1);
+        const uint64_t v = lbuf[lane];
+        const DMask m = t.masks[v ? key_node(v) : 0u];
+        const DPodX px = load_vgpr(podx + q);
+        const uint32_t st = static_raw(m.th, m.ts, m.lb0, m.lb1, pods[q].flags, px);
+        __hip_atomic_store((gu32 *)(sout + wv * 64 + lane), st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    drain_stores();
+    __syncthreads();
+    if (threadIdx.x == 0) res_add(rdy);
+}
 
 // Sharded resident stream: the block holding rank `rank`'s shard list of window
 // pod k (lbuf, L keys, node-index order among equal totals) writes it into EVERY rank's mailbox
@@ -1832,7 +1861,7 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
                                              uint32_t nwin, uint64_t *lists0, uint64_t *clists0, uint32_t lwords,
                                              uint32_t cwords, ResCtl *ctl, uint32_t sid, uint32_t S,
                                              uint64_t *rdiag, const DPodX *__restrict__ podx, uint4 *npart0,
-                                             NormInfo *norm0, const ResShard &rsh) {
+                                             NormInfo *norm0, uint32_t *stat0, const ResShard &rsh) {
     constexpr bool NORM = (F & kFeatNorm) != 0;
     // sharded (rsh.W > 1): this rank's node range; the chunks tile it
     const uint32_t lo = (uint32_t)((uint64_t)rsh.rank * t.n / rsh.W);
@@ -1984,7 +2013,11 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
                 if (rsh.W > 1) {
                     if (!res_cross_merge(lbuf, L, k, w, rsh, hello_ok, okflag, c.werr)) return false;
                 }
-                res_publish_list(lbuf, L, out, &ctl->rdy[b][0]);
+                if constexpr (NORM)
+                    res_publish_list_norm(lbuf, L, out, &ctl->rdy[b][0], t, pods, podx, s0 + k, P,
+                                          stat0 + ((size_t)b * K + k) * 128);
+                else
+                    res_publish_list(lbuf, L, out, &ctl->rdy[b][0]);
                 return true;
             };
             if (G == 1) {
@@ -2054,13 +2087,16 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
 // barrier (B0: the window's NormInfo in LDS before wave A's first keys), four per rescan.  The four
 // extra waves also stage the next window's pod extension records (176 B each) in LDS.
 constexpr uint32_t kResNormK = 32;  // window pods whose NORM records are staged per parity (K <= 32)
+constexpr uint32_t kResTStride = 65;
+constexpr size_t kResLdsMax = 96 * 1024;  // dynamic LDS of the resident launch (gfx950: up to 160 KiB per workgroup)  // slot statics [pod][lane] rows, padded: both access patterns conflict-free
 template <uint32_t F>
 constexpr size_t res_stream_lds_bytes(uint32_t n) {
     size_t b = ((((size_t)n + 31) / 32 + 3) & ~(size_t)3) * 4 + 4 * 2 * 64 * 8 + 2 * 64 * (sizeof(RowT<F>) + sizeof(int4)) +
                2 * sizeof(ResPub) + 3 * 64 * 4 + 64 * (sizeof(RowT<F>) + sizeof(int4)) + 2 * 64 * sizeof(PodT<F>);
     if ((F & kFeatNorm) != 0)
         b += 2 * kResNormK * (sizeof(DPodX) + sizeof(NormInfo) + sizeof(double2)) + 2 * 64 * sizeof(RowX) +
-             64 * sizeof(RowX) + 64 * (sizeof(RowT<F>) + sizeof(RowX)) + 2 * 64 * 4 + 64 * 4 + 16 * 4 + 8 * 8 + 16;
+             64 * sizeof(RowX) + 64 * (sizeof(RowT<F>) + sizeof(RowX)) + 2 * 64 * 4 + 64 * 4 + 16 * 4 + 8 * 8 + 16 +
+             2 * kResNormK * kResTStride * 4 + 2 * 64 * 4 + 2 * kResNormK * 4;
     return b;
 }
 // QS_RES_DIAG_BLOCK build (experiments): per-role busy shader cycles per pod step, barrier exit
@@ -2072,6 +2108,99 @@ constexpr bool kResDiag = false;
 #endif
 #define QS_RSTAMP_BEGIN() if (kResDiag && rdiag) ts_ = diag_stamp();
 #define QS_RSTAMP_END() if (kResDiag && rdiag) busy_ += diag_stamp() - ts_;
+// cycles from the step's start to point k of a role's step (rdiag[21 + k], summed)
+#define QS_RSTAMP_MARK(k) if (kResDiag && rdiag) sub_[k] += diag_stamp() - ts_;
+// NORM: exact rescan of one window pod p at the current state by the resident resolver
+// workgroup's four parked waves (4-7; wave D has staged its slot nodes in sidx / snd and wave A the
+// slot rows in srow / sxr before R1).  Rows of dirty nodes come from the slots, every other row
+// from HBM, where it is current (only slots change during a window).  Returns the pod's packed key
+// (0 = unschedulable); red_k[0..3] hold the four waves' partial keys after R3, which is how the
+// pipeline waves (res_rescan_wait: the same three barriers) read it.  Only the parked waves run it:
+// inlined into the pipeline roles, its row batches pushed their hot loops into scratch.
+template <uint32_t F>
+__device__ __forceinline__ uint64_t res_rescan_pass(const DevTable &t, const PodT<F> &p, const DPodX &pxi,
+                                                    const uint32_t *dirty, const uint32_t *sidx, const RowT<F> *srow,
+                                                    const RowX *sxr, uint32_t *red_m, uint64_t *red_k,
+                                                    const uint32_t *snd, const DevCfg &cv) {
+    __syncthreads();  // R1: slots staged
+    const int lane = threadIdx.x & 63;
+    const uint32_t wid = (threadIdx.x >> 6) - 4;
+    const uint32_t n = t.n, nds = *snd;
+    constexpr uint32_t U = 4;
+    auto rows_at = [&](uint32_t b0, RowT<F>(&r)[U], RowX(&x)[U]) {
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            const uint32_t idx = b0 + 64 * u < n ? b0 + 64 * u : 0u;
+            r[u] = load_row<F>(t, idx);
+            x[u] = load_rowx<F>(t, idx);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            const uint32_t idx = b0 + 64 * u;
+            if (idx < n && ((dirty[idx >> 5] >> (idx & 31)) & 1u)) {
+                uint32_t j = 0;
+                while (j + 1 < nds && sidx[j] != idx) ++j;  // dirty <=> held by a slot
+                r[u] = srow[j];
+                x[u] = sxr[j];
+            }
+        }
+    };
+    uint32_t mt = 0, ma = 0;
+    for (uint32_t b0 = wid * 64 * U + lane; b0 < n; b0 += 4 * 64 * U) {
+        RowT<F> r[U];
+        RowX x[U];
+        rows_at(b0, r, x);
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            if (b0 + 64 * u < n && feasible<F>(r[u], x[u], p, pxi)) {
+                const uint32_t a = (F & kFeatTaint) ? taint_raw(x[u], pxi) : 0u;
+                const uint32_t b2 = (F & kFeatAffinity) ? affinity_raw(x[u], p, pxi) : 0u;
+                mt = a > mt ? a : mt;
+                ma = b2 > ma ? b2 : ma;
+            }
+        }
+    }
+    mt = wave_max_u32(mt);
+    ma = wave_max_u32(ma);
+    if (lane == 0) { red_m[2 * wid] = mt; red_m[2 * wid + 1] = ma; }
+    __syncthreads();  // R2
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) {
+        mt = red_m[2 * q] > mt ? red_m[2 * q] : mt;
+        ma = red_m[2 * q + 1] > ma ? red_m[2 * q + 1] : ma;
+    }
+    const double ymt = rcp_exact(mt), yma = rcp_exact(ma);
+    uint64_t best = 0;
+    for (uint32_t b0 = wid * 64 * U + lane; b0 < n; b0 += 4 * 64 * U) {
+        RowT<F> r[U];
+        RowX x[U];
+        rows_at(b0, r, x);
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            const uint32_t idx = b0 + 64 * u;
+            const uint32_t tv = node_total<F>(r[u], x[u], p, pxi, cv, mt, ymt, ma, yma, nullptr);
+            const uint64_t key = (idx < n && feasible<F>(r[u], x[u], p, pxi)) ? pack_key(tv + 1, idx) : 0ull;
+            best = key > best ? key : best;
+        }
+    }
+    uint64_t ks = wave_max_u64(best);
+    if (lane == 0) red_k[wid] = ks;
+    __syncthreads();  // R3
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) ks = red_k[q] > ks ? red_k[q] : ks;
+    return ks;
+}
+// The pipeline waves' side of a rescan: R1, R2, R3, then the parked waves' key.
+__device__ __forceinline__ uint64_t res_rescan_wait(const uint64_t *red_k) {
+    __syncthreads();  // R1
+    __syncthreads();  // R2
+    __syncthreads();  // R3
+    uint64_t ks = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) ks = red_k[q] > ks ? red_k[q] : ks;
+    return ks;
+}
+
 template <uint32_t F, bool K32>
 __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable &t, const PodT<F> *__restrict__ pods,
                                                    const DevCfg &c, uint32_t P, uint32_t K, uint32_t nwin,
@@ -2079,7 +2208,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                                                    int32_t *__restrict__ out_node, uint64_t *__restrict__ out_key,
                                                    uint64_t *__restrict__ stamps, ResCtl *ctl, uint64_t *rdiag,
                                                    const DPodX *__restrict__ podx, const NormInfo *norm0,
-                                                   unsigned long long *nfall) {
+                                                   const uint32_t *stat0, unsigned long long *nfall) {
     constexpr bool NORM = (F & kFeatNorm) != 0;
     static_assert((F & kFeatWide) == 0, "compact layout");
     const int lane = threadIdx.x & 63;
@@ -2112,7 +2241,15 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
     uint32_t *sidx = (uint32_t *)base; base += 64 * 4;                // rescan: slot lane -> node
     uint32_t *red_m = (uint32_t *)base; base += 16 * 4;
     uint64_t *red_k = (uint64_t *)base; base += 8 * 8;
-    uint32_t *snd = (uint32_t *)base;                                  // rescan: slot count
+    uint32_t *snd = (uint32_t *)base; base += 16;                      // rescan: slot count
+    // slot statics (static_raw) by [window pod][slot lane]: this window's, and the next window's
+    // for the slots alive now (rank-compacted into Tcur at the boundary); stS: the statics of wave
+    // C's staged candidates against the pod two later (a new slot's first key in waves A/B);
+    // nflag2: the next window's pod flags
+    uint32_t *Tcur = (uint32_t *)base; base += kResNormK * kResTStride * 4;
+    uint32_t *Tnext = (uint32_t *)base; base += kResNormK * kResTStride * 4;
+    uint32_t(*stS)[64] = (uint32_t(*)[64])base; base += 2 * 64 * 4;
+    uint32_t(*nflag2)[kResNormK] = (uint32_t(*)[kResNormK])base;
     const ResPub none{0, 0xFFFFFFFFu, -1, -1, 0, {0, 0}};
     const DPodX px{};
     // the LeastAllocated weights and weight-sum reciprocals held in VGPRs: the score's per-lane
@@ -2120,7 +2257,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
     // select needed a v_mov first, on every wave's critical path)
     DevCfg cv = c;
     asm volatile("" : "+v"(cv.yd_both), "+v"(cv.yd_c), "+v"(cv.yd_m), "+v"(cv.wc), "+v"(cv.wm));
-    uint64_t ts_ = 0, busy_ = 0, steps_ = 0;
+    uint64_t ts_ = 0, busy_ = 0, steps_ = 0, sub_[3] = {0, 0, 0};
 
     for (uint32_t i = threadIdx.x; i < nwords; i += 256) dirty[i] = 0;
     if (threadIdx.x < min(K, P)) wpods2[0][threadIdx.x] = pods[threadIdx.x];
@@ -2132,80 +2269,10 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
     }
     __syncthreads();
 
-    // NORM: exact rescan of window pod i at the current state by all eight waves (wave D has staged
-    // its slot nodes in sidx / snd and wave A the slot rows in srow / sxr before the call).  Rows of
-    // dirty nodes come from the slots, every other row from HBM, where it is current (only slots
-    // change during a window).  Returns the pod's packed key (0 = unschedulable), the same in every
-    // wave.  Three barriers.
+    // NORM: exact rescan of window pod i by the parked waves (res_rescan_pass); the pipeline waves
+    // keep the barrier count (res_rescan_wait) and read its key
     auto rescan_pass = [&](uint32_t i, uint32_t wb) -> uint64_t {
-        __syncthreads();  // R1: slots staged
-        const uint32_t n = t.n, nds = *snd;
-        const PodT<F> p = wpods2[wb][i];
-        const DPodX pxi = wpodx2[wb][i];
-        constexpr uint32_t U = 4;
-        auto rows_at = [&](uint32_t b0, RowT<F>(&r)[U], RowX(&x)[U]) {
-#pragma unroll
-            for (uint32_t u = 0; u < U; ++u) {
-                const uint32_t idx = b0 + 64 * u < n ? b0 + 64 * u : 0u;
-                r[u] = load_row<F>(t, idx);
-                x[u] = load_rowx<F>(t, idx);
-            }
-#pragma unroll
-            for (uint32_t u = 0; u < U; ++u) {
-                const uint32_t idx = b0 + 64 * u;
-                if (idx < n && ((dirty[idx >> 5] >> (idx & 31)) & 1u)) {
-                    uint32_t j = 0;
-                    while (j + 1 < nds && sidx[j] != idx) ++j;  // dirty <=> held by a slot
-                    r[u] = srow[j];
-                    x[u] = sxr[j];
-                }
-            }
-        };
-        const uint32_t wid = (uint32_t)wv;
-        uint32_t mt = 0, ma = 0;
-        for (uint32_t b0 = wid * 64 * U + lane; b0 < n; b0 += 8 * 64 * U) {
-            RowT<F> r[U];
-            RowX x[U];
-            rows_at(b0, r, x);
-#pragma unroll
-            for (uint32_t u = 0; u < U; ++u) {
-                if (b0 + 64 * u < n && feasible<F>(r[u], x[u], p, pxi)) {
-                    const uint32_t a = (F & kFeatTaint) ? taint_raw(x[u], pxi) : 0u;
-                    const uint32_t b2 = (F & kFeatAffinity) ? affinity_raw(x[u], p, pxi) : 0u;
-                    mt = a > mt ? a : mt;
-                    ma = b2 > ma ? b2 : ma;
-                }
-            }
-        }
-        mt = wave_max_u32(mt);
-        ma = wave_max_u32(ma);
-        if (lane == 0) { red_m[2 * wid] = mt; red_m[2 * wid + 1] = ma; }
-        __syncthreads();  // R2
-#pragma unroll
-        for (uint32_t q = 0; q < 8; ++q) {
-            mt = red_m[2 * q] > mt ? red_m[2 * q] : mt;
-            ma = red_m[2 * q + 1] > ma ? red_m[2 * q + 1] : ma;
-        }
-        const double ymt = rcp_exact(mt), yma = rcp_exact(ma);
-        uint64_t best = 0;
-        for (uint32_t b0 = wid * 64 * U + lane; b0 < n; b0 += 8 * 64 * U) {
-            RowT<F> r[U];
-            RowX x[U];
-            rows_at(b0, r, x);
-#pragma unroll
-            for (uint32_t u = 0; u < U; ++u) {
-                const uint32_t idx = b0 + 64 * u;
-                const uint32_t tv = node_total<F>(r[u], x[u], p, pxi, cv, mt, ymt, ma, yma, nullptr);
-                const uint64_t key = (idx < n && feasible<F>(r[u], x[u], p, pxi)) ? pack_key(tv + 1, idx) : 0ull;
-                best = key > best ? key : best;
-            }
-        }
-        uint64_t ks = wave_max_u64(best);
-        if (lane == 0) red_k[wid] = ks;
-        __syncthreads();  // R3
-#pragma unroll
-        for (uint32_t q = 0; q < 8; ++q) ks = red_k[q] > ks ? red_k[q] : ks;
-        return ks;
+        return res_rescan_pass<F>(t, wpods2[wb][i], wpodx2[wb][i], dirty, sidx, srow, sxr, red_m, red_k, snd, cv);
     };
 
     if (wv == 0) {
@@ -2297,6 +2364,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                         if (stamps) res_stamp = __builtin_amdgcn_s_memrealtime();
                     }
                 }
+                QS_RSTAMP_MARK(0)
                 QS_RSTAMP_END()
                 __syncthreads();
                 if (NORM && unsafe) {
@@ -2304,7 +2372,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                     // slot takes source lane 0, whose staged row / key / flags wave C rewrites
                     if ((uint32_t)lane < nd) sidx[lane] = didx;
                     if (lane == 0) *snd = nd;
-                    const uint64_t ks = rescan_pass(i, w & 1);
+                    const uint64_t ks = res_rescan_wait(red_k);
                     ResPub np{ks, ks ? key_node(ks) : 0xFFFFFFFFu, -1, -1, nd, {0, 0}};
                     if (ks) {
                         const uint64_t own = __ballot((uint32_t)lane < nd && didx == np.w);
@@ -2375,28 +2443,30 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
         uint32_t nd = 0;
         uint32_t pend = 0;  // wave A: windows whose rows are stored but not yet signalled (done value)
         const __amdgpu_buffer_rsrc_t rs = row_rsrc(t);
-        // NORM: pod k's extension record, maxima and reciprocals (LDS, read one step ahead)
+        // NORM: pod k's maxima and reciprocals (LDS, read one step ahead)
         struct PodN {
-            DPodX x;
             NormInfo nf;
             double2 yr;
         };
-        auto slot_key = [&](const RowT<F> &r, const RowX &x, const PodT<F> &q, const PodN &pn) -> uint64_t {
+        // NORM: st = the slot's static_raw against pod q (Tcur, or stS for a slot created this step)
+        auto slot_key = [&](const RowT<F> &r, const RowX &x, const PodT<F> &q, const PodN &pn, uint32_t st) -> uint64_t {
             const bool act = (uint32_t)lane < nd;
+#ifdef QS_EXP_PLAIN_AB
+            if (false) {
+#else
             if constexpr (NORM) {
-                const bool f = feasible<F>(r, x, q, pn.x);
-                const uint32_t tot = node_total<F>(r, x, q, pn.x, cv, pn.nf.mt, pn.yr.x, pn.nf.ma, pn.yr.y, nullptr);
+#endif
+                const bool f = fits<F>(r, x, q) && (st & 1u) != 0u;
+                const uint32_t tot = norm_total<F>(r, q, cv, st, pn.nf.mt, pn.yr.x, pn.nf.ma, pn.yr.y);
                 uint32_t fl = 0;
-                if (act && !f) {
-                    if (F & kFeatTaint) fl |= taint_raw(x, pn.x) == pn.nf.mt ? 1u : 0u;
-                    if (F & kFeatAffinity) fl |= affinity_raw(x, q, pn.x) == pn.nf.ma ? 2u : 0u;
-                }
+                if (act && !f) fl = holder_flags<F>(st, pn.nf.mt, pn.nf.ma);
                 return ((act && f) ? ((uint64_t)(tot + 1) << 32) : 0ull) | fl;
             }
             const bool f = feasible<F>(r, x, q, px);
             const uint32_t tot = node_total<F>(r, x, q, px, cv, 0, 0.0, 0, 0.0, nullptr);
             return (act && f) ? ((uint64_t)(tot + 1) << 32) : 0ull;
         };
+        uint32_t snew = 0;  // NORM: the static of a slot created by the applied winner
         auto apply = [&](const ResPub &pv, int pp, const PodT<F> &pprev) {
             if (pv.ks == 0) return;
             if (pv.slot >= 0) {
@@ -2406,6 +2476,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                     S = stage[pp][pv.src];
                     if constexpr (NORM) {
                         SX = stagexN[pp][pv.src];
+                        snew = stS[pp][pv.src];
                     } else if (F & kFeatExt) {
                         const int4 e = stagex[pp][pv.src];
                         SX.ae0 = e.x; SX.re0 = e.y; SX.ae1 = e.z; SX.re1 = e.w;
@@ -2418,7 +2489,9 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
         // NORM: D stopped at window pod j: stage the slot rows (wave A), rescan with every wave
         auto rescan_ab = [&](uint32_t j, uint32_t wb) {
             if (wv == 1 && (uint32_t)lane < nd) { srow[lane] = S; sxr[lane] = SX; }
-            (void)rescan_pass(j, wb);
+            (void)res_rescan_wait(red_k);
+            (void)j;
+            (void)wb;
             __syncthreads();  // R5
         };
         for (uint32_t w = 0; w < nwin; ++w) {
@@ -2427,11 +2500,12 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
             auto podn = [&](uint32_t k) -> PodN {
                 PodN r{};
                 if constexpr (NORM)
-                    if (k < kend) r = PodN{wpodx2[w & 1][k], wnorm2[w & 1][k], wrcp2[w & 1][k]};
+                    if (k < kend) r = PodN{wnorm2[w & 1][k], wrcp2[w & 1][k]};
                 return r;
             };
             if (NORM) __syncthreads();  // B0 (the window's NormInfo is in LDS)
-            if (wv == 1 && nd > 0) keyA[1][lane] = slot_key(S, SX, wp[0], podn(0));  // pod 0, inherited slots
+            if (wv == 1 && nd > 0)  // pod 0, inherited slots
+                keyA[1][lane] = slot_key(S, SX, wp[0], podn(0), NORM ? Tcur[lane] : 0u);
             __syncthreads();  // B1
             const uint32_t isig = min(2u, kend - 1);
             PodT<F> pprev = wp[0], pcur = wp[0];  // pods i-1 and i (pod i+1's record is read each step)
@@ -2441,12 +2515,18 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                 const int par = i & 1, pp = par ^ 1;
                 ResPub pv = read_pub(&pub[pp]);
                 const PodT<F> pn1 = wp[i + 1];
-                __builtin_amdgcn_sched_barrier(0);  // both LDS reads go out before the pub's wait
+                const uint32_t tst = NORM ? Tcur[min(i + 1, kResNormK - 1) * kResTStride + lane] : 0u;
+                PodN pnn{};
+                if (NORM) pnn = podn(i + 2);  // next step's maxima: read with this step's LDS reads
+                __builtin_amdgcn_sched_barrier(0);  // the LDS reads go out before the pub's wait
                 if (NORM && i > 0 && pv.slot == -2) {  // D stopped at pod i-1
                     rescan_ab(i - 1, w & 1);
                     pv = read_pub(&pub[pp]);
                 }
+                const uint32_t nd0 = nd;
+                QS_RSTAMP_MARK(0)
                 if (i > 0) apply(pv, pp, pprev);
+                QS_RSTAMP_MARK(1)
                 if (wv == 1 && pend && i == isig) {
                     // the previous window's rows went out write-through a window boundary ago
                     drain_stores();
@@ -2455,11 +2535,14 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                 }
                 if (i + 1 < kend) {
                     const PodN pnc = pnx;
-                    if (NORM) pnx = podn(i + 2);  // next step's record: its LDS reads overlap this score
+                    pnx = pnn;
                     RowT<F> s2 = S;
                     RowX x2s = SX;
                     if (wv == 2) reserve(s2, x2s, pcur, +1);
-                    (wv == 1 ? keyA : keyB)[par][lane] = slot_key(s2, x2s, pn1, pnc);
+                    // a slot created by pod i-1's winner has no Tcur entry yet: its static came with
+                    // the candidate wave C staged
+                    const uint32_t st = (nd != nd0 && (uint32_t)lane == nd0) ? snew : tst;
+                    (wv == 1 ? keyA : keyB)[par][lane] = slot_key(s2, x2s, pn1, pnc, st);
                 }
                 pprev = pcur;
                 pcur = pn1;
@@ -2500,6 +2583,10 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
     } else if (wv == 3) {
         // ---- C: candidate rows, C keys, the next pod's best clean entry; next-window prefetch -----
         uint64_t eX = 0, eY = 0, c1 = 0;
+        // NORM: the statics of pod i's entries (this lane's) against pods i+1 and i+2, published by
+        // the selectors with the lists; two register pairs by pod parity, each loaded two pods ahead
+        // in place (a pair is reloaded right after its pod's step used it)
+        uint32_t sA1 = 0, sA2 = 0, sB1 = 0, sB2 = 0;
         RowT<F> r1 = empty_row<F>();
         RowX x1{};
         bool pref = false;  // window w's first entries and first candidate rows already loaded
@@ -2519,52 +2606,32 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
         for (uint32_t w = 0; w < nwin; ++w) {
             const uint32_t s0 = w * K, kend = min(K, P - s0);
             const uint64_t *lists = lists0 + (size_t)(w & 1) * lwords;
+            const uint32_t *stats = NORM ? stat0 + (size_t)(w & 1) * K * 128 : nullptr;
             const PodT<F> *wp = wpods2[w & 1];
             const bool hasnext = w + 1 < nwin;
             const uint32_t knext = hasnext ? min(K, P - s0 - K) : 0u;
             const uint64_t *listsn = lists0 + (size_t)((w + 1) & 1) * lwords;
+            const uint32_t *statsn = NORM ? stat0 + (size_t)((w + 1) & 1) * K * 128 : nullptr;
             const uint32_t tnext = ((w + 1) >> 1) * K + knext;
+            // an entry, loaded unconditionally from a clamped pod (a load under a branch made the
+            // compiler wait for every load in flight at the next join); an entry of a pod beyond the
+            // window is never consumed: every use is guarded by that pod's index
             auto ent = [&](const uint64_t *l, uint32_t pod, uint32_t kk) -> uint64_t {
-                return pod < kk ? load_coh_u64(l + (size_t)pod * 64 + lane) : 0ull;
+                return load_coh_u64(l + (size_t)min(pod, kk - 1) * 64 + lane);
             };
-            // NORM: D stopped at window pod j: rescan with every wave, then (a new slot) pod j's
-            // winner as source lane 0 of step j's staging: its row before pod j, and its key and
-            // lost-holder flags for pod j+1 after pod j
-            auto rescan_c = [&](uint32_t j) {
-                const uint64_t ks = rescan_pass(j, w & 1);
-                const uint32_t W = ks ? key_node(ks) : 0u;
-                const bool slot = __ballot((uint32_t)lane < *snd && sidx[lane] == W) != 0;
-                if (ks && !slot) {
-                    // the staged row is needed even at the window's last pod (waves A/B apply it
-                    // after the loop); the key and flags only when pod j+1 is in this window
-                    const int pj = j & 1;
-                    const RowT<F> rw = load_row<F>(t, W);
-                    const RowX xw = load_rowx<F>(t, W);
-                    if (lane == 0) {
-                        stage[pj][0] = rw;
-                        stagexN[pj][0] = xw;
-                    }
-                    if (j + 1 < kend) {
-                        RowT<F> cr = rw;
-                        RowX crx = xw;
-                        reserve(cr, crx, wp[j], +1);
-                        const PodT<F> q1 = wp[j + 1];
-                        const DPodX qx = wpodx2[w & 1][j + 1];
-                        const NormInfo nf = wnorm2[w & 1][j + 1];
-                        const double2 yr = wrcp2[w & 1][j + 1];
-                        const bool f = feasible<F>(cr, crx, q1, qx);
-                        const uint32_t tot = node_total<F>(cr, crx, q1, qx, cv, nf.mt, yr.x, nf.ma, yr.y, nullptr);
-                        uint32_t fl = 0;
-                        if (!f) {
-                            if (F & kFeatTaint) fl |= taint_raw(crx, qx) == nf.mt ? 1u : 0u;
-                            if (F & kFeatAffinity) fl |= affinity_raw(crx, q1, qx) == nf.ma ? 2u : 0u;
-                        }
-                        if (lane == 0) {
-                            keyC[pj][0] = f ? pack_key(tot + 1, W) : 0ull;
-                            flagC[pj][0] = fl;
-                        }
-                    }
+            // NORM: the statics of pod `pod`'s entries (this lane's) into a register pair
+            auto stat_load = [&](uint32_t &d1, uint32_t &d2, const uint32_t *sl, uint32_t pod, uint32_t kk) {
+                if constexpr (NORM) {
+                    const uint32_t *q = sl + (size_t)min(pod, kk - 1) * 128 + lane;
+                    d1 = load_coh_u32(q);
+                    d2 = load_coh_u32(q + 64);
                 }
+            };
+            // NORM: D stopped at window pod j: the parked waves rescan it (and stage a new slot's
+            // row, static, key and flags as source lane 0 of step j); C keeps the barrier count
+            auto rescan_c = [&](uint32_t j) {
+                (void)res_rescan_wait(red_k);
+                (void)j;
                 __syncthreads();  // R5
             };
             uint64_t e0;
@@ -2577,6 +2644,8 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                 e0 = ent(lists, 0, kend);
                 eX = ent(lists, 1, kend);
                 eY = ent(lists, 2, kend);
+                stat_load(sA1, sA2, stats, 0, kend);
+                stat_load(sB1, sB2, stats, 1, kend);
                 if constexpr (NORM) {
                     if ((uint32_t)lane < kend) {
                         const uint64_t *nq = reinterpret_cast<const uint64_t *>(norm0 + (size_t)(w & 1) * 64 + lane);
@@ -2596,7 +2665,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
             const bool pfw = hasnext && kend >= 6;  // prefetch the next window during this one
             PodT<F> pcur = wp[0];  // pod i's record (pod i+1's is read each step)
             // HOOK: the step may carry the next-window prefetch (only the last steps of a window)
-            auto step = [&](auto hook, uint32_t i, uint64_t &en) {
+            auto step = [&](auto hook, uint32_t i, uint64_t &en, uint32_t &c1s1, uint32_t &c1s2) {
                 QS_RSTAMP_BEGIN()
                 const int par = i & 1;
                 // the step's LDS reads first, together: the dirty word of pod i+1's entry (the set
@@ -2607,35 +2676,42 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                 uint32_t dword = dirty[en_node >> 5];
                 const PodT<F> pn1 = wp[i + 1];
                 const uint32_t kn = min(i + 1, kend - 1);
-                DPodX qx{};
                 NormInfo nf{0, 0, 0, 0};
                 double2 yr = make_double2(0.0, 0.0);
                 int32_t stop = 0;
                 if constexpr (NORM) {
-                    qx = wpodx2[w & 1][kn];
                     nf = wnorm2[w & 1][kn];
                     yr = wrcp2[w & 1][kn];
                     stop = pub[par ^ 1].slot;  // NORM only: a STOP of pod i-1 is read here
                 }
-                __builtin_amdgcn_sched_barrier(0);  // both LDS reads go out before their waits
+                __builtin_amdgcn_sched_barrier(0);  // the LDS reads go out before their waits
                 if (NORM && i > 0 && stop == -2) {
                     rescan_c(i - 1);
                     dword = dirty[en_node >> 5];  // pod i-1's rescanned winner is dirty now
                 }
+                QS_RSTAMP_MARK(0)
                 // keyC's score (candidate c1's row + pod i, scored for pod i+1) needs no pub
                 RowT<F> cr = r1;
                 RowX crx = x1;
                 reserve(cr, crx, pcur, +1);
-                const bool f = feasible<F>(cr, crx, pn1, NORM ? qx : px);
-                const uint32_t tot = node_total<F>(cr, crx, pn1, NORM ? qx : px, cv, nf.mt, yr.x, nf.ma, yr.y, nullptr);
-                uint32_t fl = 0;
-                if (NORM && !f) {
-                    if (F & kFeatTaint) fl |= taint_raw(crx, qx) == nf.mt ? 1u : 0u;
-                    if (F & kFeatAffinity) fl |= affinity_raw(crx, pn1, qx) == nf.ma ? 2u : 0u;
+                bool f;
+                uint32_t tot, fl = 0;
+                if constexpr (NORM) {  // the candidate's static against pod i+1 came with its entry
+                    f = fits<F>(cr, crx, pn1) && (c1s1 & 1u) != 0u;
+                    tot = norm_total<F>(cr, pn1, cv, c1s1, nf.mt, yr.x, nf.ma, yr.y);
+                    if (!f) fl = holder_flags<F>(c1s1, nf.mt, nf.ma);
+                } else {
+                    f = feasible<F>(cr, crx, pn1, px);
+                    tot = node_total<F>(cr, crx, pn1, px, cv, 0, 0.0, 0, 0.0, nullptr);
                 }
+                QS_RSTAMP_MARK(1)
                 stage[par][lane] = r1;
-                if constexpr (NORM) stagexN[par][lane] = x1;
-                else if (F & kFeatExt) stagex[par][lane] = make_int4(x1.ae0, x1.re0, x1.ae1, x1.re1);
+                if constexpr (NORM) {
+                    stagexN[par][lane] = x1;
+                    stS[par][lane] = c1s2;
+                } else if (F & kFeatExt) {
+                    stagex[par][lane] = make_int4(x1.ae0, x1.re0, x1.ae1, x1.re1);
+                }
                 if (i + 1 < kend) {
                     keyC[par][lane] = (c1 != 0 && f) ? pack_key(tot + 1, key_node(c1)) : 0ull;
                     if (NORM) flagC[par][lane] = fl;
@@ -2651,6 +2727,11 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                     r1 = load_row<F>(t, pe0 ? key_node(pe0) : 0u);
                     x1 = load_rowx<F>(t, pe0 ? key_node(pe0) : 0u);
                 }
+                // NORM: this parity's pair now holds pod i+2's statics (the next window's pod
+                // i+2-kend when prefetched)
+                if (i + 2 < kend) stat_load(c1s1, c1s2, stats, i + 2, kend);
+                else if (pref) stat_load(c1s1, c1s2, statsn, i + 2 - kend, knext);
+                QS_RSTAMP_MARK(2)
                 pcur = pn1;
                 if (decltype(hook)::value && pfw) {
                     if (i == kend - 5) rdyv = load_coh_u32(&ctl->rdy[(w + 1) & 1][0]);
@@ -2678,14 +2759,19 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
             const uint32_t ih = pfw ? ((kend - 5) & ~1u) : kend;  // first step with the hooks (even)
             uint32_t i = 0;
             for (; i + 1 < ih; i += 2) {
-                step(plain, i, eX);
-                step(plain, i + 1, eY);
+                step(plain, i, eX, sA1, sA2);
+                step(plain, i + 1, eY, sB1, sB2);
             }
             for (; i + 1 < kend; i += 2) {
-                step(hooked, i, eX);
-                step(hooked, i + 1, eY);
+                step(hooked, i, eX, sA1, sA2);
+                step(hooked, i + 1, eY, sB1, sB2);
             }
-            if (i < kend) step(hooked, i, eX);
+            if (i < kend) step(hooked, i, eX, sA1, sA2);
+            if (NORM && pref && (kend & 1)) {  // the next window's pods 0 / 1 went to the B / A pairs
+                const uint32_t t1 = sA1, t2 = sA2;
+                sA1 = sB1; sA2 = sB2;
+                sB1 = t1; sB2 = t2;
+            }
             if (NORM && pub[(kend - 1) & 1].slot == -2) rescan_c(kend - 1);
             if (NORM && pref && (uint32_t)lane < knext) put_norm((w + 1) & 1, pn0, pn1w);
             __syncthreads();  // B2
@@ -2693,35 +2779,148 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
         }
         if (rdiag && lane == 0) rdiag[4] = nfallback;
     } else if constexpr (NORM) {
-        // ---- waves 4-7: the rescans' extra hands; stage the next window's pod extension records --
+        // ---- waves 4-7: slot statics, the rescans' extra hands, the next window's pod records ------
+        // Per step (work(i), before the step's barrier; a STOP's rescan of pod i-1 already done):
+        //  wave 6: a slot created by pod i-1's winner: its static against this window's pods from
+        //          i+2 on (Tcur; waves A/B take pod i+1's from stS) and against the next window's
+        //          pods (Tnext);
+        //  wave 7: one share of the inherited slots' statics against the next window's pods (Tnext);
+        //  step 0: the next window's pod extension records and flags into LDS.
+        // Between B2 and B3, Tnext is rank-compacted into Tcur for the next window's inherited slots.
         constexpr uint32_t q = sizeof(DPodX) / 16;
+        const uint32_t pw = (uint32_t)(wv - 4);
+        uint32_t ndi = 0;  // this window's inherited slots
         for (uint32_t w = 0; w < nwin; ++w) {
             const uint32_t s0 = w * K, kend = min(K, P - s0);
             const uint32_t knext = w + 1 < nwin ? min(K, P - s0 - K) : 0u;
-            const uint32_t id0 = (uint32_t)(wv - 4) * 64 + lane, id1 = id0 + 256;
+            const uint32_t wb = w & 1, nb = (w + 1) & 1;
+            const PodT<F> *wp = wpods2[wb];
+            const uint32_t id0 = pw * 64 + lane, id1 = id0 + 256;
             const bool h0 = id0 < knext * q, h1 = id1 < knext * q;
             const int4 *src = reinterpret_cast<const int4 *>(podx + (size_t)s0 + K);
             int4 q0 = make_int4(0, 0, 0, 0), q1 = make_int4(0, 0, 0, 0);
             if (h0) q0 = src[id0];
             if (h1) q1 = src[id1];
+            uint32_t nfl = 0;
+            if (pw == 0 && (uint32_t)lane < knext) nfl = pods[s0 + K + lane].flags;
+            // Waves 6 and 7 keep one pod's extension record and flags per lane in registers for the
+            // window (read from LDS once, at step 1): wave 6 lanes 0-31 this window's pod `lane`,
+            // lanes 32-63 and every wave-7 lane the next window's pod `lane & 31`.  Reading a record
+            // per lane and step from LDS held the pipeline waves' reads up by ~850 cycles a step.
+            const uint32_t qq = (uint32_t)lane & 31u;
+            const bool mycur = wv == 6 && lane < 32;
+            DPodX myx{};
+            uint32_t myf = 0;
+            auto load_mine = [&]() {
+                myx = mycur ? wpodx2[wb][qq] : wpodx2[nb][qq];
+                myf = mycur ? wp[qq].flags : nflag2[nb][qq];
+            };
+            // new slot of pod j's winner (j = i - 1): statics against pods >= j + 3 of this window
+            // (cur) and every next-window pod
+            auto new_slot = [&](uint32_t j, bool cur) {
+#ifdef QS_EXP_NOPARK
+                return;
+#endif
+                const ResPub pv = read_pub(&pub[j & 1]);
+                if (pv.ks == 0 || pv.slot >= 0) return;
+                const RowX sx = stagexN[j & 1][pv.src];
+                const uint32_t l = pv.nd_old;
+                const uint32_t st = static_raw(sx.th, sx.ts, sx.lb0, sx.lb1, myf, myx);
+                if (lane < 32) {
+                    if (cur && qq >= j + 3 && qq < kend) Tcur[qq * kResTStride + l] = st;
+                } else if (qq < knext) {
+                    Tnext[qq * kResTStride + l] = st;
+                }
+            };
+            // inherited slots x next-window pods: slots 2j (lanes 0-31) and 2j + 1 (lanes 32-63)
+            auto inherited = [&](uint32_t j) {
+#ifdef QS_EXP_NOPARK
+                return;
+#endif
+                const uint32_t l = 2 * j + (lane < 32 ? 0u : 1u);
+                if (l < ndi && qq < knext) {
+                    const RowX sx = carryxN[l];
+                    Tnext[qq * kResTStride + l] = static_raw(sx.th, sx.ts, sx.lb0, sx.lb1, myf, myx);
+                }
+            };
+            // a rescan of pod j found winner ks: if it is a new slot, stage it as source lane 0 of
+            // step j (wave C's staging): its row before pod j, its static against pod j+2, and its
+            // key and lost-holder flags for pod j+1 after pod j (wave 4, before R5)
+            auto rescan_tail = [&](uint32_t j, uint64_t ks) {
+                const uint32_t W = ks ? key_node(ks) : 0u;
+                const bool slot = __ballot((uint32_t)lane < *snd && sidx[lane] == W) != 0;
+                if (!ks || slot) return;
+                // the staged row is needed even at the window's last pod (waves A/B apply it after
+                // the loop); the key and flags only when pod j+1 is in this window
+                const int pj = j & 1;
+                const RowT<F> rw = load_row<F>(t, W);
+                const RowX xw = load_rowx<F>(t, W);
+                uint32_t st2 = 0;
+                if (j + 2 < kend) st2 = static_raw(xw.th, xw.ts, xw.lb0, xw.lb1, wp[j + 2].flags, wpodx2[wb][j + 2]);
+                if (lane == 0) {
+                    stage[pj][0] = rw;
+                    stagexN[pj][0] = xw;
+                    stS[pj][0] = st2;
+                }
+                if (j + 1 < kend) {
+                    RowT<F> cr = rw;
+                    RowX crx = xw;
+                    reserve(cr, crx, wp[j], +1);
+                    const PodT<F> q1 = wp[j + 1];
+                    const DPodX qx = wpodx2[wb][j + 1];
+                    const NormInfo nf = wnorm2[wb][j + 1];
+                    const double2 yr = wrcp2[wb][j + 1];
+                    const bool f = feasible<F>(cr, crx, q1, qx);
+                    const uint32_t tot = node_total<F>(cr, crx, q1, qx, cv, nf.mt, yr.x, nf.ma, yr.y, nullptr);
+                    uint32_t fl = 0;
+                    if (!f) {
+                        if (F & kFeatTaint) fl |= taint_raw(crx, qx) == nf.mt ? 1u : 0u;
+                        if (F & kFeatAffinity) fl |= affinity_raw(crx, q1, qx) == nf.ma ? 2u : 0u;
+                    }
+                    if (lane == 0) {
+                        keyC[pj][0] = f ? pack_key(tot + 1, W) : 0ull;
+                        flagC[pj][0] = fl;
+                    }
+                }
+            };
             __syncthreads();  // B0
             __syncthreads();  // B1
             for (uint32_t i = 0; i < kend; ++i) {
+                if (i == 0) {
+                    int4 *dst = reinterpret_cast<int4 *>(&wpodx2[nb][0]);
+                    if (h0) dst[id0] = q0;
+                    if (h1) dst[id1] = q1;
+                    if (pw == 0 && (uint32_t)lane < knext) nflag2[nb][lane] = nfl;
+                } else if (wv >= 6) {
+                    if (i == 1) load_mine();
+                    if (wv == 6) new_slot(i - 1, true);
+                    else inherited(i - 1);
+                }
                 __syncthreads();
                 if (pub[i & 1].slot == -2) {
-                    (void)rescan_pass(i, w & 1);
+                    const uint64_t ks = rescan_pass(i, wb);
+                    if (wv == 4) rescan_tail(i, ks);
                     __syncthreads();  // R5
                 }
             }
-            int4 *dst = reinterpret_cast<int4 *>(&wpodx2[(w + 1) & 1][0]);
-            if (h0) dst[id0] = q0;
-            if (h1) dst[id1] = q1;
-            __syncthreads();  // B2
+            if (wv >= 6 && kend == 1) load_mine();
+            if (wv == 6) new_slot(kend - 1, false);
+            if (wv == 7)
+                for (uint32_t j = kend - 1; 2 * j < ndi; ++j) inherited(j);  // (short windows: the rest)
+            __syncthreads();  // B2 (D's slot ranks)
+            for (uint32_t idx = id0; idx < knext * 64; idx += 256) {
+                const uint32_t qq = idx >> 6, l = idx & 63u, r = xrank[l];
+                if (r != 0xFFFFFFFFu) Tcur[qq * kResTStride + r] = Tnext[qq * kResTStride + l];
+            }
+            ndi = (uint32_t)__popcll(__ballot(xrank[lane] != 0xFFFFFFFFu));
             __syncthreads();  // B3
         }
     }
     if (kResDiag && rdiag && lane == 0 && wv < 4) {
         rdiag[8 + wv] = busy_;
+        if (wv == 1) { rdiag[21] = sub_[0]; rdiag[22] = sub_[1]; }
+        if (wv == 3) { rdiag[23] = sub_[0]; rdiag[24] = sub_[1]; rdiag[25] = sub_[2]; }
+        if (wv == 0) rdiag[26] = sub_[0];
         if (wv == 0) rdiag[12] = steps_;
     }
 }
@@ -2737,11 +2936,11 @@ __global__ __launch_bounds__(kResBS) void k_la_stream_res(DevTable t, const PodT
                                                        uint64_t *__restrict__ out_key,
                                                        uint64_t *__restrict__ stamps, ResCtl *ctl,
                                                        uint64_t *__restrict__ rdiag, const DPodX *__restrict__ podx,
-                                                       uint4 *npart0, NormInfo *norm0, unsigned long long *nfall,
-                                                       ResShard rsh) {
+                                                       uint4 *npart0, NormInfo *norm0, uint32_t *stat0,
+                                                       unsigned long long *nfall, ResShard rsh) {
     if (blockIdx.x != 0) {
         res_selector<E, E2, F>(t, pods, c, P, K, G, L, chunk, nwin, lists0, clists0, lwords, cwords, ctl,
-                               blockIdx.x - 1, gridDim.x - 1, rdiag, podx, npart0, norm0, rsh);
+                               blockIdx.x - 1, gridDim.x - 1, rdiag, podx, npart0, norm0, stat0, rsh);
         return;
     }
     if (rsh.W > 1 && threadIdx.x == 0)  // this rank is in its new run: peers may write its mailbox
@@ -2758,16 +2957,22 @@ __global__ __launch_bounds__(kResBS) void k_la_stream_res(DevTable t, const PodT
     }
     const uint64_t t0 = rdiag ? __builtin_amdgcn_s_memrealtime() : 0ull;
     la_resolve4_stream<F, K32>(lds, t, pods, c, P, K, nwin, lists0, lwords, out_node, out_key, stamps, ctl, rdiag,
-                               podx, norm0, nfall);
+                               podx, norm0, stat0, nfall);
     if (rdiag && threadIdx.x == 0) { rdiag[1] = __builtin_amdgcn_s_memrealtime() - t0; rdiag[3] = nwin; }
 }
 
+// Dynamic LDS above 64 KiB (the normalizing resident stream's statics) needs the per-kernel limit
+// raised before the launch and before the occupancy query.
+static hipError_t res_lds_attr(const void *fn, size_t lds4) {
+    if (lds4 <= 64 * 1024) return hipSuccess;
+    return hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds4);
+}
 template <uint32_t F>
 static hipError_t la_stream_res_f(const DevTable &t, const void *pods, const DPodX *podx, const DevCfg &c, uint32_t P,
                                   const LaGeom &geo, uint64_t *lists0, uint64_t *clists0, uint32_t lwords,
-                                  uint32_t cwords, uint4 *npart0, NormInfo *norm0, unsigned long long *nfall,
-                                  int32_t *on, uint64_t *ok, uint64_t *st, void *ctl, uint32_t sel_blocks,
-                                  uint64_t *rdiag, const ResShard &rsh, hipStream_t stream) {
+                                  uint32_t cwords, uint4 *npart0, NormInfo *norm0, uint32_t *stat0,
+                                  unsigned long long *nfall, int32_t *on, uint64_t *ok, uint64_t *st, void *ctl,
+                                  uint32_t sel_blocks, uint64_t *rdiag, const ResShard &rsh, hipStream_t stream) {
     const uint32_t K = geo.K, G = geo.G, L = geo.L, nwin = (P + K - 1) / K;
     // sharded: Fit + Balanced profiles, W * L <= 512 keys per cross merge, K <= 32 pods per slot
     if (rsh.W > 1 && ((F & kFeatNorm) || rsh.W * L > (uint32_t)kResBS || K > 32 || rsh.W > 16 || !rsh.peers))
@@ -2775,18 +2980,21 @@ static hipError_t la_stream_res_f(const DevTable &t, const void *pods, const DPo
     const uint32_t E2 = 1;  // a pod's G*L <= 512 chunk keys, one per merging thread
     if (G * L > (uint32_t)kResBS) return hipErrorInvalidValue;
     const size_t lds4 = res_stream_lds_bytes<F>(t.n);
-    if (lds4 > 64 * 1024) return hipErrorInvalidValue;
+    if (lds4 > kResLdsMax) return hipErrorInvalidValue;
     // NORM: K <= kResNormK staged records per window, and a task per workgroup (the G chunks of a
     // pod wait for each other's partial maxima)
-    if ((F & kFeatNorm) && (K > kResNormK || sel_blocks < K * G || !podx || !npart0 || !norm0))
+    if ((F & kFeatNorm) && (K > kResNormK || sel_blocks < K * G || !podx || !npart0 || !norm0 || !stat0))
         return hipErrorInvalidValue;
     const dim3 grid(1 + sel_blocks);
     const PodT<F> *pp = (const PodT<F> *)pods;
     ResCtl *rc = (ResCtl *)ctl;
 #define QS_RESK(EE, EE2, KK)                                                                                          \
+    do {                                                                                                              \
+    if (hipError_t ea = res_lds_attr((const void *)k_la_stream_res<F, EE, EE2, KK>, lds4); ea != hipSuccess) return ea; \
     hipLaunchKernelGGL((k_la_stream_res<F, EE, EE2, KK>), grid, dim3(kResBS), lds4, stream, t, pp, c, P, K, G, L,       \
                        geo.chunk, nwin, lists0, clists0, lwords, cwords, on, ok, st, rc, rdiag, podx, npart0, norm0,   \
-                       nfall, rsh)
+                       stat0, nfall, rsh);                                                                       \
+    } while (0)
 #define QS_RESE(EE, EE2) \
     else if (geo.E == EE && E2 == EE2) { if (geo.k32) QS_RESK(EE, EE2, true); else QS_RESK(EE, EE2, false); }
     if (false) {
@@ -2811,7 +3019,8 @@ static int la_stream_res_per_cu(const LaGeom &geo, uint32_t n) {
     QS_RESP(8, true) QS_RESP(8, false) QS_RESP(16, true) QS_RESP(16, false)
 #undef QS_RESP
     int per = 0;
-    if (!fn || hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, kResBS, lds4) != hipSuccess) {
+    if (!fn || res_lds_attr(fn, lds4) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, kResBS, lds4) != hipSuccess) {
         (void)hipGetLastError();
         return 0;
     }

@@ -105,11 +105,12 @@ struct ResShard {
     uint64_t hello, flags, lists;
 };
 // Normalizing profiles (TaintToleration / NodeAffinity) also pass the pod extension records (podx),
-// npart (2 x K x G uint4 partial maxima), norm (2 x 64 NormInfo) and nfall ({rescans, windows with
-// a rescan}); they need K <= 32 and sel_blocks >= K * G.
+// npart (2 x K x G uint4 partial maxima), norm (2 x 64 NormInfo), stat (2 x K x 128 u32 entry
+// statics, res_stream_stat_words) and nfall ({rescans, windows with a rescan}); they need K <= 32
+// and sel_blocks >= K * G.
 hipError_t launch_la_stream_res(const DevTable &t, const void *pods, const DPodX *podx, const DevCfg &c, uint32_t P,
                                 const LaGeom &geo, uint64_t *lists0, uint64_t *clists0, uint32_t lwords,
-                                uint32_t cwords, uint4 *npart, NormInfo *norm, unsigned long long *nfall, int32_t *on,
+                                uint32_t cwords, uint4 *npart, NormInfo *norm, uint32_t *stat, unsigned long long *nfall, int32_t *on,
                                 uint64_t *ok, uint64_t *st, void *ctl, uint32_t sel_blocks, uint64_t *rdiag,
                                 const ResShard &rsh, hipStream_t stream);
 
