@@ -2258,6 +2258,9 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
     DevCfg cv = c;
     asm volatile("" : "+v"(cv.yd_both), "+v"(cv.yd_c), "+v"(cv.yd_m), "+v"(cv.wc), "+v"(cv.wm));
     uint64_t ts_ = 0, busy_ = 0, steps_ = 0, sub_[3] = {0, 0, 0};
+    // the pipeline waves (0-3) win VALU issue arbitration against the parked waves sharing their
+    // SIMDs (MI355X_MICROARCH.md, two waves per SIMD: priority, then age)
+    if (wv < 4) __builtin_amdgcn_s_setprio(3);
 
     for (uint32_t i = threadIdx.x; i < nwords; i += 256) dirty[i] = 0;
     if (threadIdx.x < min(K, P)) wpods2[0][threadIdx.x] = pods[threadIdx.x];
@@ -3063,11 +3066,9 @@ __global__ __launch_bounds__(64 * kClaimWaves) void k_batch_claim(
     const uint32_t nb = ctrl[0], cursor = ctrl[1];
     for (uint32_t i = tid; i < nwords; i += 64 * kClaimWaves) claimed[i] = 0;
     for (uint32_t i = tid; i < kMaxApps * kMaxZones / 32; i += 64 * kClaimWaves) claimed_az[i] = 0;
-    // Staging, all waves: each pod's list sorted best-first (so that a pod's claim is the first
-    // still-available lane: one ballot instead of a 64-bit max reduction in the sequential loop)
-    // and, for zone-anti-affinity pods, the zones of its candidates.
-    // Wave wv takes pods wv + 16q (q < 4): all loads of a round are issued before any is used and
-    // the four sorts interleave.
+    // Staging, all waves: each pod's list, sorted best-first by the merge (so that a pod's claim is
+    // the first still-available lane), and, for zone-anti-affinity pods, the zones of its candidates.
+    // Wave wv takes pods wv + 16q (q < 4): all loads of a round are issued before any is used.
     {
         constexpr int Q = 64 / kClaimWaves;
         uint64_t ev[Q];
@@ -3084,8 +3085,7 @@ __global__ __launch_bounds__(64 * kClaimWaves) void k_batch_claim(
             sv[q] = fv[q];
             fv[q] = (uint32_t)wv + kClaimWaves * q < nb ? pods[sv[q]].flags : 0u;
         }
-#pragma unroll
-        for (int q = 0; q < Q; ++q) ev[q] = wave_sort_desc(ev[q], lane);
+        // (the lists arrive sorted best-first: k_la_merge / a single-chunk k_la_select sort them)
         uint32_t zv[Q];
 #pragma unroll
         for (int q = 0; q < Q; ++q)

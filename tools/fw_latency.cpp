@@ -42,6 +42,14 @@ int main(int argc, char **argv) {
     std::vector<int32_t> score(4 * (size_t)n), total(n), placement(p);
     std::vector<double> lat(p);
     using clk = std::chrono::steady_clock;
+    // warm-up (module load, first-touch of the pinned output pages): score-only calls, which leave
+    // the table unchanged; a plugin process pays this once, not per pod
+    for (uint32_t j = 0; j < 32 && p > 0; ++j) {
+        int32_t best = -2;
+        if (qs_score_pod(ctx, &pods[0], outputs ? feas.data() : nullptr, outputs ? score.data() : nullptr,
+                         outputs ? total.data() : nullptr, &best) != QS_OK)
+            return 5;
+    }
     for (uint32_t j = 0; j < p; ++j) {
         const auto t0 = clk::now();
         int32_t best = -2;
