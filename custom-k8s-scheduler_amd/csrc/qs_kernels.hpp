@@ -3110,25 +3110,34 @@ __global__ __launch_bounds__(64 * kClaimWaves) void k_batch_claim(
     const uint32_t my_s = (uint32_t)lane < nb ? lpod[lane] : 0u;
     const uint32_t my_flags = (uint32_t)lane < nb ? lpod[64 + lane] : 0u;
     CLAIM_STAMP(1);
-    // Software-pipelined walk.  Entering iteration i: pod i's entries (e, z) and its exact
-    // availability mask am (claims of pods < i), pod i+1's entries (e1, z1).  Pod i+1's bitmap
+    // Software-pipelined walk.  Entering step i: pod i's entries (its register set) and its exact
+    // availability mask am (claims of pods < i), pod i+1's entries (the next set).  Pod i+1's bitmap
     // words are read before pod i's claim is written (they see the claims of pods < i) and then
     // patched with pod i's claim (node w; (app, zone) when both are zone-anti-affinity pods), so
-    // the LDS round trip overlaps pod i's scalar chain instead of following it.
+    // the LDS round trip overlaps pod i's scalar chain instead of following it.  Three entry
+    // register sets rotate over an unrolled-by-3 loop: pod i+2's entries load straight into the
+    // set pod i+1 will not need again (a copy at the back-edge would wait for that load).
     auto lane_node = [](uint64_t v, bool ok) { return (ok && v) ? key_node(v) : 0u; };
-    uint64_t e = lkey[lane];
-    uint32_t z = lzone[lane] & (kMaxZones - 1);
+    struct Ents {
+        uint64_t e;
+        uint32_t z;
+    };
+    auto ents = [&](uint32_t j) -> Ents {
+        const uint32_t jj = min(j, 63u);
+        return Ents{lkey[jj * 64 + lane], lzone[jj * 64 + lane] & (kMaxZones - 1)};
+    };
+    Ents sa = ents(0), sb = ents(1), sc{0ull, 0u};
     uint32_t fl = (uint32_t)__builtin_amdgcn_readlane((int)my_flags, 0);
     uint64_t am;
     {
-        const uint32_t node = lane_node(e, true), azb = pod_app(fl) * kMaxZones + z;
+        const uint32_t node = lane_node(sa.e, true), azb = pod_app(fl) * kMaxZones + sa.z;
         const uint32_t taken = ((claimed[node >> 5] >> (node & 31)) |
                                 (pod_aa(fl) == 2u ? claimed_az[azb >> 5] >> (azb & 31) : 0u)) & 1u;
-        am = __ballot(e != 0ull && taken == 0u);
+        am = __ballot(sa.e != 0ull && taken == 0u);
     }
-    uint64_t e1 = lkey[min(1u, 63u) * 64 + lane];
-    uint32_t z1 = lzone[min(1u, 63u) * 64 + lane] & (kMaxZones - 1);
-    for (uint32_t i = 0; i < nb; ++i) {
+    auto step = [&](uint32_t i, const Ents &cur, const Ents &nxt, Ents &n2) {
+        const uint64_t e = cur.e, e1 = nxt.e;
+        const uint32_t z = cur.z, z1 = nxt.z;
         const uint32_t aa = pod_aa(fl), app = pod_app(fl);
         const bool has1 = i + 1 < nb;
         const uint32_t fl1 = (uint32_t)__builtin_amdgcn_readlane((int)my_flags, (int)min(i + 1, 63u));
@@ -3136,9 +3145,7 @@ __global__ __launch_bounds__(64 * kClaimWaves) void k_batch_claim(
         // pod i+1: bitmap words (claims of pods < i) and pod i+2's entries, all in flight now
         const uint32_t node1 = lane_node(e1, has1), azb1 = app1 * kMaxZones + z1;
         const uint32_t cw1 = claimed[node1 >> 5], aw1 = claimed_az[azb1 >> 5];
-        const uint32_t j2 = min(i + 2, 63u);
-        const uint64_t e2 = lkey[j2 * 64 + lane];
-        const uint32_t z2 = lzone[j2 * 64 + lane] & (kMaxZones - 1);
+        n2 = ents(i + 2);
         // pod i
         uint32_t w = 0xFFFFFFFFu, zw = 0xFFFFFFFFu;
         if (am) {
@@ -3166,12 +3173,16 @@ __global__ __launch_bounds__(64 * kClaimWaves) void k_batch_claim(
         const bool az_hit = aa1 == 2u && aa == 2u && app1 == app && z1 == zw;
         const uint32_t taken1 = ((cw1 >> (node1 & 31)) | (aa1 == 2u ? aw1 >> (azb1 & 31) : 0u)) & 1u;
         am = __ballot(has1 && e1 != 0ull && taken1 == 0u && node1 != w && !az_hit);
-        e = e1;
-        z = z1;
         fl = fl1;
-        e1 = e2;
-        z1 = z2;
+    };
+    uint32_t i = 0;
+    for (; i + 2 < nb; i += 3) {
+        step(i, sa, sb, sc);
+        step(i + 1, sb, sc, sa);
+        step(i + 2, sc, sa, sb);
     }
+    if (i < nb) step(i, sa, sb, sc);
+    if (i + 1 < nb) step(i + 1, sb, sc, sa);
     CLAIM_STAMP(2);
     // apply every claim (distinct nodes; counts of one (app, zone) may be shared: atomics)
     if ((uint32_t)lane < nb && my_node != -2) {

@@ -7,7 +7,7 @@ cd "$(dirname "$0")/../custom-k8s-scheduler_amd"
 tag=$1; defs=$2
 B=build_$tag
 mkdir -p $B
-F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -fvisibility=hidden -ffp-contract=off $defs"
+F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -fvisibility=hidden -ffp-contract=off -mllvm -amdgpu-atomic-optimizer-strategy=None $defs"
 for f in qs_kernels qs_kernels_wide; do /opt/rocm/bin/hipcc $F -c csrc/$f.hip -o $B/$f.o & done
 for f in qs_host qs_helpers qs_dist; do /opt/rocm/bin/hipcc $F -x hip -c csrc/$f.cpp -o $B/$f.o & done
 wait
