@@ -1321,7 +1321,10 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                     HIPCHK(hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, c->device));
                     c->cus = cu;
                 }
-                const LaGeom rgeo = la_stream_res_plan(geo, c->dc.feat, n, (uint32_t)c->cus);
+                // two selector workgroups per CU when the occupancy check admits them, else one
+                LaGeom rgeo = la_stream_res_plan(geo, c->dc.feat, n, (uint32_t)c->cus, 2);
+                if (rgeo.G > 0 && rgeo.K * rgeo.G + 1 > la_stream_res_max_blocks(rgeo, c->dc.feat, n, (uint32_t)c->cus))
+                    rgeo = la_stream_res_plan(geo, c->dc.feat, n, (uint32_t)c->cus, 1);
                 // one selector workgroup per (pod, chunk) task of a window, at most one per
                 // remaining CU (they loop over the tasks otherwise); QS_RES_SEL overrides
                 static const char *senv = getenv("QS_RES_SEL");

@@ -141,9 +141,12 @@ hipError_t launch_la_window(const DevTable &t, const void *pods, const DPodX *po
 }
 
 // Resident-stream geometry: every (pod, chunk) task of a window gets its own selector workgroup
-// (K * G <= cus - 1, G <= 8 so a merge reads <= 512 keys), chunks of E * 256 nodes with E from
-// the instantiated set; G = 0 when the table is too large or the profile / layout is not covered.
-LaGeom la_stream_res_plan(const LaGeom &geo, uint32_t feat, uint32_t n, uint32_t cus) {
+// (K * G <= per_cu * cus - 1), chunks of E * 512 nodes with E from the instantiated set, G <= 8
+// (a merge reads <= 512 keys, one per thread) or, with two workgroups per CU, G <= 16 (Fit +
+// Balanced (+ext): e2 = 2 keys per merging thread); G = 0 when the table is too large or the
+// profile / layout is not covered.  per_cu = 2 is tried first and kept when the occupancy check
+// admits it (more, shorter selector tasks: the config-3 stream was selector-bound).
+LaGeom la_stream_res_plan(const LaGeom &geo, uint32_t feat, uint32_t n, uint32_t cus, uint32_t per_cu) {
     LaGeom r = geo;
     r.G = 0;
     // compact Fit + Balanced (+ extended) profiles, and the normalizing ones (K <= kResNormK)
@@ -154,7 +157,8 @@ LaGeom la_stream_res_plan(const LaGeom &geo, uint32_t feat, uint32_t n, uint32_t
                                      : fit && geo.nv == 1 && geo.K <= 32 && geo.W * geo.L <= (uint32_t)kResBS;
     if (!((fit || norm) && shard_ok && geo.waves == 4 && geo.L <= 64 && n > 0 && cus > geo.K)) return r;
     n = (n + geo.W - 1) / geo.W;  // this rank's node range
-    const uint32_t gmax = std::min(8u, (cus - 1) / geo.K);
+    const bool two = per_cu >= 2 && fit;
+    const uint32_t gmax = std::min(two ? 16u : 8u, ((two ? 2u : 1u) * cus - 1) / geo.K);
     if (gmax == 0) return r;
     constexpr uint32_t bs = kResBS;  // threads of a selector workgroup
     const uint32_t G0 = std::min(gmax, (n + 5 * bs - 1) / (5 * bs));
@@ -164,7 +168,9 @@ LaGeom la_stream_res_plan(const LaGeom &geo, uint32_t feat, uint32_t n, uint32_t
         if (e >= e_need) { E = e; break; }
     if (E == 0) return r;  // more than 8 chunks of 8,192 nodes: per-window launches
     const uint32_t G = (n + E * bs - 1) / (E * bs);
-    if (G * geo.L > bs) return r;
+    const uint32_t e2 = G * geo.L <= bs ? 1u : 2u;
+    if (G * geo.L > e2 * bs || (e2 == 2 && (!two || E == 3))) return r;
+    r.e2 = e2;
     r.E = E;
     r.chunk = E * bs;
     r.G = G;
@@ -180,7 +186,12 @@ uint32_t la_stream_res_max_blocks(const LaGeom &geo, uint32_t feat, uint32_t n, 
     const int per = (feat & kFeatNorm)  ? la_stream_res_per_cu<kFeatExt | kFeatTaint | kFeatAffinity>(geo, n)
                     : (feat & kFeatExt) ? la_stream_res_per_cu<kFeatExt>(geo, n)
                                         : la_stream_res_per_cu<0>(geo, n);
-    const int safe = per >= 2 ? per - 1 : per;
+    // The API's answer can exceed what the hardware admits by one workgroup when the SGPR budget
+    // (800 per SIMD, (ceil(sgpr / 16) * 16 + 16) per wave) binds first (MI355X_MICROARCH.md,
+    // residency): cap it by that rule, with kResSgprMax >= every instantiation's sgpr_count
+    // (tools/kres.sh: 104-106), two waves per SIMD for a 512-thread workgroup.
+    const int sgpr_waves = 800 / (((int)kResSgprMax + 15) / 16 * 16 + 16);
+    const int safe = std::min(per, sgpr_waves / (kResBS / 64 / 4));
     return (uint32_t)std::max(0, safe) * cus;
 }
 

@@ -2088,7 +2088,8 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
 // extra waves also stage the next window's pod extension records (176 B each) in LDS.
 constexpr uint32_t kResNormK = 32;  // window pods whose NORM records are staged per parity (K <= 32)
 constexpr uint32_t kResTStride = 65;
-constexpr size_t kResLdsMax = 96 * 1024;  // dynamic LDS of the resident launch (gfx950: up to 160 KiB per workgroup)  // slot statics [pod][lane] rows, padded: both access patterns conflict-free
+constexpr size_t kResLdsMax = 96 * 1024;
+constexpr uint32_t kResSgprMax = 112;  // bound on the resident kernels' sgpr_count (checked: tools/kres.sh)  // dynamic LDS of the resident launch (gfx950: up to 160 KiB per workgroup)  // slot statics [pod][lane] rows, padded: both access patterns conflict-free
 template <uint32_t F>
 constexpr size_t res_stream_lds_bytes(uint32_t n) {
     size_t b = ((((size_t)n + 31) / 32 + 3) & ~(size_t)3) * 4 + 4 * 2 * 64 * 8 + 2 * 64 * (sizeof(RowT<F>) + sizeof(int4)) +
@@ -2980,8 +2981,8 @@ static hipError_t la_stream_res_f(const DevTable &t, const void *pods, const DPo
     // sharded: Fit + Balanced profiles, W * L <= 512 keys per cross merge, K <= 32 pods per slot
     if (rsh.W > 1 && ((F & kFeatNorm) || rsh.W * L > (uint32_t)kResBS || K > 32 || rsh.W > 16 || !rsh.peers))
         return hipErrorInvalidValue;
-    const uint32_t E2 = 1;  // a pod's G*L <= 512 chunk keys, one per merging thread
-    if (G * L > (uint32_t)kResBS) return hipErrorInvalidValue;
+    const uint32_t E2 = geo.e2;  // a pod's G*L <= 512 * E2 chunk keys, E2 per merging thread
+    if (G * L > E2 * (uint32_t)kResBS || (E2 == 2 && (F & kFeatNorm))) return hipErrorInvalidValue;
     const size_t lds4 = res_stream_lds_bytes<F>(t.n);
     if (lds4 > kResLdsMax) return hipErrorInvalidValue;
     // NORM: K <= kResNormK staged records per window, and a task per workgroup (the G chunks of a
@@ -3000,11 +3001,17 @@ static hipError_t la_stream_res_f(const DevTable &t, const void *pods, const DPo
     } while (0)
 #define QS_RESE(EE, EE2) \
     else if (geo.E == EE && E2 == EE2) { if (geo.k32) QS_RESK(EE, EE2, true); else QS_RESK(EE, EE2, false); }
+// two keys per merging thread: Fit + Balanced (+ext) instantiations only (normalizing profiles keep G <= 8)
+#define QS_RESE2(EE) \
+    else if (geo.E == EE && E2 == 2 && (F & kFeatNorm) == 0) { \
+        if constexpr ((F & kFeatNorm) == 0) { if (geo.k32) QS_RESK(EE, 2, true); else QS_RESK(EE, 2, false); } }
     if (false) {
     }
     QS_RESE(3, 1) QS_RESE(5, 1) QS_RESE(8, 1) QS_RESE(16, 1)
+    QS_RESE2(5) QS_RESE2(8) QS_RESE2(16)
     else return hipErrorInvalidValue;
 #undef QS_RESE
+#undef QS_RESE2
 #undef QS_RESK
     return hipGetLastError();
 }
@@ -3017,10 +3024,16 @@ static int la_stream_res_per_cu(const LaGeom &geo, uint32_t n) {
     const size_t lds4 = res_stream_lds_bytes<F>(n);
     const void *fn = nullptr;
 #define QS_RESP(EE, KK) \
-    if (geo.E == EE && (geo.k32 != 0) == KK) fn = (const void *)k_la_stream_res<F, EE, 1, KK>;
+    if (geo.E == EE && geo.e2 == 1 && (geo.k32 != 0) == KK) fn = (const void *)k_la_stream_res<F, EE, 1, KK>;
     QS_RESP(3, true) QS_RESP(3, false) QS_RESP(5, true) QS_RESP(5, false)
     QS_RESP(8, true) QS_RESP(8, false) QS_RESP(16, true) QS_RESP(16, false)
 #undef QS_RESP
+    if constexpr ((F & kFeatNorm) == 0) {
+#define QS_RESP2(EE, KK) \
+        if (geo.E == EE && geo.e2 == 2 && (geo.k32 != 0) == KK) fn = (const void *)k_la_stream_res<F, EE, 2, KK>;
+        QS_RESP2(5, true) QS_RESP2(5, false) QS_RESP2(8, true) QS_RESP2(8, false) QS_RESP2(16, true) QS_RESP2(16, false)
+#undef QS_RESP2
+    }
     int per = 0;
     if (!fn || res_lds_attr(fn, lds4) != hipSuccess ||
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, kResBS, lds4) != hipSuccess) {

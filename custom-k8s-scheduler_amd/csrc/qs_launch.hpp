@@ -33,6 +33,7 @@ struct HostRow {
 struct LaGeom {
     uint32_t K, L, G, E, chunk, epl, waves, k32;
     uint32_t W, v0, nv, eplr, lr;
+    uint32_t e2 = 1;  // resident stream: chunk keys per merging thread (G * L <= 512 * e2)
 };
 // Kernel-side shard view of the lists: [W][K][GLp] uint64 keys, RS = K * GLp.
 struct LaShard {
@@ -90,7 +91,7 @@ hipError_t launch_ready_set(uint64_t *ready, uint64_t value, hipStream_t stream)
 // per-window path (lwords / cwords per parity).
 // G = 0: unsupported.  Sharded contexts (geo.W > 1, Fit + Balanced (+ ext) only) plan their own
 // node range of ceil(n / W) nodes.
-LaGeom la_stream_res_plan(const LaGeom &geo, uint32_t feat, uint32_t n, uint32_t cus);
+LaGeom la_stream_res_plan(const LaGeom &geo, uint32_t feat, uint32_t n, uint32_t cus, uint32_t per_cu = 1);
 size_t la_stream_res_ctl_bytes();
 // Workgroups of that launch guaranteed co-resident on `cus` CUs (occupancy query, one per CU of margin).
 uint32_t la_stream_res_max_blocks(const LaGeom &geo, uint32_t feat, uint32_t n, uint32_t cus);

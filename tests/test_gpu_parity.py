@@ -108,11 +108,13 @@ def test_config2_full_lookahead(oracle):
 
 @pytest.mark.parametrize("config,n,p,K", [(1, 100, 1000, 32), (2, 1500, 6000, 32), (2, 5000, 3000, 32),
                                           (2, 9000, 7000, 32), (2, 30000, 4000, 32), (2, 1500, 6000, 7),
-                                          (2, 2000, 5000, 16), (2, 3000, 2000, 1)])
+                                          (2, 2000, 5000, 16), (2, 3000, 2000, 1), (2, 50000, 3000, 32),
+                                          (4, 40000, 3000, 32), (2, 100000, 1500, 32)])
 def test_resident_stream(oracle, monkeypatch, config, n, p, K):
     """The resident lookahead stream (the whole window sequence as one launch of a resolver and
-    selector workgroups) across selector geometries (1 to 7 node chunks, 3 to 16
-    nodes per lane, partial last windows, K = 1..32): bit-exact vs the oracle, reported in
+    selector workgroups) across selector geometries (1 to 16 node chunks, 3 to 16
+    nodes per lane, one or two keys per merging thread with two selector workgroups per CU, ext
+    resources, partial last windows, K = 1..32): bit-exact vs the oracle, reported in
     stats.resident, and identical to the per-window launches (QS_RESIDENT=0)."""
     nodes, pods = synth_generate(config, n, p)
     g = run_gpu(nodes, pods, {}, "lookahead", lookahead=K)
@@ -126,8 +128,9 @@ def test_resident_stream(oracle, monkeypatch, config, n, p, K):
 
 
 def test_resident_declines_large_tables(oracle):
-    """Beyond 7 chunks of 8,192 nodes (K = 32) the stream runs as per-window launches."""
-    nodes, pods = synth_generate(2, 70000, 600)
+    """Beyond 15 chunks of 8,192 nodes (K = 32, two selector workgroups per CU) the stream runs as
+    per-window launches."""
+    nodes, pods = synth_generate(2, 130000, 600)
     g = run_gpu(nodes, pods, {}, "lookahead")
     assert g[3]["resident"] == 0
     o = run_oracle(oracle, nodes, pods, {})

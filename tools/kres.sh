@@ -15,7 +15,7 @@ for blk in re.split(r'\n\s+- \.agpr_count', txt)[1:]:
     if '$pat' not in name: continue
     g = lambda k: re.search(r'\.' + k + r':\s+(\d+)', blk).group(1)
     short = re.search(r'(k_\w+?)I(\w+?)EEEv', name)
-    print(short.group(1) if short else name[:50], short.group(2) if short else '', 'vgpr', g('vgpr_count'),
+    print(short.group(1) if short else name[:50], short.group(2) if short else '', 'vgpr', g('vgpr_count'), 'sgpr', g('sgpr_count'),
           'scratch', g('private_segment_fixed_size'), 'lds', g('group_segment_fixed_size'))
 "
 rm -rf $tmp
