@@ -495,7 +495,7 @@ def e2e_leg(cx, nodes, pods, gpu_placement):
             "placements_match": bool(np.array_equal(placement, gpu_placement))}
 
 
-def framework_leg(cx, n_nodes=5000, n_pods=2000):
+def framework_leg(cx, n_nodes=5000, n_pods=5000):
     """The framework-embedded path (SURVEY.md §3.4, §5 p99 definition): per pod one qs_score_pod
     (PreFilter..NormalizeScore over all nodes, per-node feasible / plugin scores / totals copied
     back for Filter/Score lookups) + one qs_reserve of the chosen node, host wall per pod through

@@ -940,6 +940,38 @@ static qs_status reserve_impl(qs_ctx *c, uint32_t node, const qs_pod *p, int sig
 qs_status qs_reserve(qs_ctx *c, uint32_t node, const qs_pod *p) { return reserve_impl(c, node, p, +1); }
 qs_status qs_unreserve(qs_ctx *c, uint32_t node, const qs_pod *p) { return reserve_impl(c, node, p, -1); }
 
+// The packed outputs of the one-launch score (pinned host memory, written by the kernel) into the
+// caller's arrays: 16 nodes per step as vectors (the pinned lines come from DRAM once; the byte scores
+// widen to the four int32 plugin scores), the tail one by one.
+static void unpack_scores(const int32_t *tot, const uint32_t *sco, uint32_t n, uint8_t *feas, int32_t *score,
+                          int32_t *total) {
+    typedef int32_t i32x16 __attribute__((ext_vector_type(16)));
+    typedef uint8_t u8x16 __attribute__((ext_vector_type(16)));
+    uint32_t i = 0;
+    for (; i + 16 <= n; i += 16) {
+        i32x16 t;
+        std::memcpy(&t, tot + i, sizeof t);
+        if (total) std::memcpy(total + i, &t, sizeof t);
+        if (feas) {
+            const u8x16 f = __builtin_convertvector(t >= 0, u8x16) & (uint8_t)1;
+            std::memcpy(feas + i, &f, sizeof f);
+        }
+        if (score)
+            for (uint32_t q = 0; q < 4; ++q) {
+                u8x16 b;
+                std::memcpy(&b, sco + i + 4 * q, sizeof b);
+                const i32x16 w = __builtin_convertvector(b, i32x16);
+                std::memcpy(score + 4 * (size_t)(i + 4 * q), &w, sizeof w);
+            }
+    }
+    for (; i < n; ++i) {
+        if (total) total[i] = tot[i];
+        if (feas) feas[i] = tot[i] >= 0;
+        if (score)
+            for (uint32_t k = 0; k < 4; ++k) score[4 * (size_t)i + k] = (int32_t)((sco[i] >> (8 * k)) & 255u);
+    }
+}
+
 qs_status qs_score_pod(qs_ctx *c, const qs_pod *pod, uint8_t *feas, int32_t *score, int32_t *total,
                        int32_t *best) {
     return guarded(c, [&] {
@@ -967,10 +999,14 @@ qs_status qs_score_pod(qs_ctx *c, const qs_pod *pod, uint8_t *feas, int32_t *sco
                 c->pin_bytes = pb;
                 std::memset(c->pin, 0, pb);
             }
+            if (!c->score_gs.p) {
+                c->score_gs.ensure(16);
+                HIPCHK(hipMemsetAsync(c->score_gs.p, 0, 16, c->stream));
+            }
             const uint32_t pidx = c->pend < n ? c->pend : 0xFFFFFFFFu;
             const HostRow prow = pidx < n ? compact_row(c->m, pidx, c->shift, c->wide) : HostRow{};
             const uint64_t seq = ++c->score_seq;
-            HIPCHK(launch_score_pod1(c->dt, dp, &dx, dc, static_cast<uint8_t *>(c->pin), seq, pidx, prow, c->stream));
+            HIPCHK(launch_score_pod1(c->dt, dp, &dx, dc, static_cast<uint8_t *>(c->pin), c->score_gs.as<uint64_t>(), seq, pidx, prow, c->stream));
             c->pend = 0xFFFFFFFFu;
             // the done word: polled (bounded), then the stream is checked for an error
             volatile uint64_t *done = reinterpret_cast<volatile uint64_t *>(static_cast<uint8_t *>(c->pin) + 8);
@@ -988,17 +1024,7 @@ qs_status qs_score_pod(qs_ctx *c, const qs_pod *pod, uint8_t *feas, int32_t *sco
             std::memcpy(&kbest, h, 8);
             const int32_t *tot = reinterpret_cast<const int32_t *>(h + 16);
             const uint32_t *sco = reinterpret_cast<const uint32_t *>(h + 16 + 4 * (size_t)n);
-            if (total) std::memcpy(total, tot, 4 * (size_t)n);
-            if (feas)
-                for (uint32_t i = 0; i < n; ++i) feas[i] = tot[i] >= 0;
-            if (score)
-                for (uint32_t i = 0; i < n; ++i) {
-                    const uint32_t v = sco[i];
-                    score[4 * (size_t)i] = (int32_t)(v & 255u);
-                    score[4 * (size_t)i + 1] = (int32_t)((v >> 8) & 255u);
-                    score[4 * (size_t)i + 2] = (int32_t)((v >> 16) & 255u);
-                    score[4 * (size_t)i + 3] = (int32_t)(v >> 24);
-                }
+            unpack_scores(tot, sco, n, feas, score, total);
             if (best) *best = kbest ? (int32_t)(0xFFFFFFFFu - (uint32_t)kbest) : -1;
             return;
         }

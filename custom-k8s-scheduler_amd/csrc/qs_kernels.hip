@@ -106,13 +106,13 @@ size_t scan_scratch_bytes() { return sizeof(ScanScratch); }
 uint32_t score_pod1_max_nodes() { return kScorePod1Max; }
 size_t score_pod1_pack_bytes(uint32_t n) { return score_pack_bytes(n); }
 hipError_t launch_score_pod1(const DevTable &t, const void *pod, const DPodX *podx, const DevCfg &c, uint8_t *hout,
-                             uint64_t seq, uint32_t pidx, const HostRow &prow, hipStream_t stream) {
-    if (t.wrows) return wide_score_pod1(t, pod, podx, c, hout, seq, pidx, prow, stream);
+                             uint64_t *gs, uint64_t seq, uint32_t pidx, const HostRow &prow, hipStream_t stream) {
+    if (t.wrows) return wide_score_pod1(t, pod, podx, c, hout, gs, seq, pidx, prow, stream);
     switch (feat_class(c.feat)) {
-        case 0: return score_pod1_f<0>(t, pod, podx, c, hout, seq, pidx, prow, stream);
-        case kFeatExt: return score_pod1_f<kFeatExt>(t, pod, podx, c, hout, seq, pidx, prow, stream);
+        case 0: return score_pod1_f<0>(t, pod, podx, c, hout, gs, seq, pidx, prow, stream);
+        case kFeatExt: return score_pod1_f<kFeatExt>(t, pod, podx, c, hout, gs, seq, pidx, prow, stream);
         default:
-            return score_pod1_f<kFeatExt | kFeatTaint | kFeatAffinity>(t, pod, podx, c, hout, seq, pidx, prow, stream);
+            return score_pod1_f<kFeatExt | kFeatTaint | kFeatAffinity>(t, pod, podx, c, hout, gs, seq, pidx, prow, stream);
     }
 }
 

@@ -416,6 +416,63 @@ __global__ __launch_bounds__(1024) void k_score_pod1(DevTable t, PodT<F> p, DPod
     }
 }
 
+// The same call for the profiles without NormalizeScore (no table-wide maxima to wait for): ONE node
+// per thread, ceil(n / 256) workgroups spread over the XCDs, so a row costs one memory round trip
+// instead of ceil(n / 1024) dependent ones on a single CU.  The workgroup maxima meet in a device word
+// (gs[0], atomic max); the workgroup that arrives last on gs[1] publishes best + done and re-arms both
+// words (the next launch on the stream starts after this one has finished).  Same host layout as
+// k_score_pod1.
+constexpr uint32_t kScorePodGT = 256;
+template <uint32_t F>
+__global__ __launch_bounds__(kScorePodGT) void k_score_podg(DevTable t, PodT<F> p, DPodX px, DevCfg c,
+                                                            uint8_t *hout, uint64_t *gs, uint64_t seq,
+                                                            uint32_t pidx, HostRow prow) {
+    static_assert((F & kFeatNorm) == 0, "NormalizeScore profiles need the table-wide maxima first");
+    constexpr int NW = kScorePodGT / kWave;
+    __shared__ uint64_t redk[NW];
+    const uint32_t n = t.n, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint32_t i = blockIdx.x * kScorePodGT + tid;
+    if (blockIdx.x == 0 && tid == 0 && pidx < n) set_row(t, pidx, prow);
+    uint64_t best = 0;
+    if (i < n) {
+        RowT<F> r;
+        RowX x;
+        if (i == pidx) {
+            host_row_regs<F>(prow, r, x);
+        } else {
+            r = load_row<F>(t, i);
+            x = load_rowx<F>(t, i);
+        }
+        const bool f = feasible<F>(r, x, p, px);
+        uint32_t sco[4];
+        const double y0 = rcp_exact(0u);
+        const uint32_t tot = node_total<F>(r, x, p, px, c, 0u, y0, 0u, y0, sco);
+        best = f ? pack_key(tot + 1, i) : 0ull;
+        reinterpret_cast<int32_t *>(hout + 16)[i] = f ? (int32_t)tot : -1;
+        reinterpret_cast<uint32_t *>(hout + 16 + 4 * (size_t)n)[i] =
+            f ? (sco[0] | (sco[1] << 8) | (sco[2] << 16) | (sco[3] << 24)) : 0u;
+    }
+    best = wave_max_u64(best);
+    if (lane == 0) redk[wv] = best;
+    __threadfence_system();  // this workgroup's host-memory stores before its arrival
+    __syncthreads();
+    if (tid == 0) {
+#pragma unroll
+        for (int q = 0; q < NW; ++q) best = redk[q] > best ? redk[q] : best;
+        __hip_atomic_fetch_max(gs, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t old = __hip_atomic_fetch_add(gs + 1, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (old + 1 == gridDim.x) {  // last arrival: every workgroup's maximum and outputs are in
+            const uint64_t b = __hip_atomic_load(gs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(gs, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(gs + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            *reinterpret_cast<volatile uint64_t *>(hout) = b;
+            __threadfence_system();
+            __hip_atomic_store(reinterpret_cast<uint64_t *>(hout + 8), seq, __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
 // =============================================================================================
 // LOOKAHEAD engine
 // =============================================================================================
@@ -3333,12 +3390,20 @@ static hipError_t scan_pod_f(const DevTable &t, const void *pods_, const DPodX *
 
 template <uint32_t F>
 static hipError_t score_pod1_f(const DevTable &t, const void *pod, const DPodX *podx, const DevCfg &c, uint8_t *hout,
-                               uint64_t seq, uint32_t pidx, const HostRow &prow, hipStream_t stream) {
+                               uint64_t *gs, uint64_t seq, uint32_t pidx, const HostRow &prow, hipStream_t stream) {
     if (t.n > kScorePod1Max) return hipErrorInvalidValue;
     PodT<F> p;
     std::memcpy(&p, pod, sizeof p);
     DPodX px{};
     if ((F & kFeatNorm) && podx) px = *podx;
+    if constexpr ((F & kFeatNorm) == 0) {
+        if (gs && t.n > 0) {
+            const uint32_t g = (t.n + kScorePodGT - 1) / kScorePodGT;
+            hipLaunchKernelGGL((k_score_podg<F>), dim3(g), dim3(kScorePodGT), 0, stream, t, p, px, c, hout, gs, seq,
+                               pidx, prow);
+            return hipGetLastError();
+        }
+    }
     hipLaunchKernelGGL((k_score_pod1<F>), dim3(1), dim3(1024), 0, stream, t, p, px, c, hout, seq, pidx, prow);
     return hipGetLastError();
 }
@@ -3469,7 +3534,7 @@ hipError_t wide_la_window(const DevTable &t, const void *pods, const DPodX *podx
                           hipStream_t stream, int part);
 hipError_t wide_batch_claim_prepare();
 hipError_t wide_score_pod1(const DevTable &t, const void *pod, const DPodX *podx, const DevCfg &c, uint8_t *hout,
-                           uint64_t seq, uint32_t pidx, const HostRow &prow, hipStream_t stream);
+                           uint64_t *gs, uint64_t seq, uint32_t pidx, const HostRow &prow, hipStream_t stream);
 hipError_t wide_batch_claim(const DevTable &t, const void *pods, const uint64_t *lists, uint32_t *ctrl,
                             uint32_t *bidx, uint32_t P, uint32_t B, int32_t *on, uint64_t *ok,
                             size_t lds, hipStream_t stream);

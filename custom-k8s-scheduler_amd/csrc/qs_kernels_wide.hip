@@ -43,9 +43,9 @@ hipError_t wide_la_window(const DevTable &t, const void *pods, const DPodX *podx
 hipError_t wide_batch_claim_prepare() { return batch_claim_prepare_f<kWideFit>(); }
 
 hipError_t wide_score_pod1(const DevTable &t, const void *pod, const DPodX *podx, const DevCfg &c, uint8_t *hout,
-                           uint64_t seq, uint32_t pidx, const HostRow &prow, hipStream_t stream) {
-    if (c.feat & kFeatNorm) return score_pod1_f<kWideNorm>(t, pod, podx, c, hout, seq, pidx, prow, stream);
-    return score_pod1_f<kWideFit>(t, pod, podx, c, hout, seq, pidx, prow, stream);
+                           uint64_t *gs, uint64_t seq, uint32_t pidx, const HostRow &prow, hipStream_t stream) {
+    if (c.feat & kFeatNorm) return score_pod1_f<kWideNorm>(t, pod, podx, c, hout, gs, seq, pidx, prow, stream);
+    return score_pod1_f<kWideFit>(t, pod, podx, c, hout, gs, seq, pidx, prow, stream);
 }
 
 hipError_t wide_batch_claim(const DevTable &t, const void *pods, const uint64_t *lists, uint32_t *ctrl,
