@@ -648,7 +648,7 @@ uint64_t run_batched(qs_ctx *c, qs_stream *s, const void *dp, const DPodX *dx, i
     if (!c->dt.apps) fail(QS_EINVAL, "QS_MODE_BATCHED keeps anti-affinity state for tables up to 2^20 nodes");
     if (c->world > 1 || c->cfg.virtual_shards > 1) fail(QS_EINVAL, "QS_MODE_BATCHED runs unsharded");
     if (batch_claim_lds(n) > 160 * 1024)
-        fail(QS_EINVAL, "QS_MODE_BATCHED claims batches in LDS: tables up to 845,824 nodes");
+        fail(QS_EINVAL, "QS_MODE_BATCHED claims batches in LDS: tables up to 712,672 nodes");
     HIPCHK(batch_claim_prepare());
     const uint32_t B = c->cfg.batch_pods > 0 ? (uint32_t)std::min(64, c->cfg.batch_pods) : 64u;
     LaGeom geo = la_geometry(n, B, 1, 64);

@@ -33,7 +33,7 @@ hipError_t batch_claim_prepare() {
 }
 
 size_t batch_claim_lds(uint32_t n) {
-    return ((((size_t)n + 31) / 32 + 3) & ~(size_t)3) * 4 + kMaxApps * kMaxZones / 8 + 64 * 4 + 64 * 64 * (8 + 4) + 128 * 4;
+    return batch_claim_lds_bytes(n);
 }
 
 hipError_t launch_batch_claim(const DevTable &t, const void *pods, const uint64_t *lists, uint32_t *ctrl,

@@ -506,7 +506,7 @@ __device__ __forceinline__ uint64_t wave_sort_desc(uint64_t v, int lane) {
 }
 
 // Sorts a pod's final list (out[0..L), L <= 64, zero-padded) best-first, so that the top clean
-// entries are its first clean lanes (k_la_resolve_spec).  Every thread of the block calls it.
+// entries come first (the batched claim walks them in order).  Every thread of the block calls it.
 __device__ __forceinline__ void sort_list_desc(uint64_t *__restrict__ out, uint32_t L) {
     __syncthreads();  // the block's stores of out[] are visible to wave 0
     if (threadIdx.x < 64) {
@@ -3117,6 +3117,17 @@ static __device__ uint64_t g_claim_diag[5];
 #define CLAIM_STAMP(q)
 #endif
 constexpr int kClaimWaves = 16;
+constexpr uint32_t kClaimNonEmpty = 1u << 31;  // staged pod flag: the pod's list holds a feasible node
+constexpr uint32_t kClaimCarried = 64, kClaimNone = 65;  // walk outcomes beside a source lane 0..63
+// LDS layout of k_batch_claim (bytes): the fixed-size arrays first, so that every address the walk
+// forms is a lane offset plus a compile-time immediate; the node bitmap (one extra all-ones word
+// that invalid entries point at) last.
+constexpr uint32_t kClLkey = 0, kClLnode = kClLkey + 64 * 64 * 8, kClLazb = kClLnode + 64 * 64 * 4,
+                   kClAz = kClLazb + 64 * 64 * 4, kClPend = kClAz + kMaxApps * kMaxZones / 8, kClSrc = kClPend + 256,
+                   kClPod = kClSrc + 256, kClNodes = kClPod + 512;
+__host__ __device__ constexpr size_t batch_claim_lds_bytes(uint32_t n) {
+    return kClNodes + (((size_t)n + 31) / 32 + 1 + 3) / 4 * 16;
+}
 
 template <uint32_t F>
 __global__ __launch_bounds__(64 * kClaimWaves) void k_batch_claim(
@@ -3126,19 +3137,24 @@ __global__ __launch_bounds__(64 * kClaimWaves) void k_batch_claim(
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     CLAIM_STAMP0();
-    const uint32_t nwords = (t.n + 31) / 32;
-    uint32_t *claimed = lds;                                   // node bitmap
-    uint32_t *claimed_az = lds + ((nwords + 3) & ~3u);         // (app, zone) bitmap
-    uint32_t *pend = claimed_az + kMaxApps * kMaxZones / 32;   // carried pods (<= 64)
-    uint64_t *lkey = (uint64_t *)(pend + 64);                  // [64 pods][64] keys, best first
-    uint32_t *lzone = (uint32_t *)(lkey + 64 * 64);            // [64 pods][64] their zones
-    uint32_t *lpod = lzone + 64 * 64;                          // [64] stream positions, [64] flags
+    const uint32_t nwords = (t.n + 31) / 32, sent = nwords * 32;  // sent: the all-ones bitmap word
+    uint8_t *lb = reinterpret_cast<uint8_t *>(lds);
+    uint64_t *lkey = reinterpret_cast<uint64_t *>(lb + kClLkey);  // [64 pods][64] keys, best first
+    uint32_t *lnode = reinterpret_cast<uint32_t *>(lb + kClLnode);  // their nodes (sent: no entry)
+    uint32_t *lazb = reinterpret_cast<uint32_t *>(lb + kClLazb);    // app * kMaxZones + zone
+    uint32_t *claimed_az = reinterpret_cast<uint32_t *>(lb + kClAz);  // (app, zone) bitmap
+    uint32_t *pend = reinterpret_cast<uint32_t *>(lb + kClPend);    // carried pods (<= 64)
+    uint32_t *rsrc = reinterpret_cast<uint32_t *>(lb + kClSrc);     // [64] walk outcomes
+    uint32_t *lpod = reinterpret_cast<uint32_t *>(lb + kClPod);     // [64] stream positions, [64] flags
+    uint32_t *claimed = reinterpret_cast<uint32_t *>(lb + kClNodes);  // node bitmap
     const uint32_t nb = ctrl[0], cursor = ctrl[1];
     for (uint32_t i = tid; i < nwords; i += 64 * kClaimWaves) claimed[i] = 0;
+    if (tid == 0) claimed[nwords] = 0xFFFFFFFFu;
     for (uint32_t i = tid; i < kMaxApps * kMaxZones / 32; i += 64 * kClaimWaves) claimed_az[i] = 0;
     // Staging, all waves: each pod's list, sorted best-first by the merge (so that a pod's claim is
-    // the first still-available lane), and, for zone-anti-affinity pods, the zones of its candidates.
-    // Wave wv takes pods wv + 16q (q < 4): all loads of a round are issued before any is used.
+    // the first still-available lane) as keys, nodes and, for zone-anti-affinity pods, the (app, zone)
+    // bit of every candidate.  Wave wv takes pods wv + 16q (q < 4, all 64 rows written: rows past the
+    // batch hold no entry): all loads of a round are issued before any is used.
     {
         constexpr int Q = 64 / kClaimWaves;
         uint64_t ev[Q];
@@ -3155,7 +3171,6 @@ __global__ __launch_bounds__(64 * kClaimWaves) void k_batch_claim(
             sv[q] = fv[q];
             fv[q] = (uint32_t)wv + kClaimWaves * q < nb ? pods[sv[q]].flags : 0u;
         }
-        // (the lists arrive sorted best-first: k_la_merge / a single-chunk k_la_select sort them)
         uint32_t zv[Q];
 #pragma unroll
         for (int q = 0; q < Q; ++q)
@@ -3163,86 +3178,77 @@ __global__ __launch_bounds__(64 * kClaimWaves) void k_batch_claim(
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
             const uint32_t i = (uint32_t)wv + kClaimWaves * q;
-            if (i < nb) {
-                lkey[i * 64 + lane] = ev[q];
-                lzone[i * 64 + lane] = zv[q];
-                if (lane == 0) { lpod[i] = sv[q]; lpod[64 + i] = fv[q]; }
-            }
+            const bool ok = ev[q] != 0ull;
+            lkey[i * 64 + lane] = ev[q];
+            lnode[i * 64 + lane] = ok ? key_node(ev[q]) : sent;
+            lazb[i * 64 + lane] = pod_app(fv[q]) * kMaxZones + (zv[q] & (kMaxZones - 1));
+            const uint32_t ne = __ballot(ok) ? kClaimNonEmpty : 0u;
+            if (lane == 0) { lpod[i] = sv[q]; lpod[64 + i] = fv[q] | ne; }
         }
     }
     __syncthreads();
     if (wv != 0) return;
     CLAIM_STAMP(0);  // the claim walk and the apply step are one wave's work
-    int32_t my_node = -2;  // lane i: batch pod i's outcome (-2 carried, -1 unschedulable)
-    uint64_t my_key = 0;
     uint32_t npend = 0;
     // lane i holds batch pod i's stream position and flags (read with readlane in the walk)
     const uint32_t my_s = (uint32_t)lane < nb ? lpod[lane] : 0u;
-    const uint32_t my_flags = (uint32_t)lane < nb ? lpod[64 + lane] : 0u;
+    const uint32_t my_flags = lpod[64 + lane];
     CLAIM_STAMP(1);
-    // Software-pipelined walk.  Entering step i: pod i's entries (its register set) and its exact
-    // availability mask am (claims of pods < i), pod i+1's entries (the next set).  Pod i+1's bitmap
-    // words are read before pod i's claim is written (they see the claims of pods < i) and then
-    // patched with pod i's claim (node w; (app, zone) when both are zone-anti-affinity pods), so
-    // the LDS round trip overlaps pod i's scalar chain instead of following it.  Three entry
-    // register sets rotate over an unrolled-by-3 loop: pod i+2's entries load straight into the
-    // set pod i+1 will not need again (a copy at the back-edge would wait for that load).
-    auto lane_node = [](uint64_t v, bool ok) { return (ok && v) ? key_node(v) : 0u; };
+    // Software-pipelined walk, one pod per step.  Entering step i: pod i's entries (node, (app, zone)
+    // per lane) and its exact availability mask am (claims of pods < i), pod i+1's entries.  Pod
+    // i+1's bitmap words are read before pod i's claim is written (they see the claims of pods < i)
+    // and then patched with pod i's claim, so the LDS round trip overlaps pod i's scalar chain.
+    // Invalid entries point at the all-ones word (always taken); a step records only pod i's source
+    // lane (or carried / none), the keys are gathered after the walk.  Three entry register sets
+    // rotate over an unrolled-by-3 loop (a copy at the back-edge would wait for the next load).
     struct Ents {
-        uint64_t e;
-        uint32_t z;
+        uint32_t node, azb;
     };
     auto ents = [&](uint32_t j) -> Ents {
-        const uint32_t jj = min(j, 63u);
-        return Ents{lkey[jj * 64 + lane], lzone[jj * 64 + lane] & (kMaxZones - 1)};
+        const uint32_t o = min(j, 63u) * 64 + (uint32_t)lane;
+        return Ents{lnode[o], lazb[o]};
     };
-    Ents sa = ents(0), sb = ents(1), sc{0ull, 0u};
+    Ents sa = ents(0), sb = ents(1), sc{sent, 0u};
     uint32_t fl = (uint32_t)__builtin_amdgcn_readlane((int)my_flags, 0);
     uint64_t am;
     {
-        const uint32_t node = lane_node(sa.e, true), azb = pod_app(fl) * kMaxZones + sa.z;
-        const uint32_t taken = ((claimed[node >> 5] >> (node & 31)) |
-                                (pod_aa(fl) == 2u ? claimed_az[azb >> 5] >> (azb & 31) : 0u)) & 1u;
-        am = __ballot(sa.e != 0ull && taken == 0u);
+        uint32_t tk = (claimed[sa.node >> 5] >> (sa.node & 31)) & 1u;
+        am = __ballot(tk == 0u);  // no claims yet: only the invalid entries are taken
     }
     auto step = [&](uint32_t i, const Ents &cur, const Ents &nxt, Ents &n2) {
-        const uint64_t e = cur.e, e1 = nxt.e;
-        const uint32_t z = cur.z, z1 = nxt.z;
-        const uint32_t aa = pod_aa(fl), app = pod_app(fl);
-        const bool has1 = i + 1 < nb;
         const uint32_t fl1 = (uint32_t)__builtin_amdgcn_readlane((int)my_flags, (int)min(i + 1, 63u));
-        const uint32_t aa1 = pod_aa(fl1), app1 = pod_app(fl1);
+        const bool aa = pod_aa(fl) == 2u, aa1 = pod_aa(fl1) == 2u;
         // pod i+1: bitmap words (claims of pods < i) and pod i+2's entries, all in flight now
-        const uint32_t node1 = lane_node(e1, has1), azb1 = app1 * kMaxZones + z1;
-        const uint32_t cw1 = claimed[node1 >> 5], aw1 = claimed_az[azb1 >> 5];
+        const uint32_t cw1 = claimed[nxt.node >> 5];
+        const uint32_t aw1 = aa1 ? claimed_az[nxt.azb >> 5] : 0u;
         n2 = ents(i + 2);
         // pod i
-        uint32_t w = 0xFFFFFFFFu, zw = 0xFFFFFFFFu;
+        uint32_t w = 0xFFFFFFFFu, bw = 0xFFFFFFFFu;
         if (am) {
             const int src = __builtin_ctzll(am);
-            const uint64_t best = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(e >> 32), src) << 32) |
-                                  (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)e, src);
-            w = key_node(best);
-            zw = (uint32_t)__builtin_amdgcn_readlane((int)z, src);
-            const uint32_t b2 = app * kMaxZones + zw;
+            w = (uint32_t)__builtin_amdgcn_readlane((int)cur.node, src);
+            if (aa) bw = (uint32_t)__builtin_amdgcn_readlane((int)cur.azb, src);
             if (lane == 0) {
                 __hip_atomic_fetch_or(&claimed[w >> 5], 1u << (w & 31), __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (aa == 2u)
-                    __hip_atomic_fetch_or(&claimed_az[b2 >> 5], 1u << (b2 & 31), __ATOMIC_RELAXED,
+                if (aa)
+                    __hip_atomic_fetch_or(&claimed_az[bw >> 5], 1u << (bw & 31), __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+                rsrc[i] = (uint32_t)src;
             }
-            if ((uint32_t)lane == i) { my_node = (int32_t)w; my_key = best; }
-        } else if (__ballot(e != 0ull)) {
-            if (lane == 0) pend[npend] = (uint32_t)__builtin_amdgcn_readlane((int)my_s, (int)i);
-            ++npend;  // every candidate taken by an earlier pod: carried to the next batch
-        } else if ((uint32_t)lane == i) {
-            my_node = -1;  // no feasible node at all (spec S7: unschedulable)
+        } else if (fl & kClaimNonEmpty) {  // every candidate taken by an earlier pod: carried
+            if (lane == 0) {
+                pend[npend] = (uint32_t)__builtin_amdgcn_readlane((int)my_s, (int)i);
+                rsrc[i] = kClaimCarried;
+            }
+            ++npend;
+        } else if (lane == 0) {
+            rsrc[i] = kClaimNone;  // no feasible node at all (spec S7: unschedulable)
         }
         // pod i+1's exact mask: bitmap words patched with pod i's claim
-        const bool az_hit = aa1 == 2u && aa == 2u && app1 == app && z1 == zw;
-        const uint32_t taken1 = ((cw1 >> (node1 & 31)) | (aa1 == 2u ? aw1 >> (azb1 & 31) : 0u)) & 1u;
-        am = __ballot(has1 && e1 != 0ull && taken1 == 0u && node1 != w && !az_hit);
+        uint32_t tk = (cw1 >> (nxt.node & 31)) & 1u;
+        if (aa1) tk |= ((aw1 >> (nxt.azb & 31)) & 1u) | ((aa && nxt.azb == bw) ? 1u : 0u);
+        am = __ballot(tk == 0u && nxt.node != w);
         fl = fl1;
     };
     uint32_t i = 0;
@@ -3254,6 +3260,18 @@ __global__ __launch_bounds__(64 * kClaimWaves) void k_batch_claim(
     if (i < nb) step(i, sa, sb, sc);
     if (i + 1 < nb) step(i + 1, sb, sc, sa);
     CLAIM_STAMP(2);
+    // lane i: batch pod i's outcome (-2 carried, -1 unschedulable) and its key
+    int32_t my_node = -2;
+    uint64_t my_key = 0;
+    if ((uint32_t)lane < nb) {
+        const uint32_t r = rsrc[lane];
+        if (r < 64u) {
+            my_key = lkey[(uint32_t)lane * 64 + r];
+            my_node = (int32_t)key_node(my_key);
+        } else {
+            my_node = r == kClaimCarried ? -2 : -1;
+        }
+    }
     // apply every claim (distinct nodes; counts of one (app, zone) may be shared: atomics)
     if ((uint32_t)lane < nb && my_node != -2) {
         const uint32_t s = my_s;
