@@ -2643,7 +2643,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
         }
     } else if (wv == 3) {
         // ---- C: candidate rows, C keys, the next pod's best clean entry; next-window prefetch -----
-        uint64_t eX = 0, eY = 0, c1 = 0;
+        uint64_t eX = 0, eY = 0, eZ = 0, c1 = 0;
         // NORM: the statics of pod i's entries (this lane's) against pods i+1 and i+2, published by
         // the selectors with the lists; two register pairs by pod parity, each loaded two pods ahead
         // in place (a pair is reloaded right after its pod's step used it)
@@ -2726,7 +2726,10 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
             const bool pfw = hasnext && kend >= 6;  // prefetch the next window during this one
             PodT<F> pcur = wp[0];  // pod i's record (pod i+1's is read each step)
             // HOOK: the step may carry the next-window prefetch (only the last steps of a window)
-            auto step = [&](auto hook, uint32_t i, uint64_t &en, uint32_t &c1s1, uint32_t &c1s2) {
+            // LM (entry loads): 0 pod i+3's entry into en; 1 pods i+3 and i+4 (into en and eZ); 2 none,
+            // en takes eZ.  The plain pairs use 1 then 2, so no entry load is in flight at the loop's
+            // back-edge (the compiler waits for every load in flight there, vmcnt(0)).
+            auto step = [&](auto hook, auto lm, uint32_t i, uint64_t &en, uint32_t &c1s1, uint32_t &c1s2) {
                 QS_RSTAMP_BEGIN()
                 const int par = i & 1;
                 // the step's LDS reads first, together: the dirty word of pod i+1's entry (the set
@@ -2781,7 +2784,12 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                     C1[par][lane] = c1;
                     r1 = load_row<F>(t, c1 ? key_node(c1) : 0u);
                     x1 = load_rowx<F>(t, c1 ? key_node(c1) : 0u);
-                    en = ent(lists, i + 3, kend);
+                    if constexpr (decltype(lm)::value == 2) {
+                        en = eZ;
+                    } else {
+                        en = ent(lists, i + 3, kend);
+                        if constexpr (decltype(lm)::value == 1) eZ = ent(lists, i + 4, kend);
+                    }
                 } else if (pref) {
                     // last pod: the next window's first candidate rows (its entries arrived meanwhile;
                     // a node dirtied from here on is masked out at the boundary)
@@ -2817,17 +2825,20 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
             };
             const std::integral_constant<bool, false> plain{};
             const std::integral_constant<bool, true> hooked{};
+            const std::integral_constant<int, 0> l1{};
+            const std::integral_constant<int, 1> l2{};
+            const std::integral_constant<int, 2> l0{};
             const uint32_t ih = pfw ? ((kend - 5) & ~1u) : kend;  // first step with the hooks (even)
             uint32_t i = 0;
             for (; i + 1 < ih; i += 2) {
-                step(plain, i, eX, sA1, sA2);
-                step(plain, i + 1, eY, sB1, sB2);
+                step(plain, l2, i, eX, sA1, sA2);
+                step(plain, l0, i + 1, eY, sB1, sB2);
             }
             for (; i + 1 < kend; i += 2) {
-                step(hooked, i, eX, sA1, sA2);
-                step(hooked, i + 1, eY, sB1, sB2);
+                step(hooked, l1, i, eX, sA1, sA2);
+                step(hooked, l1, i + 1, eY, sB1, sB2);
             }
-            if (i < kend) step(hooked, i, eX, sA1, sA2);
+            if (i < kend) step(hooked, l1, i, eX, sA1, sA2);
             if (NORM && pref && (kend & 1)) {  // the next window's pods 0 / 1 went to the B / A pairs
                 const uint32_t t1 = sA1, t2 = sA2;
                 sA1 = sB1; sA2 = sB2;

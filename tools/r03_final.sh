@@ -7,6 +7,6 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 TESTS=tests SMOKE=1 TEST_TIMEOUT=1000 bash tools/r03_check.sh || exit 1
 bash tools/profile_fetch.sh ${TAG:-r03} || exit 2
-for o in 1 0; do timeout -k 10 60 custom-k8s-scheduler_amd/fw_latency 5000 2000 $o >> gpurun_out/fw_final.log 2>&1 || exit 3; done
+for o in 1 0; do timeout -k 10 60 custom-k8s-scheduler_amd/fw_latency 5000 5000 $o >> gpurun_out/fw_final.log 2>&1 || exit 3; done
 cat gpurun_out/fw_final.log
 echo FINALDONE
