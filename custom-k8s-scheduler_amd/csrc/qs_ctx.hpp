@@ -130,7 +130,7 @@ struct qs_ctx {
     void *pin = nullptr;   // qs_score_pod's packed outputs, written by the kernel (pinned host memory)
     size_t pin_bytes = 0;
     uint64_t score_seq = 0;  // the kernel's done word for the call in flight
-    qs_host::DevBuf score_gs;  // the multi-workgroup score launch's {maximum, arrivals} (zero between launches)
+    qs_host::DevBuf score_gs;  // the multi-workgroup score launch's {best, arrivals, taint max, affinity max} (zero between calls)
     uint32_t pend = 0xFFFFFFFFu;  // a qs_reserve / qs_unreserve row not yet written to the device:
                                   // the next qs_score_pod writes it, every other call first flushes it
     qs_host::DevBuf hand;  // window hand-off words: {unused, ready, timeout flag} (u64 each)

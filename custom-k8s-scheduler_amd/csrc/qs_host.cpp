@@ -1000,8 +1000,8 @@ qs_status qs_score_pod(qs_ctx *c, const qs_pod *pod, uint8_t *feas, int32_t *sco
                 std::memset(c->pin, 0, pb);
             }
             if (!c->score_gs.p) {
-                c->score_gs.ensure(16);
-                HIPCHK(hipMemsetAsync(c->score_gs.p, 0, 16, c->stream));
+                c->score_gs.ensure(32);
+                HIPCHK(hipMemsetAsync(c->score_gs.p, 0, 32, c->stream));
             }
             const uint32_t pidx = c->pend < n ? c->pend : 0xFFFFFFFFu;
             const HostRow prow = pidx < n ? compact_row(c->m, pidx, c->shift, c->wide) : HostRow{};

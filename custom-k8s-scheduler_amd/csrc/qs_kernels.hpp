@@ -416,23 +416,55 @@ __global__ __launch_bounds__(1024) void k_score_pod1(DevTable t, PodT<F> p, DPod
     }
 }
 
-// The same call for the profiles without NormalizeScore (no table-wide maxima to wait for): ONE node
-// per thread, ceil(n / 256) workgroups spread over the XCDs, so a row costs one memory round trip
-// instead of ceil(n / 1024) dependent ones on a single CU.  The workgroup maxima meet in a device word
-// (gs[0], atomic max); the workgroup that arrives last on gs[1] publishes best + done and re-arms both
-// words (the next launch on the stream starts after this one has finished).  Same host layout as
-// k_score_pod1.
+// The same call as ONE node per thread, ceil(n / 256) workgroups spread over the XCDs, so a row
+// costs one memory round trip instead of ceil(n / 1024) dependent ones on a single CU.  The workgroup
+// maxima meet in a device word (gs[0], atomic max); the workgroup that arrives last on gs[1]
+// publishes best + done and re-arms the words (the next launch on the stream starts after this one
+// has finished).  Same host layout as k_score_pod1.  NormalizeScore profiles first run
+// k_score_podg_max (same grid: the feasible nodes' taint / affinity raw maxima into gs[2] / gs[3]);
+// the kernel boundary makes them visible to every workgroup here.
 constexpr uint32_t kScorePodGT = 256;
+template <uint32_t F>
+__global__ __launch_bounds__(kScorePodGT) void k_score_podg_max(DevTable t, PodT<F> p, DPodX px, uint64_t *gs,
+                                                                uint32_t pidx, HostRow prow) {
+    static_assert((F & kFeatNorm) != 0, "maxima of the normalizing plugins only");
+    const uint32_t n = t.n, i = blockIdx.x * kScorePodGT + threadIdx.x;
+    uint32_t mt = 0, ma = 0;
+    if (i < n) {
+        RowT<F> r;
+        RowX x;
+        if (i == pidx) {
+            host_row_regs<F>(prow, r, x);
+        } else {
+            r = load_row<F>(t, i);
+            x = load_rowx<F>(t, i);
+        }
+        if (feasible<F>(r, x, p, px)) {
+            mt = taint_raw(x, px);
+            ma = affinity_raw(x, p, px);
+        }
+    }
+    mt = wave_max_u32(mt);
+    ma = wave_max_u32(ma);
+    if ((threadIdx.x & 63) == 0) {  // one atomic per wave (words stay zero between calls)
+        if (mt) __hip_atomic_fetch_max(gs + 2, (uint64_t)mt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (ma) __hip_atomic_fetch_max(gs + 3, (uint64_t)ma, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
 template <uint32_t F>
 __global__ __launch_bounds__(kScorePodGT) void k_score_podg(DevTable t, PodT<F> p, DPodX px, DevCfg c,
                                                             uint8_t *hout, uint64_t *gs, uint64_t seq,
                                                             uint32_t pidx, HostRow prow) {
-    static_assert((F & kFeatNorm) == 0, "NormalizeScore profiles need the table-wide maxima first");
     constexpr int NW = kScorePodGT / kWave;
     __shared__ uint64_t redk[NW];
     const uint32_t n = t.n, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t i = blockIdx.x * kScorePodGT + tid;
     if (blockIdx.x == 0 && tid == 0 && pidx < n) set_row(t, pidx, prow);
+    uint32_t mt = 0, ma = 0;
+    if constexpr ((F & kFeatNorm) != 0) {  // k_score_podg_max's maxima (the previous launch)
+        mt = (uint32_t)__hip_atomic_load(gs + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ma = (uint32_t)__hip_atomic_load(gs + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     uint64_t best = 0;
     if (i < n) {
         RowT<F> r;
@@ -445,8 +477,7 @@ __global__ __launch_bounds__(kScorePodGT) void k_score_podg(DevTable t, PodT<F> 
         }
         const bool f = feasible<F>(r, x, p, px);
         uint32_t sco[4];
-        const double y0 = rcp_exact(0u);
-        const uint32_t tot = node_total<F>(r, x, p, px, c, 0u, y0, 0u, y0, sco);
+        const uint32_t tot = node_total<F>(r, x, p, px, c, mt, rcp_exact(mt), ma, rcp_exact(ma), sco);
         best = f ? pack_key(tot + 1, i) : 0ull;
         reinterpret_cast<int32_t *>(hout + 16)[i] = f ? (int32_t)tot : -1;
         reinterpret_cast<uint32_t *>(hout + 16 + 4 * (size_t)n)[i] =
@@ -465,6 +496,10 @@ __global__ __launch_bounds__(kScorePodGT) void k_score_podg(DevTable t, PodT<F> 
             const uint64_t b = __hip_atomic_load(gs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(gs, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(gs + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if constexpr ((F & kFeatNorm) != 0) {  // every workgroup read them before arriving
+                __hip_atomic_store(gs + 2, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(gs + 3, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
             *reinterpret_cast<volatile uint64_t *>(hout) = b;
             __threadfence_system();
             __hip_atomic_store(reinterpret_cast<uint64_t *>(hout + 8), seq, __ATOMIC_RELEASE,
@@ -3425,13 +3460,14 @@ static hipError_t score_pod1_f(const DevTable &t, const void *pod, const DPodX *
     std::memcpy(&p, pod, sizeof p);
     DPodX px{};
     if ((F & kFeatNorm) && podx) px = *podx;
-    if constexpr ((F & kFeatNorm) == 0) {
-        if (gs && t.n > 0) {
-            const uint32_t g = (t.n + kScorePodGT - 1) / kScorePodGT;
-            hipLaunchKernelGGL((k_score_podg<F>), dim3(g), dim3(kScorePodGT), 0, stream, t, p, px, c, hout, gs, seq,
-                               pidx, prow);
-            return hipGetLastError();
-        }
+    if (gs && t.n > 0) {
+        const uint32_t g = (t.n + kScorePodGT - 1) / kScorePodGT;
+        if constexpr ((F & kFeatNorm) != 0)
+            hipLaunchKernelGGL((k_score_podg_max<F>), dim3(g), dim3(kScorePodGT), 0, stream, t, p, px, gs, pidx,
+                               prow);
+        hipLaunchKernelGGL((k_score_podg<F>), dim3(g), dim3(kScorePodGT), 0, stream, t, p, px, c, hout, gs, seq,
+                           pidx, prow);
+        return hipGetLastError();
     }
     hipLaunchKernelGGL((k_score_pod1<F>), dim3(1), dim3(1024), 0, stream, t, p, px, c, hout, seq, pidx, prow);
     return hipGetLastError();

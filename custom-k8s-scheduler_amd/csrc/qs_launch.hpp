@@ -54,8 +54,8 @@ hipError_t launch_rows_to_soa(const DevTable &t, hipStream_t stream);
 // qs_score_pod in ONE launch for tables up to score_pod1_max_nodes(): pod record (DPod / DPodW) and
 // extension by value; outputs written into pinned host memory hout (score_pod1_pack_bytes(n) bytes:
 // [best u64 | done u64 | total i32 x n (-1 infeasible) | scores u8 x 4n]), done = seq stored last;
-// pidx < n: the pending row prow is written to the table first (and scored as such).  gs: two zeroed
-// device u64 (the multi-workgroup form's maximum and arrival count; left zeroed by every launch).
+// pidx < n: the pending row prow is written to the table first (and scored as such).  gs: four zeroed
+// device u64 (the multi-workgroup form's best key, arrival count and normalize maxima; left zeroed).
 uint32_t score_pod1_max_nodes();
 size_t score_pod1_pack_bytes(uint32_t n);
 hipError_t launch_score_pod1(const DevTable &t, const void *pod, const DPodX *podx, const DevCfg &c, uint8_t *hout,

@@ -203,20 +203,29 @@ class Scheduler:
         self._chk(self.lib.qs_unreserve(self.ctx, node, _ptr(p)))
 
     # ---- one pod, all nodes ----
-    def score_pod(self, pod, outputs=True):
+    def score_pod(self, pod, outputs=True, out=None):
         """qs_score_pod: {"best"} and, with outputs, the per-node "feasible" / "scores" / "total"
-        arrays (fresh copies).  outputs=False asks the library for the best node only."""
+        arrays (fresh copies, or the caller's reusable buffers from score_buffers() passed as
+        `out`, filled in place).  outputs=False asks the library for the best node only."""
         p = np.array([pod], POD_DTYPE) if isinstance(pod, np.void) else pods_to_struct(pod)[:1]
         best = ctypes.c_int32(-2)
         if not outputs:
             self._chk(self.lib.qs_score_pod(self.ctx, _ptr(p), None, None, None, ctypes.byref(best)))
             return dict(best=best.value)
-        feas = np.zeros(self.n, np.uint8)
-        score = np.zeros((self.n, 4), np.int32)
-        total = np.zeros(self.n, np.int32)
+        if out is None:
+            out = self.score_buffers()
+        feas, score, total = out["feasible"], out["scores"], out["total"]
+        if len(total) != self.n or score.shape != (self.n, 4) or feas.dtype != np.bool_:
+            raise ValueError("score_pod: out buffers do not match the node table (use score_buffers())")
         self._chk(self.lib.qs_score_pod(self.ctx, _ptr(p), _ptr(feas), _ptr(score), _ptr(total),
                                         ctypes.byref(best)))
-        return dict(feasible=feas.astype(bool), scores=score, total=total, best=best.value)
+        return dict(feasible=feas, scores=score, total=total, best=best.value)
+
+    def score_buffers(self):
+        """Output arrays for score_pod(..., out=...) sized to the current table (feasible is a bool
+        array the library fills with 0 / 1 bytes)."""
+        return dict(feasible=np.zeros(self.n, np.bool_), scores=np.zeros((self.n, 4), np.int32),
+                    total=np.zeros(self.n, np.int32))
 
     # ---- exact stream ----
     def schedule(self, pods, with_stats=False, mode="exact"):

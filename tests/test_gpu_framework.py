@@ -46,6 +46,34 @@ def test_score_pod_parity(layout, config, n):
             np.testing.assert_array_equal(got["scores"][feas], sc[feas])
 
 
+@pytest.mark.parametrize("n", [1, 255, 257, 4096, 16384])
+def test_score_pod_grid_edges_reused_buffers(n):
+    """The multi-workgroup score launch (one node per thread, ceil(n/256) workgroups, the last
+    arrival publishing best + done) at workgroup-count edges up to the one-launch limit, with the
+    outputs unpacked 16 nodes at a time (tails 1, 15, 1, 0, 0) into caller buffers reused across
+    calls and Reserves; every call diffed against the oracle and against a fresh-buffer call."""
+    from oracle import oracle as O
+    nodes, pods = synth_generate(2, n, 12)
+    with Scheduler({}) as s:
+        s.load_nodes(nodes)
+        ref = {k: v.copy() for k, v in nodes.items()}
+        op = pods_from_struct(pods)
+        bufs = s.score_buffers()
+        for j in range(6):
+            got = s.score_pod(pods[j], out=bufs)
+            assert got["total"] is bufs["total"]
+            fresh = s.score_pod(pods[j])
+            feas, sc, total, best = oracle_scores(ref, pods, j)
+            for g in (got, fresh):
+                assert np.array_equal(g["feasible"], feas)
+                assert np.array_equal(g["total"], total)
+                assert g["best"] == best
+                np.testing.assert_array_equal(g["scores"][feas], sc[feas])
+            if best >= 0:
+                s.reserve(best, pods[j])
+                O.lib().or_reserve(O.ctypes.byref(O._mk_nodes(ref)), O.ctypes.byref(O._mk_pods(op)), j, best, 1)
+
+
 @pytest.mark.parametrize("layout", LAYOUTS)
 def test_reserve_unreserve_roundtrip(layout):
     """Reserve changes the next pod's scores exactly like the oracle's Reserve; Unreserve restores."""
