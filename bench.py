@@ -71,6 +71,9 @@ def parse(argv=None):
                     help="skip the end-to-end, framework-path and wide-layout legs")
     ap.add_argument("--transport", default="mailbox", choices=["mailbox", "rccl"],
                     help="sharded exchange (N > 1): peer-memory mailbox over xGMI, or RCCL all-gather")
+    ap.add_argument("--leg", default=None, choices=["wide", "config3", "config4", "config5", "framework"],
+                    help="run only this sub-leg on one GPU and print its JSON object (iteration probe, "
+                         "not the bench line)")
     ap.add_argument("--dry-run", action="store_true",
                     help="print the launch plan (torchrun argv for --gpus N > 1) and exit, no GPU touched")
     return ap.parse_args(argv)
@@ -157,44 +160,96 @@ class Ctx:
 TRANSPORT = {"name": "mailbox"}  # sharded exchange: peer-memory mailbox (default) or RCCL
 
 
+class PeerFailed(RuntimeError):
+    """Another rank failed a phase this rank completed (raised on every rank at the same point)."""
+
+
+def agree(cx, err):
+    """Fixed collective point: every rank learns whether all ranks completed the phase; a local
+    error is re-raised, a peer's surfaces as PeerFailed, on every rank after the same all-reduce
+    (a rank that fails must not leave its peers blocked in a different collective)."""
+    if cx.min(0.0 if err is not None else 1.0) > 0:
+        return
+    raise err if err is not None else PeerFailed("failed on another rank")
+
+
 def open_sched(cx, cfg, sharded):
     """Sharded runs use the peer-memory mailbox (every rank exports its mailbox handle, the handles
-    are all-gathered over the process group) or, with --transport rccl, an RCCL communicator."""
+    are all-gathered over the process group) or, with --transport rccl, an RCCL communicator.  The
+    mailbox path runs the same collectives on every rank whatever fails locally."""
     if not sharded:
         return qsched.Scheduler(cfg, device=cx.local)
     if TRANSPORT["name"] == "rccl":
         return qsched.Scheduler(cfg, device=cx.local, shard=cx.shard())
-    s = qsched.Scheduler(cfg, device=cx.local, shard=(cx.rank, cx.world, None))
-    h = s.mailbox_export()
+    s = h = err = None
+    try:
+        s = qsched.Scheduler(cfg, device=cx.local, shard=(cx.rank, cx.world, None))
+        h = s.mailbox_export()
+    except Exception as e:
+        err = e
     allh = [None] * cx.world
     cx.dist.all_gather_object(allh, h)
-    s.mailbox_connect(allh)
+    if err is None and all(x is not None for x in allh):
+        try:
+            s.mailbox_connect(allh)
+        except Exception as e:
+            err = e
+    try:
+        agree(cx, err)
+    except Exception:
+        if s is not None:
+            s.close()
+        raise
     return s
+
+
+def run_phase(cx, fn):
+    """Local work of one phase, then the agreement point; returns fn's value."""
+    out, err = None, None
+    try:
+        out = fn()
+    except Exception as e:
+        err = e
+    agree(cx, err)
+    return out
+
+
+def load_prepare(s, nodes, pods):
+    s.load_nodes(nodes)
+    return s.prepare(pods)
 
 
 def diag_runs(cx, nodes, pods, cfg, sharded):
     """Untimed diagnostic runs: per-pod device timestamps (p50/p99 decision interval) and per-kernel
     HIP-event times on the library's own stream (config.profile_kernels)."""
-    p50 = p99 = None
     s2 = open_sched(cx, dict(cfg, record_timestamps=1), sharded)
-    s2.load_nodes(nodes)
-    st2 = s2.prepare(pods)
-    cx.barrier()  # every rank's first window within the exchange's wait bound (ADVICE r2)
-    st2.run()
-    d = np.diff(st2.stamps().astype(np.int64)) * 0.01  # 100 MHz s_memrealtime ticks -> us
-    p50, p99 = float(np.percentile(d, 50)), float(np.percentile(d, 99))
-    st2.free()
-    s2.close()
+    try:
+        st2 = run_phase(cx, lambda: load_prepare(s2, nodes, pods))
+        cx.barrier()  # every rank's first window within the exchange's wait bound (ADVICE r2)
+
+        def stamps():
+            st2.run()
+            d = np.diff(st2.stamps().astype(np.int64)) * 0.01  # 100 MHz s_memrealtime ticks -> us
+            st2.free()
+            return float(np.percentile(d, 50)), float(np.percentile(d, 99))
+        p50, p99 = run_phase(cx, stamps)
+    finally:
+        s2.close()
     s3 = open_sched(cx, dict(cfg, profile_kernels=1), sharded)
-    s3.load_nodes(nodes)
-    st3 = s3.prepare(pods)
-    cx.barrier()
-    r3 = st3.run()
-    kp = r3["kernels"]
-    if r3.get("resident") and "resolve" in kp:  # one resident launch (DESIGN.md §4.1c)
-        kp = {"stream": kp["resolve"]}
-    st3.free()
-    s3.close()
+    try:
+        st3 = run_phase(cx, lambda: load_prepare(s3, nodes, pods))
+        cx.barrier()
+
+        def prof():
+            r3 = st3.run()
+            kp = r3["kernels"]
+            if r3.get("resident") and "resolve" in kp:  # one resident launch (DESIGN.md §4.1c)
+                kp = {"stream": kp["resolve"]}
+            st3.free()
+            return kp
+        kp = run_phase(cx, prof)
+    finally:
+        s3.close()
     return p50, p99, kp
 
 
@@ -274,19 +329,24 @@ def cpu_baseline(nodes, pods, n_nodes, n_pods, sample, threads=1, gpu_placement=
 
 
 def measure(cx, a, workload, steps, warmup, with_diag=True):
-    """Timed exact stream of `workload`; returns a dict of measurements (rank-0 meaningful)."""
+    """Timed exact stream of `workload`; returns a dict of measurements (rank-0 meaningful).  Every
+    rank runs the same collectives in the same order whatever fails locally: open (open_sched's
+    agreement), load + prepare (agreement), the steps (a failed step skips the rest; barriers and an
+    agreement after the loop), results (agreement)."""
     gen, n_nodes, n_pods, desc = WORKLOADS[workload]
     sharded = workload == "config3" and cx.world > 1
     seed = 0x5EED0000 + gen + (cx.rank if (cx.world > 1 and not sharded) else 0)
     nodes, pods = qsched.synth_generate(gen, n_nodes, n_pods, seed=seed)
     cfg = dict({"engine": a.engine, "lookahead": a.lookahead}, **PROFILE.get(workload, {}))
+    mode = MODE.get(workload, "exact")
     s = open_sched(cx, cfg, sharded)
     try:
-        s.load_nodes(nodes)
-        st = s.prepare(pods)  # (may re-lay the table out for the pods' quantities: snapshot after)
-        s.save_table()
-
-        mode = MODE.get(workload, "exact")
+        def setup():
+            s.load_nodes(nodes)
+            st_ = s.prepare(pods)  # (may re-lay the table out for the pods' quantities: snapshot after)
+            s.save_table()
+            return st_
+        st = run_phase(cx, setup)
 
         def step():
             s.restore_table()
@@ -294,19 +354,33 @@ def measure(cx, a, workload, steps, warmup, with_diag=True):
 
         # all ranks enter their first run together: a sharded rank's first window waits (bounded)
         # for its peers' lists, and a one-sided timeout would void only that rank's run
+        err, last = None, None
         cx.barrier()
         for _ in range(warmup):
-            step()
+            if err is None:
+                try:
+                    step()
+                except Exception as e:
+                    err = e
         cx.barrier()
         t0 = time.perf_counter()
-        last = None
         for _ in range(steps):
-            last = step()
+            if err is None:
+                try:
+                    last = step()
+                except Exception as e:
+                    err = e
         cx.barrier()
-        elapsed = cx.max(time.perf_counter() - t0)
-        placement, keys = st.results()
-        final = s.read_nodes()  # the table after the last timed step (which started from the snapshot)
-        st.free()
+        dt = time.perf_counter() - t0
+        agree(cx, err)
+        elapsed = cx.max(dt)
+
+        def collect():
+            pl_, keys_ = st.results()
+            final_ = s.read_nodes()  # the table after the last timed step (which started from the snapshot)
+            st.free()
+            return pl_, keys_, final_
+        placement, keys, final = run_phase(cx, collect)
     finally:
         s.close()
     ranks_work = cx.world if (cx.world > 1 and not sharded) else 1  # replicas multiply the work
@@ -327,8 +401,9 @@ def measure(cx, a, workload, steps, warmup, with_diag=True):
 def measure_sharded(cx, a, workload):
     """N > 1 config 3: the requested transport (default: the peer-memory mailbox, which runs the
     sharded RESIDENT stream), falling back to the RCCL all-gather when any rank fails or the ranks'
-    placements disagree.  Every rank takes the same decision (all-reduces of an ok flag and of the
-    placement checksum), so a fallback never leaves ranks out of step."""
+    placements disagree.  measure() fails on every rank at the same agreement point, and the ranks
+    then all-reduce an ok flag and the placement checksum, so a fallback never leaves ranks out of
+    step (tests/test_bench_launch.py drives real measure() failures at world 2 over gloo)."""
     import zlib
 
     tried = []
@@ -381,6 +456,26 @@ def check_stream(m):
             "table_match": all(bool(np.array_equal(on[k], m["final"][k])) for k in on),
             "oracle": how, "oracle_s": round(dt, 2),
             "invariants": {k: v for k, v in inv.items() if v is not None}}
+
+
+def check_batched(m):
+    """Correctness of the batched leg (config 5, spec S11): the incremental batched oracle over the
+    WHOLE stream (or_schedule_batched_incremental, identical to or_schedule_batched: per pod type and
+    zone a max tree, only claimed nodes re-scored), diffed against the GPU's placements, claimed keys
+    and final table, plus conservation / capacity / anti-affinity invariants."""
+    from oracle import oracle as O
+    from qsched.checks import batched_invariants
+
+    on = {k: v.copy() for k, v in m["nodes"].items()}
+    t0 = time.perf_counter()
+    ref, rkeys, _ = O.schedule_batched_incremental(on, qsched.pods_from_struct(m["pods"]), nthreads=16)
+    dt = time.perf_counter() - t0
+    inv = batched_invariants(m["nodes"], m["pods"], m["placement"], m["final"])
+    return {"placements_match": bool(np.array_equal(ref, m["placement"])),
+            "keys_match": bool(np.array_equal(rkeys, m["keys"])),
+            "table_match": all(bool(np.array_equal(on[k], m["final"][k])) for k in on),
+            "oracle": "oracle/qs_oracle.c or_schedule_batched_incremental, 16 OpenMP threads",
+            "oracle_s": round(dt, 2), "invariants": inv}
 
 
 def scan_roofline(cx, a, n_nodes=1 << 24, n_pods=32):
@@ -468,6 +563,7 @@ def wide_leg(cx, a, n_nodes=5000, n_pods=100000, steps=3):
     return {"workload": f"{n_nodes:,} nodes (odd-Ki allocatable 64-768 GiB) x {n_pods:,} pods "
                         "(decimal requests 100M/512M/1G/3G): exact stream on the wide layout",
             "table_layout": stats["table_layout"], "engine": stats["engine_used"],
+            "launch": "resident" if stats.get("resident") else "per-window",
             "value": round(n_pods / wall, 1), "unit": "pods/s", "ms_per_step": round(wall * 1e3, 3),
             "placements_match": bool(np.array_equal(placement, ref))}
 
@@ -540,6 +636,21 @@ def framework_leg(cx, n_nodes=5000, n_pods=5000):
     return out
 
 
+def run_leg(cx, a, leg):
+    """One sub-leg alone (--leg), with its correctness check."""
+    if leg == "wide":
+        return wide_leg(cx, a)
+    if leg == "framework":
+        return framework_leg(cx)
+    steps = 1 if leg == "config3" else 3
+    m = measure(cx, a, leg, steps, 1, with_diag=False)
+    out = {"workload": m["desc"], "value": round(m["value"], 1), "unit": "pods/s",
+           "ms_per_step": round(m["ms_per_step"], 3), "engine": m["engine"], "launch": m["launch"],
+           "unschedulable_frac": round(m["unschedulable_frac"], 5)}
+    out["check"] = check_batched(m) if leg == "config5" else check_stream(m)
+    return out
+
+
 def main():
     argv = sys.argv[1:]
     a = parse(argv)
@@ -553,6 +664,9 @@ def main():
         import subprocess
         return subprocess.run(plan["argv"]).returncode
     cx = Ctx()
+    if a.leg:
+        print(json.dumps(run_leg(cx, a, a.leg)), flush=True)
+        return 0
     workload = a.workload if a.workload != "auto" else ("config2" if cx.world == 1 else "config3")
     if cx.world > 1 and workload == "config3":
         m = measure_sharded(cx, a, workload)
@@ -623,7 +737,8 @@ def main():
                                       "unit": "pods/s", "evals_per_s": round(c5["value"] * c5["n_nodes"], 1),
                                       "ms_per_step": round(c5["ms_per_step"], 3), "steps": 3,
                                       "engine": c5["engine"],
-                                      "unschedulable_frac": round(c5["unschedulable_frac"], 5)}
+                                      "unschedulable_frac": round(c5["unschedulable_frac"], 5),
+                                      "check": check_batched(c5)}
         if scan is not None:
             out["scan"] = scan
         if e2e is not None:

@@ -136,7 +136,12 @@ struct qs_ctx {
     qs_host::DevBuf hand;  // window hand-off words: {unused, ready, timeout flag} (u64 each)
     bool handoff_off = false;  // a hand-off timed out once: cross-stream events from then on
     qs_host::DevBuf resctl;    // resident stream's hand-off counters
-    bool resident_off = false; // a resident stream timed out once: per-window launches from then on
+    // Resident-stream timeouts (QS_ETIMEOUT of a resident run): the run right after one uses
+    // per-window launches (cooldown), the next is resident again; a second consecutive resident
+    // timeout keeps per-window launches for the context's life (qs_dist_mailbox_connect resets both)
+    int res_timeouts = 0;
+    bool res_cooldown = false;
+    uint32_t inject_used = 0;  // QS_INJECT_FAULT test hooks already fired on this context (bit per hook)
     bool last_resident = false;  // the last lookahead run was a resident stream
     int cus = 0;               // compute units of the device (resident stream's selector count)
     uint64_t run_seq = 0;      // lookahead runs of this context (the hand-off's epoch)

@@ -32,10 +32,12 @@ struct alignas(16) DRow {
 // be stored exactly as int32 multiples of 2^u bytes below 2^24 (odd-Ki kubelet allocatable,
 // decimal "100M" requests).  Memory columns are f64 integers in bytes (exact below 2^53); cpu,
 // pod counts and extended resources stay int32 as in DRow.  80 bytes.
+// The fields a Reserve changes sit in q0 / q1 (and q4): the resident stream hands exactly those
+// quads off write-through, as it does q0 / q1 / q3 of a compact row.
 struct alignas(16) DRowW {
-    int32_t ac, rc, zc, np;      // q0
-    double am, rm;               // q1  Allocatable / Requested memory (bytes)
-    double zm, ym;               // q2  NonZeroRequested memory, RN_f64(1/am)
+    int32_t rc, zc, np, ac;      // q0  Requested / NonZeroRequested cpu, pod count; Allocatable cpu
+    double rm, zm;               // q1  Requested / NonZeroRequested memory (bytes)
+    double am, ym;               // q2  Allocatable memory, RN_f64(1/am)
     double yc;                   // q3  RN_f64(1/ac)
     int32_t mp, pad;
     int32_t ae0, re0, ae1, re1;  // q4  extended resources
@@ -100,6 +102,10 @@ struct DevCfg {
     // the resident stream never deliver window 3's first task, so the resolver's wait times out
     // and the in-kernel werr drain runs for real.  0 in every normal run.
     uint32_t inject;
+    // Bound (s_memrealtime ticks, 100 MHz) of the resident stream's waits in its first window, whose
+    // producers may be a peer rank still in host-side prepare (sharded: 5 s, as the per-window
+    // mailbox wait, qs_dist.cpp); 0 = the 0.5 s bound of every later wait.
+    uint64_t first_ticks;
 };
 
 // Resolver prologue: thread 0 spins (s_sleep) until window s0/K's lists are published, then every
@@ -189,8 +195,8 @@ __device__ __forceinline__ RowT<F> load_row(const DevTable &t, uint32_t i) {
         const double2 *y = reinterpret_cast<const double2 *>(t.wrows + i);
         const double2 b = y[1], c = y[2];
         RowW r;
-        r.ac = a.x; r.rc = a.y; r.zc = a.z; r.np = a.w;
-        r.am = b.x; r.rm = b.y; r.zm = c.x; r.ym = c.y;
+        r.rc = a.x; r.zc = a.y; r.np = a.z; r.ac = a.w;
+        r.rm = b.x; r.zm = b.y; r.am = c.x; r.ym = c.y;
         r.yc = __builtin_bit_cast(double, ((uint64_t)(uint32_t)d.y << 32) | (uint32_t)d.x);
         r.mp = d.z;
         return r;
@@ -255,10 +261,8 @@ template <uint32_t F>
 __device__ __forceinline__ void store_dyn(const DevTable &t, uint32_t i, const RowT<F> &r) {
     if constexpr ((F & kFeatWide) != 0) {
         int32_t *w = reinterpret_cast<int32_t *>(t.wrows + i);
-        w[1] = r.rc; w[2] = r.zc; w[3] = r.np;
-        double *d = reinterpret_cast<double *>(t.wrows + i);
-        d[3] = r.rm;  // q1.y
-        d[4] = r.zm;  // q2.x
+        w[0] = r.rc; w[1] = r.zc; w[2] = r.np;
+        *reinterpret_cast<double2 *>(w + 4) = make_double2(r.rm, r.zm);  // q1
     } else {
         int32_t *w = reinterpret_cast<int32_t *>(t.rows + i);
         *reinterpret_cast<int2 *>(w + 2) = make_int2(r.rc, r.rm);
@@ -278,12 +282,18 @@ __device__ __forceinline__ void store_dynx(const DevTable &t, uint32_t i, const 
 // ---- in-launch hand-off forms of the resident stream -------------------------
 // Per MI355X_MICROARCH.md § inter-workgroup visibility (valid forms, row 1): every handed-off byte
 // is stored write-through (sc1) and read with sc1 loads to registers, so neither side needs an L2
-// write-back or an L1 invalidate.  Only compact rows (DRow) are handed off this way.
+// write-back or an L1 invalidate.  Both row layouts: the quads a Reserve changes (compact q0 q1
+// q3, wide q0 q1 q4) go through sc1, the static ones (reciprocals, wide allocatable memory) are
+// read plainly.
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) uint64_t gu64;
 typedef __attribute__((address_space(1))) uint32_t gu32;
+template <uint32_t F>
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const DevTable &t) {
-    return __builtin_amdgcn_make_buffer_rsrc((void *)t.rows, (short)0, (int)(t.n * sizeof(DRow)), 0x00020000);
+    if constexpr ((F & kFeatWide) != 0)
+        return __builtin_amdgcn_make_buffer_rsrc((void *)t.wrows, (short)0, (int)(t.n * sizeof(DRowW)), 0x00020000);
+    else
+        return __builtin_amdgcn_make_buffer_rsrc((void *)t.rows, (short)0, (int)(t.n * sizeof(DRow)), 0x00020000);
 }
 __device__ __forceinline__ uint64_t load_coh_u64(const uint64_t *p) {
     return __hip_atomic_load((gu64 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -296,36 +306,60 @@ __device__ __forceinline__ uint32_t load_coh_u32(const uint32_t *p) {
 }
 // Every storing wave drains its sc1 stores before the workgroup barrier that precedes a signal.
 __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-// A compact row whose dynamic quads (q0 = ac am rc rm, q1 = zc zm np mp, q3 = extended) another
-// workgroup writes during the launch: those quads by sc1 loads, the static reciprocals plainly.
+__device__ __forceinline__ double u2d(uint32_t lo, uint32_t hi) {
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+// A row whose dynamic quads another workgroup writes during the launch: those quads by sc1
+// loads, the static ones plainly.
 template <uint32_t F>
-__device__ __forceinline__ Row load_row_coh(const DevTable &t, __amdgpu_buffer_rsrc_t rs, uint32_t i, RowX &x) {
-    static_assert((F & kFeatWide) == 0, "compact rows only");
-    const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(i * sizeof(DRow)), 0, 16);
-    const u32x4 b = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(i * sizeof(DRow) + 16), 0, 16);
-    const double2 y = reinterpret_cast<const double2 *>(t.rows + i)[2];
-    Row r;
-    r.ac = (int32_t)a.x; r.am = (int32_t)a.y; r.rc = (int32_t)a.z; r.rm = (int32_t)a.w;
-    r.zc = (int32_t)b.x; r.zm = (int32_t)b.y; r.np = (int32_t)b.z; r.mp = (int32_t)b.w;
-    r.yc = y.x; r.ym = y.y;
+__device__ __forceinline__ RowT<F> load_row_coh(const DevTable &t, __amdgpu_buffer_rsrc_t rs, uint32_t i, RowX &x) {
+    constexpr int RB = (int)((F & kFeatWide) ? sizeof(DRowW) : sizeof(DRow));
+    constexpr int XQ = (F & kFeatWide) ? 64 : 48;  // byte offset of the extended-resource quad
+    const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)i * RB, 0, 16);
+    const u32x4 b = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)i * RB + 16, 0, 16);
+    RowT<F> r;
+    if constexpr ((F & kFeatWide) != 0) {
+        const int4 *q = reinterpret_cast<const int4 *>(t.wrows + i);
+        const double2 c = reinterpret_cast<const double2 *>(t.wrows + i)[2];
+        const int4 d = q[3];
+        r.rc = (int32_t)a.x; r.zc = (int32_t)a.y; r.np = (int32_t)a.z; r.ac = (int32_t)a.w;
+        r.rm = u2d(b.x, b.y); r.zm = u2d(b.z, b.w);
+        r.am = c.x; r.ym = c.y;
+        r.yc = u2d((uint32_t)d.x, (uint32_t)d.y);
+        r.mp = d.z;
+    } else {
+        const double2 y = reinterpret_cast<const double2 *>(t.rows + i)[2];
+        r.ac = (int32_t)a.x; r.am = (int32_t)a.y; r.rc = (int32_t)a.z; r.rm = (int32_t)a.w;
+        r.zc = (int32_t)b.x; r.zm = (int32_t)b.y; r.np = (int32_t)b.z; r.mp = (int32_t)b.w;
+        r.yc = y.x; r.ym = y.y;
+    }
     x = RowX{};
     if (F & kFeatExt) {
-        const u32x4 e = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(i * sizeof(DRow) + 48), 0, 16);
+        const u32x4 e = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)i * RB + XQ, 0, 16);
         x.ae0 = (int32_t)e.x; x.re0 = (int32_t)e.y; x.ae1 = (int32_t)e.z; x.re1 = (int32_t)e.w;
     }
     return r;
 }
 template <uint32_t F>
-__device__ __forceinline__ void store_row_coh(const DevTable &t, __amdgpu_buffer_rsrc_t rs, uint32_t i, const Row &r,
-                                              const RowX &x) {
+__device__ __forceinline__ void store_row_coh(const DevTable &t, __amdgpu_buffer_rsrc_t rs, uint32_t i,
+                                              const RowT<F> &r, const RowX &x) {
     (void)t;
-    const u32x4 a = {(uint32_t)r.ac, (uint32_t)r.am, (uint32_t)r.rc, (uint32_t)r.rm};
-    const u32x4 b = {(uint32_t)r.zc, (uint32_t)r.zm, (uint32_t)r.np, (uint32_t)r.mp};
-    __builtin_amdgcn_raw_buffer_store_b128(a, rs, (int)(i * sizeof(DRow)), 0, 16);
-    __builtin_amdgcn_raw_buffer_store_b128(b, rs, (int)(i * sizeof(DRow) + 16), 0, 16);
+    constexpr int RB = (int)((F & kFeatWide) ? sizeof(DRowW) : sizeof(DRow));
+    constexpr int XQ = (F & kFeatWide) ? 64 : 48;
+    u32x4 a, b;
+    if constexpr ((F & kFeatWide) != 0) {
+        const uint64_t rm = __builtin_bit_cast(uint64_t, r.rm), zm = __builtin_bit_cast(uint64_t, r.zm);
+        a = u32x4{(uint32_t)r.rc, (uint32_t)r.zc, (uint32_t)r.np, (uint32_t)r.ac};
+        b = u32x4{(uint32_t)rm, (uint32_t)(rm >> 32), (uint32_t)zm, (uint32_t)(zm >> 32)};
+    } else {
+        a = u32x4{(uint32_t)r.ac, (uint32_t)r.am, (uint32_t)r.rc, (uint32_t)r.rm};
+        b = u32x4{(uint32_t)r.zc, (uint32_t)r.zm, (uint32_t)r.np, (uint32_t)r.mp};
+    }
+    __builtin_amdgcn_raw_buffer_store_b128(a, rs, (int)i * RB, 0, 16);
+    __builtin_amdgcn_raw_buffer_store_b128(b, rs, (int)i * RB + 16, 0, 16);
     if (F & kFeatExt) {
         const u32x4 e = {(uint32_t)x.ae0, (uint32_t)x.re0, (uint32_t)x.ae1, (uint32_t)x.re1};
-        __builtin_amdgcn_raw_buffer_store_b128(e, rs, (int)(i * sizeof(DRow) + 48), 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(e, rs, (int)i * RB + XQ, 0, 16);
     }
 }
 

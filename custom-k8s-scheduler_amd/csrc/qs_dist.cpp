@@ -193,6 +193,9 @@ qs_status qs_dist_mailbox_connect(qs_ctx *c, const uint8_t *handles) {
         HIPCHK(hipDeviceSynchronize());
         c->run_seq = 0;
         c->mbox_broken = false;
+        // every rank starts the new connection from the same resident / per-window choice
+        c->res_timeouts = 0;
+        c->res_cooldown = false;
         std::vector<char *> bases((size_t)c->world);
         for (int r = 0; r < c->world; ++r) {
             if (r == c->rank) {

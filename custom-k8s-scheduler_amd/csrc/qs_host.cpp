@@ -496,14 +496,19 @@ void put_row(Mirror &m, uint32_t i, const RowSnap &r) {
     m.gen[i] = r.gen; m.zone[i] = r.zone;
 }
 
-// Test hook for the recovery path (tests/test_gpu_recovery.py): QS_INJECT_FAULT=<entry> makes the
-// next call of that entry point fail as a device error after its device work; one-shot.
-void maybe_inject_fault(const char *entry) {
+// Test hooks for the recovery path (tests/test_gpu_recovery.py): QS_INJECT_FAULT=<entry> makes the
+// next call of that entry point fail as a device error after its device work.  One-shot per
+// context and hook (the environment itself is never modified by the library).
+enum InjectHook : uint32_t { kInjStreamRun = 1u, kInjHandoff = 2u, kInjResidentStall = 4u };
+bool inject_once(qs_ctx *c, const char *name, uint32_t bit) {
     const char *e = getenv("QS_INJECT_FAULT");
-    if (e && std::strcmp(e, entry) == 0) {
-        unsetenv("QS_INJECT_FAULT");
+    if (!e || std::strcmp(e, name) != 0 || (c->inject_used & bit)) return false;
+    c->inject_used |= bit;
+    return true;
+}
+void maybe_inject_fault(qs_ctx *c, const char *entry) {
+    if (inject_once(c, entry, kInjStreamRun))
         fail(QS_EDEVICE, std::string("injected device fault in ") + entry);
-    }
 }
 
 // A pending row (qs_reserve's fast path defers its device write to the next qs_score_pod launch)
@@ -1367,9 +1372,12 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                 // profiles: there the selectors exchange every pod's shard list through the peers'
                 // mailboxes inside the launch (RCCL cannot be called in a kernel)
                 const bool res_transport = c->world == 1 ? !mbox && !c->comm : mbox && !norm;
-                const bool resident = overlap && res_transport && !c->resident_off && !diag_on && !c->wide &&
+                const bool res_allowed = c->res_timeouts < 2 && !c->res_cooldown;
+                const bool resident = overlap && res_transport && res_allowed && !diag_on &&
                                       !(renv && renv[0] == '0') && rgeo.G > 0 && coresident;
                 c->last_resident = resident;
+                // the per-window run after a resident timeout ends the cooldown (whatever it returns)
+                if (!resident) c->res_cooldown = false;
                 if (resident) {
                     c->resctl.ensure(la_stream_res_ctl_bytes());
                     c->dc.ready = nullptr;
@@ -1396,11 +1404,13 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                                        kMbResHello, kMbResFlags, kMbResLists};
                     // test hook: a selector that never delivers window 3 (one-shot), so the
                     // in-kernel timeout drain runs (tests/test_gpu_recovery.py)
+                    DevCfg dcr = c->dc;  // (the launch's copy: the hook never sticks to the context)
+                    // (QS_INJECT_FAULT=resident_stall_always: every resident launch of the context)
                     const char *inj = getenv("QS_INJECT_FAULT");
-                    if (inj && std::strcmp(inj, "resident_stall") == 0) {
-                        unsetenv("QS_INJECT_FAULT");
-                        c->dc.inject = 1;
-                    }
+                    dcr.inject = (inject_once(c, "resident_stall", kInjResidentStall) ||
+                                  (inj && std::strcmp(inj, "resident_stall_always") == 0)) ? 1u : 0u;
+                    // sharded: window 0's waits cover a peer still in host-side prepare (5 s)
+                    dcr.first_ticks = c->world > 1 ? 500000000ull : 0ull;
                     // QS_RES_DIAG=1: the resolver's time split (list waits / window bodies / between)
                     static const bool rdiag_on = getenv("QS_RES_DIAG") && getenv("QS_RES_DIAG")[0] == '1';
                     uint64_t *rdiag = nullptr;
@@ -1410,13 +1420,12 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                         HIPCHK(hipMemsetAsync(rdiag, 0, 256, c->stream));
                     }
                     kt.begin(3, c->stream);  // the one launch, under "resolve"
-                    HIPCHK(launch_la_stream_res(c->dt, dp, dx, c->dc, P, rgeo, L0, c->clists.as<uint64_t>(),
+                    HIPCHK(launch_la_stream_res(c->dt, dp, dx, dcr, P, rgeo, L0, c->clists.as<uint64_t>(),
                                                 (uint32_t)lwords, (uint32_t)rcw, c->npart.as<uint4>(),
                                                 c->normi.as<NormInfo>(), c->nstat.as<uint32_t>(),
                                                 c->nfall.as<unsigned long long>(), on, ok,
                                                 st, c->resctl.p, sel, rdiag, rsh, c->stream));
                     kt.end(3, c->stream);
-                    c->dc.inject = 0;
                     if (rdiag) {
                         uint64_t h[32] = {0};
                         HIPCHK(hipMemcpyAsync(h, rdiag, 256, hipMemcpyDeviceToHost, c->stream));
@@ -1503,23 +1512,23 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
         if (eng == QS_ENGINE_LOOKAHEAD && c->last_waits) {
             uint64_t w = 0;  // a resolver gave up waiting for its window's lists (device hand-off)
             HIPCHK(hipMemcpy(&w, c->hand.as<uint64_t>() + 2, 8, hipMemcpyDeviceToHost));
-            const char *inj = getenv("QS_INJECT_FAULT");  // test hook: a timed-out hand-off
-            if (inj && std::strcmp(inj, "handoff") == 0) {
-                unsetenv("QS_INJECT_FAULT");
-                w = 1;
-            }
+            if (inject_once(c, "handoff", kInjHandoff)) w = 1;  // test hook: a timed-out hand-off
             if (w) {
                 // the select stream did not run beside the resolvers (e.g. a profiler serialising
                 // dispatches), or a mailbox peer never posted: the run's results and table updates
                 // are void and the device table is rebuilt from the host mirror (guarded(), as for
                 // a device fault); an unsharded context uses cross-stream events from now on
-                if (c->last_resident) c->resident_off = true;
-                else if (!c->mbox_on) c->handoff_off = true;
+                if (c->last_resident) {
+                    ++c->res_timeouts;
+                    c->res_cooldown = true;
+                } else if (!c->mbox_on) {
+                    c->handoff_off = true;
+                }
                 if (c->mbox_on && !c->comm) c->mbox_broken = true;
                 fail(QS_ETIMEOUT, c->mbox_on ? "mailbox exchange timed out (a peer never posted its window)"
                                              : c->last_resident
                                                    ? "resident lookahead stream timed out (a hand-off never arrived); "
-                                                     "the context falls back to per-window launches"
+                                                     "the next run uses per-window launches"
                                                    : "lookahead window hand-off timed out (lists never published); "
                                                      "the context falls back to stream events");
             }
@@ -1536,7 +1545,7 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
         c->mirror_stale = true;
         if (eng != QS_ENGINE_SCAN) c->soa_valid = false;  // those engines update the rows only
         kt.finish();
-        maybe_inject_fault("stream_run");
+        maybe_inject_fault(c, "stream_run");
         // keep the host mirror authoritative after every stream (one D2H of the rows, outside
         // the timed region): a later device fault rebuilds the table from it
         sync_mirror(c);

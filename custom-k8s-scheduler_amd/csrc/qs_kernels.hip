@@ -151,8 +151,9 @@ LaGeom la_stream_res_plan(const LaGeom &geo, uint32_t feat, uint32_t n, uint32_t
     r.G = 0;
     // compact Fit + Balanced (+ extended) profiles, and the normalizing ones (K <= kResNormK)
     // sharded (geo.W > 1 ranks, one shard each): Fit + Balanced (+ extended) only, W * L <= 512
-    const bool fit = feat == 0 || feat == kFeatExt;
-    const bool norm = (feat & kFeatNorm) != 0 && (feat & kFeatWide) == 0 && geo.K <= kResNormK;
+    const uint32_t fl = feat & ~kFeatWide;  // both row layouts
+    const bool fit = fl == 0 || fl == kFeatExt;
+    const bool norm = (feat & kFeatNorm) != 0 && geo.K <= kResNormK;
     const bool shard_ok = geo.W == 1 ? geo.nv == 1 && geo.epl == 1
                                      : fit && geo.nv == 1 && geo.K <= 32 && geo.W * geo.L <= (uint32_t)kResBS;
     if (!((fit || norm) && shard_ok && geo.waves == 4 && geo.L <= 64 && n > 0 && cus > geo.K)) return r;
@@ -183,7 +184,8 @@ size_t la_stream_res_ctl_bytes() { return kResCtlBytes; }
 // CU can exceed what the hardware admits by one workgroup (MI355X_MICROARCH.md, residency), so one
 // is taken off whenever the API allows two or more.
 uint32_t la_stream_res_max_blocks(const LaGeom &geo, uint32_t feat, uint32_t n, uint32_t cus) {
-    const int per = (feat & kFeatNorm)  ? la_stream_res_per_cu<kFeatExt | kFeatTaint | kFeatAffinity>(geo, n)
+    const int per = (feat & kFeatWide)  ? wide_la_stream_res_per_cu(geo, feat, n)
+                    : (feat & kFeatNorm)  ? la_stream_res_per_cu<kFeatExt | kFeatTaint | kFeatAffinity>(geo, n)
                     : (feat & kFeatExt) ? la_stream_res_per_cu<kFeatExt>(geo, n)
                                         : la_stream_res_per_cu<0>(geo, n);
     // The API's answer can exceed what the hardware admits by one workgroup when the SGPR budget
@@ -200,7 +202,11 @@ hipError_t launch_la_stream_res(const DevTable &t, const void *pods, const DPodX
                                 uint32_t cwords, uint4 *npart, NormInfo *norm, uint32_t *stat, unsigned long long *nfall,
                                 int32_t *on, uint64_t *ok, uint64_t *st, void *ctl, uint32_t sel_blocks, uint64_t *rdiag,
                                 const ResShard &rsh, hipStream_t stream) {
-    if (t.wrows || geo.G == 0 || (uint64_t)t.n * sizeof(DRow) >= (1ull << 31)) return hipErrorInvalidValue;
+    if (geo.G == 0 || (uint64_t)t.n * (t.wrows ? sizeof(DRowW) : sizeof(DRow)) >= (1ull << 31))
+        return hipErrorInvalidValue;
+    if (t.wrows)
+        return wide_la_stream_res(t, pods, podx, c, P, geo, lists0, clists0, lwords, cwords, npart, norm, stat, nfall, on,
+                                  ok, st, ctl, sel_blocks, rdiag, rsh, stream);
     if (c.feat & kFeatNorm)
         return la_stream_res_f<kFeatExt | kFeatTaint | kFeatAffinity>(t, pods, podx, c, P, geo, lists0, clists0, lwords,
                                                                       cwords, npart, norm, stat, nfall, on, ok, st, ctl,

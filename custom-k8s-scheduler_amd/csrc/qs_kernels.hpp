@@ -1807,15 +1807,21 @@ struct ResCtl {                // zeroed before every launch; each counter on it
     uint32_t ticket[2][64];    // chunk lists delivered, per window parity and window pod
     uint32_t nticket[2][64];   // normalizing profiles: chunk partial maxima published, likewise
 };
-// Bounded relaxed poll by one lane: true once *p >= want; false on werr or after 0.5 s (100 MHz).
-__device__ __forceinline__ bool res_wait_ge(const uint32_t *p, uint32_t want, uint32_t *werr) {
+// Bounded relaxed poll by one lane: true once *p >= want; false on werr or after `ticks` (100 MHz;
+// 0.5 s, or DevCfg::first_ticks in a run's first window).
+constexpr uint64_t kResWaitTicks = 50000000ull;
+__device__ __forceinline__ uint64_t res_bound(const DevCfg &c, uint32_t w) {
+    return (w == 0 && c.first_ticks) ? c.first_ticks : kResWaitTicks;
+}
+__device__ __forceinline__ bool res_wait_ge(const uint32_t *p, uint32_t want, uint32_t *werr,
+                                            uint64_t ticks = kResWaitTicks) {
     if (load_coh_u32(p) >= want) return true;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (;;) {
         __builtin_amdgcn_s_sleep(1);
         if (load_coh_u32(p) >= want) return true;
         if (load_coh_u32(werr) != 0u) return false;
-        if (__builtin_amdgcn_s_memrealtime() - t0 > 50000000ull) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
             __hip_atomic_store((gu32 *)werr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return false;
         }
@@ -1880,17 +1886,19 @@ __device__ __forceinline__ void res_publish_list_norm(uint64_t *lbuf, uint32_t L
 // cross merges read slot (w - 4) % 4.  Returns false on a timeout (werr raised).
 __device__ __forceinline__ bool res_cross_merge(uint64_t *lbuf, uint32_t L, uint32_t k, uint32_t w,
                                                 const ResShard &rsh, bool &hello_ok, uint32_t &okflag,
-                                                uint32_t *werr) {
+                                                uint32_t *werr, uint64_t first_ticks) {
     const int tid = threadIdx.x, lane = tid & 63;
     const uint32_t W = rsh.W;
     const uint64_t tag = (rsh.seq << 32) | (uint64_t)(w + 1);
     const size_t cell = ((size_t)(w & 3) * 32 + k) * 16;  // [slot][pod][rank] index base
+    // the hello and window 0's flags may wait for a peer still in host-side prepare: first_ticks
+    const uint64_t bound = (w == 0 || !hello_ok) && first_ticks ? first_ticks : kResWaitTicks;
     auto sys_poll = [&](const uint64_t *p, uint64_t want) -> bool {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         while (__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < want) {
             __builtin_amdgcn_s_sleep(1);
             if (load_coh_u32(werr) != 0u) return false;
-            if (__builtin_amdgcn_s_memrealtime() - t0 > 50000000ull) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > bound) {
                 __hip_atomic_store((gu32 *)werr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 return false;
             }
@@ -1967,7 +1975,7 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
     __shared__ uint32_t nred[4][8];  // NORM: per-wave partial maxima and counts
     uint32_t &okflag = okflag_[0];
     const int tid = threadIdx.x, lane = tid & 63, w8 = tid >> 6;
-    const __amdgpu_buffer_rsrc_t rs = row_rsrc(t);
+    const __amdgpu_buffer_rsrc_t rs = row_rsrc<F>(t);
     DevCfg cv = c;  // (weights in VGPRs, as in la_resolve4_stream)
     asm volatile("" : "+v"(cv.yd_both), "+v"(cv.yd_c), "+v"(cv.yd_m), "+v"(cv.wc), "+v"(cv.wm));
     for (uint32_t w = 0; w < nwin; ++w) {
@@ -2000,7 +2008,7 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
                     raw[j] = 0xFFFFFFFFu;
                     if (idx < end) {
                         RowX x;
-                        const Row r = load_row_coh<F>(t, rs, idx, x);
+                        const RowT<F> r = load_row_coh<F>(t, rs, idx, x);
                         const DMask m = t.masks[idx];  // static during a stream
                         x.th = m.th; x.ts = m.ts; x.lb0 = m.lb0; x.lb1 = m.lb1;
                         if (feasible<F>(r, x, p, px)) {
@@ -2048,7 +2056,7 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
                         store_coh_u64(reinterpret_cast<uint64_t *>(np + g) + 1, (uint64_t)o.z | ((uint64_t)o.w << 32));
                         drain_stores();
                         res_add(&ctl->nticket[b][k]);
-                        okflag = res_wait_ge(&ctl->nticket[b][k], ((w >> 1) + 1) * G, c.werr) ? 1u : 0u;
+                        okflag = res_wait_ge(&ctl->nticket[b][k], ((w >> 1) + 1) * G, c.werr, res_bound(c, w)) ? 1u : 0u;
                     }
                     __syncthreads();
                     if (!okflag) return;
@@ -2079,7 +2087,7 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
                     tv[j] = 0;
                     if (idx < end) {
                         RowX x;
-                        const Row r = load_row_coh<F>(t, rs, idx, x);
+                        const RowT<F> r = load_row_coh<F>(t, rs, idx, x);
                         const bool f = feasible<F>(r, x, p, px);
                         const uint32_t tot = node_total<F>(r, x, p, px, cv, 0, 0.0, 0, 0.0, nullptr);
                         tv[j] = f ? tot + 1 : 0;
@@ -2103,7 +2111,7 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
             // every rank and publish the top-L of the W shard lists (sharded)
             auto publish = [&]() {
                 if (rsh.W > 1) {
-                    if (!res_cross_merge(lbuf, L, k, w, rsh, hello_ok, okflag, c.werr)) return false;
+                    if (!res_cross_merge(lbuf, L, k, w, rsh, hello_ok, okflag, c.werr, c.first_ticks)) return false;
                 }
                 if constexpr (NORM)
                     res_publish_list_norm(lbuf, L, out, &ctl->rdy[b][0], t, pods, podx, s0 + k, P,
@@ -2303,7 +2311,6 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                                                    const DPodX *__restrict__ podx, const NormInfo *norm0,
                                                    const uint32_t *stat0, unsigned long long *nfall) {
     constexpr bool NORM = (F & kFeatNorm) != 0;
-    static_assert((F & kFeatWide) == 0, "compact layout");
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t nwords = (t.n + 31) / 32;
@@ -2380,9 +2387,11 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
             const uint32_t knext = w + 1 < nwin ? min(K, P - s0 - K) : 0u;
             // next window's pod records (to LDS at the end; loaded unconditionally, clamped, so the
             // loads stay in flight through the window instead of being waited for at a branch join)
-            static_assert(sizeof(PodT<F>) == 32, "two 16-byte quads per pod record");
+            constexpr int PQ = (int)(sizeof(PodT<F>) / 16);  // 16-byte quads per pod record (2, wide 3)
             const int4 *pq = reinterpret_cast<const int4 *>(pods + min(s0 + K + (uint32_t)lane, P - 1));
-            const int4 npa = pq[0], npb = pq[1];
+            int4 npq[PQ];
+#pragma unroll
+            for (int q = 0; q < PQ; ++q) npq[q] = pq[q];
             uint64_t res_key = 0, res_stamp = 0;
             ResPub pv = none;
             bool stopped = false;  // NORM: a rescan ran in this window
@@ -2522,8 +2531,8 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
             if ((uint32_t)lane < knext) {
                 int4 *dq = reinterpret_cast<int4 *>(&wpods2[(w + 1) & 1][lane]);
-                dq[0] = npa;
-                dq[1] = npb;
+#pragma unroll
+                for (int q = 0; q < PQ; ++q) dq[q] = npq[q];
             }
             __syncthreads();  // B2
             __syncthreads();  // B3 (wave A stored and staged the won rows)
@@ -2538,7 +2547,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
         RowX SX{};
         uint32_t nd = 0;
         uint32_t pend = 0;  // wave A: windows whose rows are stored but not yet signalled (done value)
-        const __amdgpu_buffer_rsrc_t rs = row_rsrc(t);
+        const __amdgpu_buffer_rsrc_t rs = row_rsrc<F>(t);
         // NORM: pod k's maxima and reciprocals (LDS, read one step ahead)
         struct PodN {
             NormInfo nf;
@@ -2735,7 +2744,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                 e0 = pe0; eX = pe1; eY = pe2;
             } else {
                 ++nfallback;
-                if (lane == 0) (void)res_wait_ge(&ctl->rdy[w & 1][0], (w >> 1) * K + kend, c.werr);
+                if (lane == 0) (void)res_wait_ge(&ctl->rdy[w & 1][0], (w >> 1) * K + kend, c.werr, res_bound(c, w));
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below)
                 e0 = ent(lists, 0, kend);
                 eX = ent(lists, 1, kend);
@@ -3603,5 +3612,11 @@ hipError_t wide_score_pod1(const DevTable &t, const void *pod, const DPodX *podx
 hipError_t wide_batch_claim(const DevTable &t, const void *pods, const uint64_t *lists, uint32_t *ctrl,
                             uint32_t *bidx, uint32_t P, uint32_t B, int32_t *on, uint64_t *ok,
                             size_t lds, hipStream_t stream);
+hipError_t wide_la_stream_res(const DevTable &t, const void *pods, const DPodX *podx, const DevCfg &c, uint32_t P,
+                              const LaGeom &geo, uint64_t *lists0, uint64_t *clists0, uint32_t lwords, uint32_t cwords,
+                              uint4 *npart, NormInfo *norm, uint32_t *stat, unsigned long long *nfall, int32_t *on,
+                              uint64_t *ok, uint64_t *st, void *ctl, uint32_t sel_blocks, uint64_t *rdiag,
+                              const ResShard &rsh, hipStream_t stream);
+int wide_la_stream_res_per_cu(const LaGeom &geo, uint32_t feat, uint32_t n);
 
 }  // namespace qs

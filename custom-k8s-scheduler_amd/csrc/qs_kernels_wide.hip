@@ -3,7 +3,7 @@
 // allocatable, decimal requests — anything the compact 2^u-byte int32 layout cannot hold below
 // 2^24).  Two feature classes: Fit + Balanced (+ extended resources), and the normalizing profile
 // (TaintToleration / NodeAffinity); extended-resource columns are always on (a zero request skips
-// them, spec S4).
+// them, spec S4).  Every engine, the resident stream included.
 #include "qs_kernels.hpp"
 
 namespace qs {
@@ -52,6 +52,22 @@ hipError_t wide_batch_claim(const DevTable &t, const void *pods, const uint64_t 
                             uint32_t *bidx, uint32_t P, uint32_t B, int32_t *on, uint64_t *ok,
                             size_t lds, hipStream_t stream) {
     return batch_claim_f<kWideFit>(t, pods, lists, ctrl, bidx, P, B, on, ok, lds, stream);
+}
+
+hipError_t wide_la_stream_res(const DevTable &t, const void *pods, const DPodX *podx, const DevCfg &c, uint32_t P,
+                              const LaGeom &geo, uint64_t *lists0, uint64_t *clists0, uint32_t lwords, uint32_t cwords,
+                              uint4 *npart, NormInfo *norm, uint32_t *stat, unsigned long long *nfall, int32_t *on,
+                              uint64_t *ok, uint64_t *st, void *ctl, uint32_t sel_blocks, uint64_t *rdiag,
+                              const ResShard &rsh, hipStream_t stream) {
+    if (c.feat & kFeatNorm)
+        return la_stream_res_f<kWideNorm>(t, pods, podx, c, P, geo, lists0, clists0, lwords, cwords, npart, norm, stat,
+                                          nfall, on, ok, st, ctl, sel_blocks, rdiag, rsh, stream);
+    return la_stream_res_f<kWideFit>(t, pods, podx, c, P, geo, lists0, clists0, lwords, cwords, npart, norm, stat, nfall,
+                                     on, ok, st, ctl, sel_blocks, rdiag, rsh, stream);
+}
+
+int wide_la_stream_res_per_cu(const LaGeom &geo, uint32_t feat, uint32_t n) {
+    return (feat & kFeatNorm) ? la_stream_res_per_cu<kWideNorm>(geo, n) : la_stream_res_per_cu<kWideFit>(geo, n);
 }
 
 }  // namespace qs

@@ -9,7 +9,13 @@ size without re-running the decision sequence:
 * monotone unschedulability (Fit + Balanced profiles: feasibility only shrinks as Reserve adds
   requests) — a pod that found no feasible node at its turn fits no node of the final table.
 
-Used by tests/test_gpu_scale.py and bench.py's config-3 / config-4 legs beside the oracle diffs.
+Batched mode (spec S11) adds:
+
+* anti-affinity — no two placed pods of an app with hostname anti-affinity share a node, and no two
+  of an app with zone anti-affinity share a zone.
+
+Used by tests/test_gpu_scale.py, tests/test_gpu_batched.py and bench.py's config-3 / config-4 /
+config-5 legs beside the oracle diffs.
 """
 from __future__ import annotations
 
@@ -68,3 +74,18 @@ def stream_invariants(nodes0: dict, pods, placement: np.ndarray, final: dict, fi
                     break
     return {"conservation": bool(cons), "capacity": cap, "unschedulable_infeasible": unsched,
             "placed": int(placed.sum())}
+
+
+def batched_invariants(nodes0: dict, pods, placement: np.ndarray, final: dict) -> dict:
+    """stream_invariants (conservation, capacity) plus spec S11's required anti-affinity."""
+    out = stream_invariants(nodes0, pods, placement, final, fit_only=False)
+    pl = np.asarray(placement)
+    placed = pl >= 0
+    app, aa = pods["app"].astype(np.int64), pods["anti_affinity"]
+    host = placed & (aa == 1)
+    hk = app[host] * (1 << 32) + pl[host]
+    zon = placed & (aa == 2)
+    zk = app[zon] * 64 + nodes0["zone"][pl[zon]].astype(np.int64)
+    out["anti_affinity"] = bool(np.unique(hk).size == hk.size and np.unique(zk).size == zk.size)
+    out.pop("unschedulable_infeasible", None)
+    return out

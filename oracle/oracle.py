@@ -125,6 +125,8 @@ def lib():
         L.or_reserve.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_uint32] * 2 + [ctypes.c_int]
         L.or_schedule_batched.restype = ctypes.c_uint32
         L.or_schedule_batched.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint32] + [ctypes.c_void_p] * 2 + [ctypes.c_int]
+        L.or_schedule_batched_incremental.restype = ctypes.c_uint32
+        L.or_schedule_batched_incremental.argtypes = L.or_schedule_batched.argtypes
         L.or_generate.restype = None
         L.or_generate.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
         _LIB = L
@@ -214,6 +216,22 @@ def schedule_batched(nodes, pods, batch=64, cfg=None, nthreads=1):
     nb = lib().or_schedule_batched(ctypes.byref(sc), ctypes.byref(sn), ctypes.byref(sp),
                                    ctypes.c_uint32(batch), _ptr(placement), _ptr(best),
                                    ctypes.c_int(nthreads))
+    return placement, best, int(nb)
+
+
+def schedule_batched_incremental(nodes, pods, batch=64, cfg=None, nthreads=1):
+    """schedule_batched with incremental lists (per pod type and zone a max tree over the nodes'
+    keys, only the claimed nodes re-scored per batch): identical results for Fit + Balanced (+ ext)
+    profiles.  Mutates ``nodes``.  Returns (placement[p], key[p], batches)."""
+    p = len(pods["req_cpu"])
+    placement = np.full(p, -3, np.int32)
+    best = np.zeros(p, np.uint64)
+    sn, sp, sc = _mk_nodes(nodes), _mk_pods(pods), _mk_cfg(cfg)
+    nb = lib().or_schedule_batched_incremental(ctypes.byref(sc), ctypes.byref(sn), ctypes.byref(sp),
+                                               ctypes.c_uint32(batch), _ptr(placement), _ptr(best),
+                                               ctypes.c_int(nthreads))
+    if nb == 0xFFFFFFFF:
+        raise ValueError("or_schedule_batched_incremental: normalizing profile or zone id >= 64")
     return placement, best, int(nb)
 
 

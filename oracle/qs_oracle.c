@@ -485,6 +485,267 @@ uint32_t or_schedule_batched(const or_config *cfg, or_nodes *nd, const or_pods *
     return batches;
 }
 
+/* ---------------- spec S11 batched mode, incremental lists (same results as or_schedule_batched)
+ * For Fit + Balanced (+ ext) profiles a node's key for pod j depends only on the node's row and the
+ * pod's type (type_fields), and a batch changes at most `batch` rows (the claimed nodes).  Per pod
+ * type and topology zone a max tree over the zone's nodes' keys (node_key(), as or_schedule_batched
+ * evaluates them); a pod's list = the 64 largest keys of the zones its anti-affinity allows, by a
+ * best-first walk over those trees that skips hostname-anti-affinity nodes, i.e. the 64 largest
+ * keys k != 0 with aa_ok, in descending order — exactly or_schedule_batched's list.  Claims and
+ * the apply step are or_schedule_batched's.  After a batch only the claimed nodes are re-scored,
+ * once per type.  tests/test_oracle_incremental.py diffs it against or_schedule_batched bit for bit;
+ * used for config 5's full 10,000 x 200,000 check, where the brute-force oracle takes minutes.
+ * Returns the number of batches, or 0xFFFFFFFF for normalizing profiles / zones >= 64. */
+typedef struct {
+    int64_t f[7];
+    uint32_t rep;
+    uint64_t *tree; /* per zone z: [2 * zM[z]] at zoff[z] */
+} or_btype;
+typedef struct { uint64_t key; uint32_t z, v; } or_hent;
+
+static void heap_push(or_hent **h, uint32_t *n, uint32_t *cap, or_hent e) {
+    if (*n == *cap) { *cap = *cap ? 2 * *cap : 256; *h = (or_hent *)realloc(*h, sizeof(or_hent) * *cap); }
+    or_hent *a = *h;
+    uint32_t i = (*n)++;
+    while (i > 0) {
+        uint32_t p = (i - 1) / 2;
+        if (a[p].key >= e.key) break;
+        a[i] = a[p];
+        i = p;
+    }
+    a[i] = e;
+}
+static or_hent heap_pop(or_hent *a, uint32_t *n) {
+    or_hent top = a[0], last = a[--(*n)];
+    uint32_t i = 0;
+    for (;;) {
+        uint32_t c = 2 * i + 1;
+        if (c >= *n) break;
+        if (c + 1 < *n && a[c + 1].key > a[c].key) c++;
+        if (a[c].key <= last.key) break;
+        a[i] = a[c];
+        i = c;
+    }
+    if (*n) a[i] = last;
+    return top;
+}
+
+typedef struct {
+    or_btype *types;
+    uint32_t T, cap, hcap;
+    int32_t *htab;
+    const uint32_t *zM, *zoff, *leaf;
+} or_bset;
+/* The type of pod j; its per-zone trees are built over the current table on first sight. */
+static int32_t bt_type_of(or_bset *bs, const or_config *cfg, const or_nodes *nd, const or_pods *pd, uint32_t j,
+                          int nthreads) {
+    int64_t f[7];
+    type_fields(pd, j, f);
+    uint32_t h = (uint32_t)type_hash(f) & (bs->hcap - 1);
+    while (bs->htab[h] >= 0) {
+        if (memcmp(bs->types[bs->htab[h]].f, f, sizeof f) == 0) return bs->htab[h];
+        h = (h + 1) & (bs->hcap - 1);
+    }
+    if (bs->T == bs->cap) {
+        bs->cap = bs->cap ? 2 * bs->cap : 64;
+        bs->types = (or_btype *)realloc(bs->types, sizeof(or_btype) * bs->cap);
+    }
+    if (2 * (bs->T + 1) > bs->hcap) { /* grow the hash table (load <= 1/2) */
+        uint32_t nh = 2 * bs->hcap;
+        int32_t *nt = (int32_t *)malloc(sizeof(int32_t) * nh);
+        for (uint32_t i = 0; i < nh; i++) nt[i] = -1;
+        for (uint32_t u = 0; u < bs->T; u++) {
+            uint32_t g = (uint32_t)type_hash(bs->types[u].f) & (nh - 1);
+            while (nt[g] >= 0) g = (g + 1) & (nh - 1);
+            nt[g] = (int32_t)u;
+        }
+        free(bs->htab);
+        bs->htab = nt;
+        bs->hcap = nh;
+        h = (uint32_t)type_hash(f) & (nh - 1);
+        while (bs->htab[h] >= 0) h = (h + 1) & (nh - 1);
+    }
+    or_btype *ty = &bs->types[bs->T];
+    memcpy(ty->f, f, sizeof f);
+    ty->rep = j;
+    const uint32_t *zM = bs->zM, *zoff = bs->zoff, *leaf = bs->leaf;
+    ty->tree = (uint64_t *)calloc(zoff[OR_ZONES] ? zoff[OR_ZONES] : 1, sizeof(uint64_t));
+    uint64_t *tr = ty->tree;
+    const int64_t N = nd->n;
+#pragma omp parallel for num_threads(nthreads) if (nthreads > 1)
+    for (int64_t n = 0; n < N; n++) {
+        const int z = nd->zone[n];
+        tr[zoff[z] + zM[z] + leaf[n]] = node_key(cfg, nd, pd, (uint32_t)n, j, 0, 0, NULL);
+    }
+    for (int z = 0; z < OR_ZONES; z++) {
+        uint64_t *b = tr + zoff[z];
+        for (uint32_t v = zM[z] ? zM[z] - 1 : 0; v >= 1; v--) b[v] = b[2 * v] > b[2 * v + 1] ? b[2 * v] : b[2 * v + 1];
+    }
+    bs->htab[h] = (int32_t)bs->T;
+    return (int32_t)bs->T++;
+}
+
+uint32_t or_schedule_batched_incremental(const or_config *cfg, or_nodes *nd, const or_pods *pd, uint32_t batch,
+                                         int32_t *placement, uint64_t *best_key, int nthreads) {
+    if (cfg->enable_taint || cfg->enable_affinity) return 0xFFFFFFFFu;
+    uint32_t P = pd->p, N = nd->n;
+    if (batch == 0 || batch > OR_LIST) batch = OR_LIST;
+    if (nthreads < 1) nthreads = 1;
+    /* zones: node lists in index order, leaf positions, tree offsets */
+    uint32_t zcnt[OR_ZONES] = {0}, zM[OR_ZONES], zoff[OR_ZONES + 1];
+    for (uint32_t n = 0; n < N; n++) {
+        if (nd->zone[n] < 0 || nd->zone[n] >= OR_ZONES) return 0xFFFFFFFFu;
+        zcnt[nd->zone[n]]++;
+    }
+    zoff[0] = 0;
+    for (int z = 0; z < OR_ZONES; z++) {
+        uint32_t m = 1;
+        while (m < zcnt[z]) m <<= 1;
+        zM[z] = zcnt[z] ? m : 0;
+        zoff[z + 1] = zoff[z] + 2 * zM[z];
+    }
+    uint32_t *znodes = (uint32_t *)malloc(sizeof(uint32_t) * (N ? N : 1)); /* zone-major node lists */
+    uint32_t *zbase = (uint32_t *)calloc(OR_ZONES + 1, sizeof(uint32_t));
+    uint32_t *leaf = (uint32_t *)malloc(sizeof(uint32_t) * (N ? N : 1)); /* node -> position in its zone */
+    for (int z = 0; z < OR_ZONES; z++) zbase[z + 1] = zbase[z] + zcnt[z];
+    {
+        uint32_t fill[OR_ZONES] = {0};
+        for (uint32_t n = 0; n < N; n++) {
+            const int z = nd->zone[n];
+            leaf[n] = fill[z]++;
+            znodes[zbase[z] + leaf[n]] = n;
+        }
+    }
+    uint32_t *order = (uint32_t *)malloc(sizeof(uint32_t) * (P ? P : 1));
+    order_pods(cfg, pd, order);
+    uint8_t *present = (uint8_t *)calloc((size_t)OR_APPS * (N ? N : 1), 1);
+    int32_t *zcount = (int32_t *)calloc((size_t)OR_APPS * OR_ZONES, sizeof(int32_t));
+    uint8_t *claimed = (uint8_t *)calloc(N ? N : 1, 1);
+    uint8_t *claimed_az = (uint8_t *)calloc((size_t)OR_APPS * OR_ZONES, 1);
+    uint64_t(*lists)[OR_LIST] = malloc(sizeof(uint64_t) * OR_LIST * batch);
+    int32_t tix[OR_LIST];
+    uint32_t cur[OR_LIST], pend[OR_LIST], nb = 0, npend = 0, cursor = 0, batches = 0;
+    int32_t won[OR_LIST];
+    or_bset bs = {0};
+    bs.hcap = 1024;
+    bs.htab = (int32_t *)malloc(sizeof(int32_t) * bs.hcap);
+    for (uint32_t i = 0; i < bs.hcap; i++) bs.htab[i] = -1;
+    bs.zM = zM;
+    bs.zoff = zoff;
+    bs.leaf = leaf;
+    nb = P < batch ? P : batch;
+    for (uint32_t i = 0; i < nb; i++) cur[i] = i;
+    cursor = nb;
+    while (nb > 0) {
+        ++batches;
+        for (uint32_t i = 0; i < nb; i++)
+            tix[i] = bt_type_of(&bs, cfg, nd, pd, order[cur[i]], nthreads);
+        /* each pod's 64 best keys against the batch-start state (best-first over allowed zones) */
+        int64_t nb_ = nb;
+#pragma omp parallel for num_threads(nthreads) if (nthreads > 1) schedule(dynamic, 1)
+        for (int64_t i = 0; i < nb_; i++) {
+            const uint32_t j = order[cur[i]];
+            const int32_t app = pd->app[j], aa = pd->anti_affinity[j];
+            const uint64_t *tr = bs.types[tix[i]].tree;
+            or_hent *hp = NULL;
+            uint32_t hn = 0, hc = 0, nt = 0;
+            for (int z = 0; z < OR_ZONES; z++) {
+                if (!zM[z]) continue;
+                if (aa == 2 && zcount[app * OR_ZONES + z] != 0) continue;
+                const uint64_t k = tr[zoff[z] + 1]; /* the root (a single node's leaf when zM = 1) */
+                if (k) heap_push(&hp, &hn, &hc, (or_hent){k, (uint32_t)z, 1u});
+            }
+            while (hn > 0 && nt < OR_LIST) {
+                const or_hent e = heap_pop(hp, &hn);
+                const uint32_t z = e.z, M = zM[z];
+                if (e.v >= M) { /* a leaf: node znodes[zbase[z] + v - M] */
+                    const uint32_t n = znodes[zbase[z] + (e.v - M)];
+                    if (aa == 1 && present[(size_t)app * N + n]) continue;
+                    lists[i][nt++] = e.key;
+                    continue;
+                }
+                const uint64_t *b = tr + zoff[z];
+                const uint32_t l = 2 * e.v, r = 2 * e.v + 1;
+                if (b[l]) heap_push(&hp, &hn, &hc, (or_hent){b[l], z, l});
+                if (b[r]) heap_push(&hp, &hn, &hc, (or_hent){b[r], z, r});
+            }
+            for (uint32_t t = nt; t < OR_LIST; t++) lists[i][t] = 0;
+            free(hp);
+        }
+        /* claims in batch order (or_schedule_batched) */
+        memset(claimed, 0, N ? N : 1);
+        memset(claimed_az, 0, (size_t)OR_APPS * OR_ZONES);
+        npend = 0;
+        for (uint32_t i = 0; i < nb; i++) {
+            uint32_t j = order[cur[i]];
+            uint64_t best = 0;
+            int any = 0;
+            for (uint32_t t = 0; t < OR_LIST; t++) {
+                uint64_t k = lists[i][t];
+                if (!k) continue;
+                any = 1;
+                uint32_t n = 0xFFFFFFFFu - (uint32_t)(k & 0xFFFFFFFFu);
+                if (claimed[n]) continue;
+                if (pd->anti_affinity[j] == 2 && claimed_az[pd->app[j] * OR_ZONES + nd->zone[n]]) continue;
+                if (k > best) best = k;
+            }
+            won[i] = -2;
+            if (best) {
+                uint32_t n = 0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFu);
+                claimed[n] = 1;
+                if (pd->anti_affinity[j] == 2) claimed_az[pd->app[j] * OR_ZONES + nd->zone[n]] = 1;
+                won[i] = (int32_t)n;
+                if (best_key) best_key[j] = best;
+            } else if (any) {
+                pend[npend++] = cur[i];
+            } else {
+                won[i] = -1;
+                if (best_key) best_key[j] = 0;
+            }
+        }
+        /* apply the batch, then re-score the claimed nodes for every type */
+        uint32_t chg[OR_LIST], nchg = 0;
+        for (uint32_t i = 0; i < nb; i++) {
+            uint32_t j = order[cur[i]];
+            if (won[i] == -2) continue;
+            placement[j] = won[i];
+            if (won[i] >= 0) {
+                uint32_t n = (uint32_t)won[i];
+                or_reserve(nd, pd, j, n, +1);
+                present[(size_t)pd->app[j] * N + n] = 1;
+                zcount[pd->app[j] * OR_ZONES + nd->zone[n]]++;
+                chg[nchg++] = n;
+            }
+        }
+        int64_t T_ = bs.T;
+#pragma omp parallel for num_threads(nthreads) if (nthreads > 1 && T_ >= 16)
+        for (int64_t u = 0; u < T_; u++) {
+            for (uint32_t c = 0; c < nchg; c++) {
+                const uint32_t n = chg[c];
+                const int z = nd->zone[n];
+                uint64_t *b = bs.types[u].tree + zoff[z];
+                uint32_t v = zM[z] + leaf[n];
+                b[v] = node_key(cfg, nd, pd, n, bs.types[u].rep, 0, 0, NULL);
+                for (v >>= 1; v >= 1; v >>= 1) {
+                    const uint64_t m = b[2 * v] > b[2 * v + 1] ? b[2 * v] : b[2 * v + 1];
+                    if (b[v] == m) break;
+                    b[v] = m;
+                }
+            }
+        }
+        uint32_t take = batch - npend;
+        if (take > P - cursor) take = P - cursor;
+        for (uint32_t i = 0; i < npend; i++) cur[i] = pend[i];
+        for (uint32_t i = 0; i < take; i++) cur[npend + i] = cursor + i;
+        nb = npend + take;
+        cursor += take;
+    }
+    for (uint32_t u = 0; u < bs.T; u++) free(bs.types[u].tree);
+    free(bs.types); free(bs.htab); free(znodes); free(zbase); free(leaf);
+    free(order); free(present); free(zcount); free(claimed); free(claimed_az); free(lists);
+    return batches;
+}
+
 /* ---------------- spec/synth.md generator (independent restatement) ---------------- */
 static uint64_t sm_at(uint64_t seed, uint64_t c) {
     uint64_t z = seed + (c + 1) * 0x9E3779B97F4A7C15ULL;

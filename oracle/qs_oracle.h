@@ -74,6 +74,12 @@ int or_schedule_incremental(const or_config *cfg, or_nodes *nodes, const or_pods
 uint32_t or_schedule_batched(const or_config *cfg, or_nodes *nodes, const or_pods *pods,
                              uint32_t batch, int32_t *placement, uint64_t *best_key, int nthreads);
 
+/* The same batched stream with incremental lists (per pod type and zone a max tree over the
+ * nodes' keys; only the claimed nodes are re-scored per batch): identical results for Fit +
+ * Balanced (+ ext) profiles.  Returns 0xFFFFFFFF (nothing usable) for normalizing profiles. */
+uint32_t or_schedule_batched_incremental(const or_config *cfg, or_nodes *nodes, const or_pods *pods,
+                                         uint32_t batch, int32_t *placement, uint64_t *best_key, int nthreads);
+
 /* Reserve / Unreserve of pod j on node n (spec S7). */
 void or_reserve(or_nodes *nodes, const or_pods *pods, uint32_t j, uint32_t n, int sign);
 

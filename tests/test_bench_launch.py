@@ -140,3 +140,120 @@ def test_world2_transport_fallback(mode):
         p.join(60)
         assert p.exitcode == 0
     assert res == [(0, "rccl", ["mailbox"]), (1, "rccl", ["mailbox"])]
+
+
+_RUNS = [0]  # stream runs of this process on the failing transport's schedulers
+
+
+class _FakeStream:
+    """A prepared stream of the fake scheduler: fixed placements (identical on both ranks), a
+    configurable failure at the n-th run of the process (diagnostic runs included)."""
+
+    def __init__(self, owner, pods):
+        self.o, self.pods = owner, pods
+
+    def run(self, mode="exact"):
+        _RUNS[0] += 1
+        if self.o.fail_at == ("run", _RUNS[0]):
+            raise RuntimeError("QS_ETIMEOUT: resident lookahead stream timed out")
+        return {"engine_used": "lookahead", "resident": 1, "table_layout": "compact", "wall_s": 1e-3,
+                "kernels": {"resolve": {"s": 1e-3, "launches": 1}}}
+
+    def results(self):
+        import numpy as np
+        p = len(self.pods)
+        return np.arange(p, dtype=np.int32) % 7, np.zeros(p, np.uint64)
+
+    def stamps(self):
+        import numpy as np
+        return np.arange(len(self.pods), dtype=np.uint64) * 50
+
+    def free(self):
+        pass
+
+
+def _fake_scheduler_cls(rank, fail):
+    class FakeScheduler:
+        def __init__(self, cfg, device=0, shard=None):
+            self.fail_at = fail if (fail and fail[2] == rank) else None
+            self.fail_at = self.fail_at[:2] if self.fail_at else None
+            if self.fail_at == ("open", 1):
+                raise RuntimeError("QS_EDEVICE: hipIpcGetMemHandle failed")
+
+        def mailbox_export(self):
+            return bytes([rank]) * 8
+
+        def mailbox_connect(self, handles):
+            assert len(handles) == 2
+
+        def load_nodes(self, nodes):
+            self.nodes = nodes
+
+        def prepare(self, pods):
+            if self.fail_at == ("prepare", 1):
+                raise RuntimeError("QS_EINVAL: pod out of range")
+            return _FakeStream(self, pods)
+
+        def save_table(self):
+            pass
+
+        def restore_table(self):
+            pass
+
+        def read_nodes(self):
+            return {k: v.copy() for k, v in self.nodes.items()}
+
+        def close(self):
+            pass
+
+    return FakeScheduler
+
+
+def _rank_measure_fail(rank, port, q, fail):
+    """bench.measure_sharded with the REAL measure() / open_sched() / diag_runs() at world 2 over
+    gloo; only the library's Scheduler is a CPU fake whose rank fail[2] fails in phase fail[:2]
+    (mailbox open, prepare, or the n-th stream run).  Every rank must end on the same transport
+    (RCCL after a mailbox failure) without a collective mismatch (ADVICE r3 bench.py:339)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE="2",
+                      LOCAL_RANK=str(rank))
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "custom-k8s-scheduler_amd")]
+    import bench
+    import qsched
+
+    bench.WORKLOADS["config3"] = (3, 300, 2000, "config3 (small, fake scheduler)")
+    qsched.dist_unique_id = lambda: bytes(range(128))
+    fake = _fake_scheduler_cls(rank, fail)
+    mailbox_only = fake
+
+    class Sched:  # the mailbox transport fails as configured, the RCCL one never
+        def __new__(cls, cfg, device=0, shard=None):
+            if shard is not None and shard[2] is not None:
+                return _fake_scheduler_cls(rank, None)(cfg, device, shard)
+            return mailbox_only(cfg, device, shard)
+
+    qsched.Scheduler = Sched
+    cx = bench.Ctx(backend="gloo")
+    a = bench.parse(["--gpus", "2", "--steps", "3", "--warmup", "1"])
+    m = bench.measure_sharded(cx, a, "config3")
+    cx.dist.destroy_process_group()
+    q.put((rank, m["transport"], [t["transport"] for t in m["transport_tried"]]))
+
+
+@pytest.mark.parametrize("fail", [("open", 1, 1), ("prepare", 1, 0), ("run", 1, 1), ("run", 3, 0), ("run", 5, 1)],
+                         ids=["open-r1", "prepare-r0", "warmup-r1", "timed-step-r0", "diag-run-r1"])
+def test_world2_measure_fails_on_one_rank(fail):
+    import torch.multiprocessing as mp
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank_measure_fail, args=(r, port, q, fail)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert res == [(0, "rccl", ["mailbox"]), (1, "rccl", ["mailbox"])]

@@ -38,3 +38,23 @@ def test_invariants_catch_corruption(oracle):
     fin3["req_mem"][:] = 0
     fin3["pods"][0] = 0
     assert stream_invariants(nodes, pods, pl, fin3)["unschedulable_infeasible"] is False
+
+
+def test_batched_invariants(oracle):
+    """Batched mode (spec S11): the oracle's result satisfies conservation, capacity and required
+    anti-affinity; two pods of one hostname-anti-affinity app forced onto one node break the last."""
+    from qsched.checks import batched_invariants
+
+    nodes, pods = synth_generate(5, 400, 6000)
+    fin = {k: v.copy() for k, v in nodes.items()}
+    pl, _, _ = oracle.schedule_batched(fin, pods_from_struct(pods), nthreads=4)
+    r = batched_invariants(nodes, pods, pl, fin)
+    assert r["conservation"] and r["capacity"] and r["anti_affinity"], r
+    host = np.nonzero((pods["anti_affinity"] == 1) & (pl >= 0))[0]
+    a = pods["app"][host]
+    vals, cnt = np.unique(a, return_counts=True)
+    two = host[a == vals[np.argmax(cnt)]][:2]
+    assert two.size == 2
+    bad = pl.copy()
+    bad[two[1]] = bad[two[0]]
+    assert not batched_invariants(nodes, pods, bad, fin)["anti_affinity"]

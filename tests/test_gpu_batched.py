@@ -47,6 +47,22 @@ def test_batched_full_config5_invariants():
     assert (pl >= 0).mean() > 0.5
 
 
+def test_batched_full_config5_exact(oracle):
+    """BASELINE.json configs[4] at full size, bit for bit: every placement, claimed key and the final
+    table of the 10,000 x 200,000 batched stream against or_schedule_batched_incremental (identical to
+    or_schedule_batched, tests/test_oracle_incremental.py), plus the batch count."""
+    nodes, pods = synth_generate(5, 10000, 200000)
+    g_pl, g_keys, g_final, stats = run_gpu_batched(nodes, pods)
+    on = {k: v.copy() for k, v in nodes.items()}
+    o_pl, o_keys, o_nb = oracle.schedule_batched_incremental(on, pods_from_struct(pods), nthreads=16)
+    bad = np.nonzero(g_pl != o_pl)[0]
+    assert bad.size == 0, f"{bad.size} placements differ; first at pod {bad[0]}: gpu {g_pl[bad[0]]} oracle {o_pl[bad[0]]}"
+    assert np.array_equal(g_keys, o_keys)
+    for k in on:
+        assert np.array_equal(g_final[k], on[k]), k
+    assert stats["batches"] == o_nb
+
+
 def test_batched_then_exact_share_the_table(oracle):
     """A batched stream leaves the table (and its anti-affinity state) for the next stream."""
     nodes, pods = synth_generate(5, 500, 6000)

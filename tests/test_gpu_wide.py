@@ -83,11 +83,52 @@ def test_wide_config4_profile(engine):
 
 
 def test_wide_full_config2_shape():
-    """5,000 x 100,000 on the wide layout (the headline shape), every placement bit-exact."""
+    """5,000 x 100,000 on the wide layout (the headline shape) as the one-launch resident stream
+    (DESIGN.md §4.1e), every placement bit-exact."""
     nodes, pods = ki_cluster(5000, 100000, seed=3)
     g = run(nodes, pods, {})
     assert g[3]["table_layout"] == "wide" and g[3]["engine_used"] == "lookahead"
+    assert g[3]["resident"] == 1
     assert_exact(g, oracle_run(nodes, pods))
+
+
+@pytest.mark.parametrize("n,p,K,features", [(100, 1000, 32, False), (1500, 6000, 32, False), (5000, 20000, 32, False),
+                                            (9000, 7000, 32, False), (30000, 4000, 32, False), (1500, 6000, 7, False),
+                                            (3000, 2000, 1, False), (50000, 3000, 32, False), (40000, 3000, 32, True),
+                                            (2000, 5000, 16, True)])
+def test_wide_resident_stream(monkeypatch, n, p, K, features):
+    """The wide layout (f64 byte memory columns: odd-Ki allocatable, decimal requests) as the
+    resident stream across selector geometries (1 to 13 node chunks, one or two keys per merging
+    thread, amd.com/gpu, partial last windows, K = 1..32): bit-exact vs the oracle and identical to
+    the per-window launches (QS_RESIDENT=0)."""
+    # features: the config-4 cluster (amd.com/gpu requests) under the Fit + Balanced profile
+    nodes, pods = ki_cluster(n, p, seed=n + p, features=features)
+    cfg = {"engine": "lookahead", "lookahead": K}
+    g = run(nodes, pods, cfg)
+    assert g[3]["table_layout"] == "wide" and g[3]["resident"] == 1
+    assert_exact(g, oracle_run(nodes, pods))
+    monkeypatch.setenv("QS_RESIDENT", "0")
+    w = run(nodes, pods, cfg)
+    assert w[3]["resident"] == 0
+    assert np.array_equal(w[0], g[0]) and np.array_equal(w[1], g[1])
+
+
+@pytest.mark.parametrize("n,p,K", [(400, 14000, 32), (600, 12000, 32), (5000, 20000, 32), (3000, 5000, 7)])
+def test_wide_resident_stream_norm(monkeypatch, n, p, K):
+    """All four plugins + amd.com/gpu on the wide layout as ONE resident launch (in-launch maxima,
+    the lost-maximum test and the parked waves' exact rescans); the tight cluster
+    takes the rescan path."""
+    nodes, pods = ki_cluster(n, p, seed=n + 3 * p, features=True)
+    cfg = dict(enable_taint=1, enable_affinity=1)
+    g = run(nodes, pods, dict(cfg, engine="lookahead", lookahead=K))
+    assert g[3]["table_layout"] == "wide" and g[3]["resident"] == 1
+    assert_exact(g, oracle_run(nodes, pods, cfg))
+    if n == 400:
+        assert g[3]["truncations"] > 0 and g[3]["resumed_windows"] > 0
+    monkeypatch.setenv("QS_RESIDENT", "0")
+    w = run(nodes, pods, dict(cfg, engine="lookahead", lookahead=K))
+    assert w[3]["resident"] == 0
+    assert np.array_equal(w[0], g[0]) and np.array_equal(w[1], g[1])
 
 
 def test_wide_batched():

@@ -1,5 +1,6 @@
 """The incremental-argmax oracle (or_schedule_incremental) against the brute-force oracle
-(or_schedule), bit for bit: placements, per-pod best keys and the final node table.
+(or_schedule), bit for bit: placements, per-pod best keys and the final node table; likewise the
+incremental batched oracle (or_schedule_batched_incremental) against or_schedule_batched.
 
 or_schedule_incremental keeps, per pod type (requests, non-zero requests, extended requests, QoS
 class), a max tree over the nodes' packed keys and re-scores only the reserved node per pod; it
@@ -70,3 +71,40 @@ def test_incremental_rejects_normalizing_profiles(oracle):
     with pytest.raises(ValueError):
         oracle.schedule_incremental({k: v.copy() for k, v in nodes.items()}, pods_from_struct(pods),
                                     dict(enable_taint=1, enable_affinity=1))
+
+
+def both_batched(oracle, nodes, pods, batch=64, cfg=None, nthreads=4):
+    a = {k: v.copy() for k, v in nodes.items()}
+    b = {k: v.copy() for k, v in nodes.items()}
+    sub = pods_from_struct(pods)
+    p1, k1, n1 = oracle.schedule_batched(a, sub, batch=batch, cfg=cfg, nthreads=nthreads)
+    p2, k2, n2 = oracle.schedule_batched_incremental(b, sub, batch=batch, cfg=cfg, nthreads=nthreads)
+    return (p1, k1, n1, a), (p2, k2, n2, b)
+
+
+@pytest.mark.parametrize("config,n,p,batch", [(5, 1000, 20000, 64), (5, 300, 9000, 7), (5, 200, 2000, 1),
+                                              (5, 64, 3000, 64), (2, 2000, 30000, 64), (4, 800, 12000, 64),
+                                              (1, 100, 1000, 32)])
+def test_batched_incremental_matches_brute_force(oracle, config, n, p, batch):
+    """Per-type per-zone max trees + a best-first walk over the allowed zones give each pod the same
+    64-entry list as the brute-force scan (hostname / zone anti-affinity, carried pods, tight
+    clusters where most pods are unschedulable or carried)."""
+    x, y = both_batched(oracle, *synth_generate(config, n, p), batch=batch)
+    assert_equal(x, y)
+
+
+def test_batched_incremental_tight_zones(oracle):
+    """Few nodes per zone, many zone-anti-affinity pods: most lists run out of allowed zones."""
+    nodes, pods = synth_generate(5, 120, 6000, seed=3)
+    nodes["zone"][:] = np.arange(120) % 3
+    pods["anti_affinity"][::2] = 2
+    x, y = both_batched(oracle, nodes, pods)
+    assert_equal(x, y)
+    assert (x[0] < 0).mean() > 0.2
+
+
+def test_batched_incremental_rejects_normalizing_profiles(oracle):
+    nodes, pods = synth_generate(4, 100, 100)
+    with pytest.raises(ValueError):
+        oracle.schedule_batched_incremental({k: v.copy() for k, v in nodes.items()}, pods_from_struct(pods),
+                                            cfg=dict(enable_taint=1))
