@@ -302,30 +302,61 @@ def host_info():
             "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
-def cpu_baseline(nodes, pods, n_nodes, n_pods, sample, threads=1, gpu_placement=None):
+def cpu_baseline(nodes, pods, n_nodes, n_pods, sample, threads=1, gpu_placement=None, repeats=5):
     """Oracle (C restatement) on the same stream: 1 thread, or the node-parallel OpenMP arm
     (SURVEY §8(d) arm 2: upstream's Parallelizer runs 16 workers).  sample = 0 runs the whole
-    stream, and its placements are diffed against the GPU's (`placements_match`)."""
+    stream, and its placements are diffed against the GPU's (`placements_match`).  The value is the
+    median of `repeats` runs (median of 5); every run's rate is listed."""
     from oracle import oracle as O
 
     whole = sample <= 0 or sample >= n_pods
     sample = n_pods if whole else sample
     sub = qsched.pods_from_struct(pods[:sample])
-    on = {k: v.copy() for k, v in nodes.items()}
-    t0 = time.perf_counter()
-    placement, _, _ = O.schedule(on, sub, nthreads=threads)
-    dt = time.perf_counter() - t0
+    times, placement = [], None
+    for _ in range(repeats):
+        on = {k: v.copy() for k, v in nodes.items()}
+        t0 = time.perf_counter()
+        pl, _, _ = O.schedule(on, sub, nthreads=threads)
+        times.append(time.perf_counter() - t0)
+        placement = pl if placement is None else placement
+    dt = float(np.median(times))
     how = "1 thread" if threads == 1 else f"{threads} OpenMP threads over the nodes of each pod"
     what = (f"the whole {n_pods:,}-pod stream" if whole else
-            f"first {sample} of the {n_pods:,} pods (QoS-sorted within the sample)")
+            f"first {sample:,} of the {n_pods:,} pods (QoS-sorted within the sample)")
     out = {"value": round(sample / dt, 1), "unit": "pods/s", "cores": threads, "kind": "port",
            "host": host_info(),
            "sample": f"{what} onto the empty {n_nodes:,}-node cluster, oracle/qs_oracle.c {how}, "
-                     f"{dt:.2f} s",
+                     f"median of {repeats} runs, {dt:.2f} s each",
+           "runs_pods_per_s": [round(sample / t, 1) for t in times],
            "evals_per_s": round(sample * n_nodes / dt, 1)}
     if whole and gpu_placement is not None:
         out["placements_match"] = bool(np.array_equal(placement, gpu_placement))
     return out
+
+
+def cpu_baseline_framework(n_nodes=5000, sample=4000, threads=16, repeats=5):
+    """The north_star's baseline shape (BASELINE.json:5, configs[0] :7): the CPU reference plugins
+    (host/cpu_plugins.cpp: NodeResourcesFit + LeastAllocated, BalancedAllocation, QoS-class profile
+    weights) through the framework runtime (Run*Plugins, upstream's 16-worker node Parallelizer,
+    deterministic selectHost) on config 2's cluster as k8s objects, timed by tools/cpu_framework.cpp
+    (Go is absent: the plugin set is C++).  Median of `repeats`; placements diffed against the
+    oracle on the same pods inside the tool."""
+    import subprocess
+    exe = os.path.join(ROOT, "custom-k8s-scheduler_amd", "cpu_framework")
+    runs = []
+    for _ in range(repeats):
+        r = subprocess.run([exe, "2", str(n_nodes), str(sample), str(threads)], capture_output=True, text=True,
+                           timeout=300)
+        runs.append(json.loads(r.stdout.strip().splitlines()[-1]))
+    med = sorted(runs, key=lambda x: x["pods_per_s"])[len(runs) // 2]
+    return {"value": med["pods_per_s"], "unit": "pods/s", "cores": threads, "kind": "port",
+            "host": host_info(),
+            "sample": f"first {sample:,} pods of config 2 (QoS-sorted) onto the empty {n_nodes:,}-node cluster "
+                      "as k8s objects: CPU plugins through the framework runtime (tools/cpu_framework.cpp), "
+                      f"{threads}-worker Parallelizer, median of {repeats} runs, {med['seconds']:.2f} s each",
+            "runs_pods_per_s": [x["pods_per_s"] for x in runs],
+            "evals_per_s": med["evals_per_s"],
+            "placements_match": all(x["placements_match"] for x in runs)}
 
 
 def measure(cx, a, workload, steps, warmup, with_diag=True):
@@ -751,6 +782,11 @@ def main():
             out["cpu_baseline_parallel"] = cpu_baseline(m["nodes"], m["pods"], m["n_nodes"], m["n_pods"],
                                                         a.cpu_sample, threads=16,
                                                         gpu_placement=m["placement"])
+            usable = host_info()["usable_cpus"] or os.cpu_count() or 16
+            if usable != 16:  # the OpenMP arm at every CPU this process may use (a bounded sample)
+                out["cpu_baseline_parallel_nproc"] = cpu_baseline(m["nodes"], m["pods"], m["n_nodes"], m["n_pods"],
+                                                                  20000, threads=usable)
+            out["cpu_baseline_framework"] = cpu_baseline_framework()
         print(json.dumps(out), flush=True)
     if cx.dist is not None:
         cx.dist.destroy_process_group()

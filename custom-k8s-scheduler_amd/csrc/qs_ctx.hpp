@@ -126,7 +126,7 @@ struct qs_ctx {
     bool mirror_stale = false;  // device table changed since the last mirror sync
     uint64_t device_faults = 0; // QS_EDEVICE results so far (each one drops the device table)
     qs_host::DevBuf diag;
-    qs_host::DevBuf scratch, lists, clists, dio, npart, normi, nstat, nfall, nrec, bctrl, one_pod, one_podx, out_feas, out_score, out_total;
+    qs_host::DevBuf scratch, lists, clists, dio, npart, normi, nstat, nfall, nrec, bctrl, one_pod, one_podx;
     void *pin = nullptr;   // qs_score_pod's packed outputs, written by the kernel (pinned host memory)
     size_t pin_bytes = 0;
     uint64_t score_seq = 0;  // the kernel's done word for the call in flight

@@ -476,19 +476,30 @@ __device__ __forceinline__ double fraction(int32_t a, int32_t r, double y) {
     return r >= a ? 1.0 : q;
 }
 
-// Wide layout (memory in f64 bytes, every value < 2^46, so (a - r) * 100 and q * a are exact):
-// floor((a - reqd) * 100 / a) from the f64 quotient and a one-step integer correction (SURVEY.md
-// A.4 note): n * RN(1/a) is within 100 * 2^-52 of n / a, i.e. within one of the floor.
+// Wide layout (memory in f64 bytes, every value < 2^46, so (a - r) * 100 is exact):
+// floor((a - reqd) * 100 / a) from the f64 quotient (within one of the floor: n * RN(1/a) is within
+// 100 * 2^-52 of n / a) and one integer correction from the remainder n - q * a, which fma gives
+// exactly (an integer below 2a in magnitude).  Branch-free; tests/native/exact_arith.c mode 4.
 __device__ __forceinline__ uint32_t least_requested_w(double a, double reqd, double ya) {
     const double rq = reqd < a ? reqd : a;
     const double n = (a - rq) * 100.0;
     double q = __builtin_trunc(n * ya);
-    if (q * a > n) q -= 1.0;
-    else if ((q + 1.0) * a <= n) q += 1.0;
+    const double r = __builtin_fma(-q, a, n);
+    q = r < 0.0 ? q - 1.0 : q;
+    q = (r >= a && a > 0.0) ? q + 1.0 : q;  // (a = 0: score 0, as upstream's capacity == 0 case)
     return reqd > a ? 0u : (uint32_t)q;
 }
-// min(RN(r / a), 1): IEEE division (correctly rounded; -ffp-contract=off, no fast-math)
-__device__ __forceinline__ double fraction_w(double a, double r) { return r >= a ? 1.0 : r / a; }
+// min(RN(r / a), 1) for the wide layout: the Markstein quotient of `fraction` with y = RN(1/a) (the
+// row's ym).  Exact for integers r < a <= 2^46: q0 = RN(r y) lies within 1.5 ulp of r / a, so the
+// remainder r - q0 a is a multiple of ulp(q0) below 2^48 of them (exact in the fma), and q0 + rem y
+// is within 2^-52 ulp of r / a, which lies at least ulp / 2a from every rounding midpoint
+// (spec/semantics.md S10; tests/native/exact_arith.c mode 4).
+__device__ __forceinline__ double fraction_w(double a, double r, double y) {
+    const double q0 = r * y;
+    const double rem = __builtin_fma(-q0, a, r);
+    const double q = __builtin_fma(rem, y, q0);
+    return r >= a ? 1.0 : q;
+}
 
 // ---- spec S5/S6: QoS-weighted total of one feasible node ------------------------------------
 // LeastAllocated (UP least_allocated.go#leastResourceScorer), NonZeroRequested + pod nz.
@@ -519,7 +530,7 @@ __device__ __forceinline__ uint32_t ba_score(const R &r, const P &p, const DevCf
     const bool hc = r.ac != 0, hm = r.am != 0;
     const double f0 = fraction(r.ac, r.rc + p.rc, r.yc);
     double f1;
-    if constexpr (std::is_same<R, RowW>::value) f1 = fraction_w(r.am, r.rm + p.rm);
+    if constexpr (std::is_same<R, RowW>::value) f1 = fraction_w(r.am, r.rm + p.rm, r.ym);
     else f1 = fraction(r.am, r.rm + p.rm, r.ym);
     double sd = 0.0;
     if (hc & hm) sd = __builtin_fabs((f0 - f1) / 2);

@@ -945,122 +945,135 @@ static qs_status reserve_impl(qs_ctx *c, uint32_t node, const qs_pod *p, int sig
 qs_status qs_reserve(qs_ctx *c, uint32_t node, const qs_pod *p) { return reserve_impl(c, node, p, +1); }
 qs_status qs_unreserve(qs_ctx *c, uint32_t node, const qs_pod *p) { return reserve_impl(c, node, p, -1); }
 
-// The packed outputs of the one-launch score (pinned host memory, written by the kernel) into the
-// caller's arrays: 16 nodes per step as vectors (the pinned lines come from DRAM once; the byte scores
-// widen to the four int32 plugin scores), the tail one by one.
-static void unpack_scores(const int32_t *tot, const uint32_t *sco, uint32_t n, uint8_t *feas, int32_t *score,
+// The packed outputs of the one-launch score (pinned host memory, written by the kernel: one u32 of
+// four byte scores per node, 0xFFFFFFFF = infeasible) into the caller's arrays, 16 nodes per step as
+// vectors: feasible = not the sentinel, the four int32 plugin scores (0 where infeasible) and the
+// QoS-weighted total (w = {wfit, wbal, wtt, wna}: the sums node_total forms, -1 where infeasible).
+static void unpack_scores(const uint32_t *pk, uint32_t n, const uint32_t w[4], uint8_t *feas, int32_t *score,
                           int32_t *total) {
+    typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
     typedef int32_t i32x16 __attribute__((ext_vector_type(16)));
     typedef uint8_t u8x16 __attribute__((ext_vector_type(16)));
+    typedef uint8_t u8x64 __attribute__((ext_vector_type(64)));
+    typedef int32_t i32x64 __attribute__((ext_vector_type(64)));
     uint32_t i = 0;
     for (; i + 16 <= n; i += 16) {
-        i32x16 t;
-        std::memcpy(&t, tot + i, sizeof t);
-        if (total) std::memcpy(total + i, &t, sizeof t);
+        u32x16 v;
+        std::memcpy(&v, pk + i, sizeof v);
+        const i32x16 ok = v != kScoreInfeasible;  // -1 (all ones) where feasible
+        const u32x16 z = v & (u32x16)ok;           // infeasible -> 0
         if (feas) {
-            const u8x16 f = __builtin_convertvector(t >= 0, u8x16) & (uint8_t)1;
+            const u8x16 f = __builtin_convertvector(ok, u8x16) & (uint8_t)1;
             std::memcpy(feas + i, &f, sizeof f);
         }
-        if (score)
-            for (uint32_t q = 0; q < 4; ++q) {
-                u8x16 b;
-                std::memcpy(&b, sco + i + 4 * q, sizeof b);
-                const i32x16 w = __builtin_convertvector(b, i32x16);
-                std::memcpy(score + 4 * (size_t)(i + 4 * q), &w, sizeof w);
-            }
+        if (total) {
+            const u32x16 t = (z & 255u) * w[0] + ((z >> 8) & 255u) * w[1] + ((z >> 16) & 255u) * w[2] + (z >> 24) * w[3];
+            const i32x16 r = ((i32x16)t & ok) | ~ok;  // -1 where infeasible
+            std::memcpy(total + i, &r, sizeof r);
+        }
+        if (score) {
+            u8x64 b;
+            std::memcpy(&b, &z, sizeof b);
+            const i32x64 wd = __builtin_convertvector(b, i32x64);
+            std::memcpy(score + 4 * (size_t)i, &wd, sizeof wd);
+        }
     }
     for (; i < n; ++i) {
-        if (total) total[i] = tot[i];
-        if (feas) feas[i] = tot[i] >= 0;
+        const bool f = pk[i] != kScoreInfeasible;
+        const uint32_t z = f ? pk[i] : 0u;
+        if (feas) feas[i] = f;
         if (score)
-            for (uint32_t k = 0; k < 4; ++k) score[4 * (size_t)i + k] = (int32_t)((sco[i] >> (8 * k)) & 255u);
+            for (uint32_t k = 0; k < 4; ++k) score[4 * (size_t)i + k] = (int32_t)((z >> (8 * k)) & 255u);
+        if (total)
+            total[i] = f ? (int32_t)((z & 255u) * w[0] + ((z >> 8) & 255u) * w[1] + ((z >> 16) & 255u) * w[2] +
+                                     (z >> 24) * w[3])
+                         : -1;
     }
+}
+
+// The one-launch score of one pod into the context's pinned buffer: pod by value,
+// the previous Reserve's row folded in, outputs written by the kernel into pinned host memory,
+// completion seen by polling its done word (no copy command, no stream sync).  Returns the packed
+// per-node words (valid until the next call on the context); *wts = {wfit, wbal, wtt, wna}.
+static const uint32_t *score_pod_launch(qs_ctx *c, const qs_pod *pod, uint32_t wts[4], int32_t *best) {
+    if (!pod) fail(QS_EINVAL, "null pod");
+    HIPCHK(hipSetDevice(c->device));
+    check_pod(*pod, 0);
+    if (!pod_fits_layout(c, *pod)) {
+        flush_pending(c);  // (a re-layout re-uploads the table from the mirror)
+        ensure_layout(c, pod, 1);
+    }
+    const uint32_t n = c->m.n;
+    alignas(16) uint8_t dp[sizeof(DPodW)];
+    compact_pod(c, *pod, 0, c->shift, c->wide, dp);
+    if (c->wide) {
+        const DPodW *q = reinterpret_cast<const DPodW *>(dp);
+        wts[0] = q->wfit; wts[1] = q->wbal;
+    } else {
+        const DPod *q = reinterpret_cast<const DPod *>(dp);
+        wts[0] = q->wfit; wts[1] = q->wbal;
+    }
+    DevCfg dc = c->dc;
+    dc.feat = feat_of(c->cfg) | ((pod->req_ext[0] || pod->req_ext[1]) ? kFeatExt : 0u) |
+              (c->wide ? kFeatWide | kFeatExt : 0u);
+    wts[2] = (dc.feat & kFeatTaint) ? (uint32_t)dc.wtt : 0u;
+    wts[3] = (dc.feat & kFeatAffinity) ? (uint32_t)dc.wna : 0u;
+    if (n == 0 || !c->dev_valid) {
+        if (best) *best = -1;
+        return nullptr;
+    }
+    const DPodX dx = compact_podx(c, *pod);
+    const size_t pb = score_pod1_pack_bytes(n);
+    if (c->pin_bytes < pb) {
+        if (c->pin) (void)hipHostFree(c->pin);
+        c->pin = nullptr;
+        c->pin_bytes = 0;
+        HIPCHK(hipHostMalloc(&c->pin, pb, hipHostMallocDefault));
+        c->pin_bytes = pb;
+        std::memset(c->pin, 0, pb);
+    }
+    if (!c->score_gs.p) {
+        c->score_gs.ensure(32);
+        HIPCHK(hipMemsetAsync(c->score_gs.p, 0, 32, c->stream));
+    }
+    const uint32_t pidx = c->pend < n ? c->pend : 0xFFFFFFFFu;
+    const HostRow prow = pidx < n ? compact_row(c->m, pidx, c->shift, c->wide) : HostRow{};
+    const uint64_t seq = ++c->score_seq;
+    HIPCHK(launch_score_pod1(c->dt, dp, &dx, dc, static_cast<uint8_t *>(c->pin), c->score_gs.as<uint64_t>(), seq,
+                             pidx, prow, c->stream));
+    c->pend = 0xFFFFFFFFu;
+    // the done word: polled (bounded), then the stream is checked for an error
+    volatile uint64_t *done = reinterpret_cast<volatile uint64_t *>(static_cast<uint8_t *>(c->pin) + 8);
+    const auto t0 = std::chrono::steady_clock::now();
+    while (*done != seq) {
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) {
+            HIPCHK(hipStreamSynchronize(c->stream));  // a fault surfaces here
+            if (*done != seq) fail(QS_EDEVICE, "qs_score_pod: the scoring kernel did not complete");
+            break;
+        }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    const uint8_t *h = static_cast<const uint8_t *>(c->pin);
+    uint64_t kbest = 0;
+    std::memcpy(&kbest, h, 8);
+    if (best) *best = kbest ? (int32_t)(0xFFFFFFFFu - (uint32_t)kbest) : -1;
+    return reinterpret_cast<const uint32_t *>(h + 16);
 }
 
 qs_status qs_score_pod(qs_ctx *c, const qs_pod *pod, uint8_t *feas, int32_t *score, int32_t *total,
                        int32_t *best) {
     return guarded(c, [&] {
-        if (!pod) fail(QS_EINVAL, "null pod");
-        HIPCHK(hipSetDevice(c->device));
-        const uint32_t n = c->m.n;
-        check_pod(*pod, 0);
-        if (!pod_fits_layout(c, *pod)) ensure_layout(c, pod, 1);
-        if (n > 0 && n <= score_pod1_max_nodes() && c->dev_valid) {
-            // the framework path's one-launch form (VERDICT r2 "do this" #5): pod by value, the
-            // previous Reserve's row folded in, outputs written by the kernel into pinned host
-            // memory, completion seen by polling its done word (no copy command, no stream sync)
-            alignas(16) uint8_t dp[sizeof(DPodW)];
-            compact_pod(c, *pod, 0, c->shift, c->wide, dp);
-            const DPodX dx = compact_podx(c, *pod);
-            DevCfg dc = c->dc;
-            dc.feat = feat_of(c->cfg) | ((pod->req_ext[0] || pod->req_ext[1]) ? kFeatExt : 0u) |
-                      (c->wide ? kFeatWide | kFeatExt : 0u);
-            const size_t pb = score_pod1_pack_bytes(n);
-            if (c->pin_bytes < pb) {
-                if (c->pin) (void)hipHostFree(c->pin);
-                c->pin = nullptr;
-                c->pin_bytes = 0;
-                HIPCHK(hipHostMalloc(&c->pin, pb, hipHostMallocDefault));
-                c->pin_bytes = pb;
-                std::memset(c->pin, 0, pb);
-            }
-            if (!c->score_gs.p) {
-                c->score_gs.ensure(32);
-                HIPCHK(hipMemsetAsync(c->score_gs.p, 0, 32, c->stream));
-            }
-            const uint32_t pidx = c->pend < n ? c->pend : 0xFFFFFFFFu;
-            const HostRow prow = pidx < n ? compact_row(c->m, pidx, c->shift, c->wide) : HostRow{};
-            const uint64_t seq = ++c->score_seq;
-            HIPCHK(launch_score_pod1(c->dt, dp, &dx, dc, static_cast<uint8_t *>(c->pin), c->score_gs.as<uint64_t>(), seq, pidx, prow, c->stream));
-            c->pend = 0xFFFFFFFFu;
-            // the done word: polled (bounded), then the stream is checked for an error
-            volatile uint64_t *done = reinterpret_cast<volatile uint64_t *>(static_cast<uint8_t *>(c->pin) + 8);
-            const auto t0 = std::chrono::steady_clock::now();
-            while (*done != seq) {
-                if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) {
-                    HIPCHK(hipStreamSynchronize(c->stream));  // a fault surfaces here
-                    if (*done != seq) fail(QS_EDEVICE, "qs_score_pod: the scoring kernel did not complete");
-                    break;
-                }
-            }
-            std::atomic_thread_fence(std::memory_order_acquire);
-            const uint8_t *h = static_cast<const uint8_t *>(c->pin);
-            uint64_t kbest = 0;
-            std::memcpy(&kbest, h, 8);
-            const int32_t *tot = reinterpret_cast<const int32_t *>(h + 16);
-            const uint32_t *sco = reinterpret_cast<const uint32_t *>(h + 16 + 4 * (size_t)n);
-            unpack_scores(tot, sco, n, feas, score, total);
-            if (best) *best = kbest ? (int32_t)(0xFFFFFFFFu - (uint32_t)kbest) : -1;
-            return;
-        }
-        flush_pending(c);
-        alignas(16) uint8_t dp[sizeof(DPodW)];
-        compact_pod(c, *pod, 0, c->shift, c->wide, dp);
-        const DPodX dx = compact_podx(c, *pod);
-        c->dc.feat = feat_of(c->cfg) | ((pod->req_ext[0] || pod->req_ext[1]) ? kFeatExt : 0u) |
-                     (c->wide ? kFeatWide | kFeatExt : 0u);
-        c->one_pod.ensure(sizeof(DPodW));
-        c->one_podx.ensure(sizeof(DPodX));
-        c->out_feas.ensure(std::max<size_t>(n, 1));
-        c->out_score.ensure(std::max<size_t>(16 * (size_t)n, 16));
-        c->out_total.ensure(std::max<size_t>(4 * (size_t)n, 4));
-        HIPCHK(hipMemcpyAsync(c->one_pod.p, dp, pod_record_bytes(c->wide), hipMemcpyHostToDevice, c->stream));
-        HIPCHK(hipMemcpyAsync(c->one_podx.p, &dx, sizeof dx, hipMemcpyHostToDevice, c->stream));
-        HIPCHK(hipMemsetAsync(c->scratch.p, 0, scan_scratch_bytes(), c->stream));
-        if (n) {
-            ensure_soa(c);
-            HIPCHK(launch_scan_pod(c->dt, c->one_pod.p, c->one_podx.as<DPodX>(), 0, c->dc,
-                                   c->scratch.p, nullptr, nullptr, nullptr, c->out_feas.as<uint8_t>(),
-                                   c->out_score.as<int32_t>(), c->out_total.as<int32_t>(), 3,
-                                   c->stream));  // scan + reduce (no Reserve: out_node == nullptr)
-        }
-        unsigned long long kbest = 0;
-        HIPCHK(hipMemcpyAsync(&kbest, c->scratch.p, 8, hipMemcpyDeviceToHost, c->stream));
-        if (feas && n) HIPCHK(hipMemcpyAsync(feas, c->out_feas.p, n, hipMemcpyDeviceToHost, c->stream));
-        if (score && n) HIPCHK(hipMemcpyAsync(score, c->out_score.p, 16 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
-        if (total && n) HIPCHK(hipMemcpyAsync(total, c->out_total.p, 4 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));
-        if (best) *best = kbest ? (int32_t)(0xFFFFFFFFu - (uint32_t)kbest) : -1;
+        uint32_t w[4];
+        const uint32_t *pk = score_pod_launch(c, pod, w, best);
+        if (pk) unpack_scores(pk, c->m.n, w, feas, score, total);
+    }, /*keep_pending=*/true);
+}
+
+qs_status qs_score_pod_packed(qs_ctx *c, const qs_pod *pod, const uint32_t **packed, int32_t *best) {
+    return guarded(c, [&] {
+        uint32_t w[4];
+        const uint32_t *pk = score_pod_launch(c, pod, w, best);
+        if (packed) *packed = pk;
     }, /*keep_pending=*/true);
 }
 

@@ -337,16 +337,21 @@ __device__ __forceinline__ void host_row_regs(const HostRow &v, RowT<F> &r, RowX
     if (F & (kFeatTaint | kFeatAffinity)) { x.th = v.th; x.ts = v.ts; x.lb0 = v.lb0; x.lb1 = v.lb1; }
 }
 
-// qs_score_pod for tables up to kScorePod1Max nodes (the framework-embedded path, one call per pod,
-// DESIGN.md §4.6): ONE 1024-thread workgroup, the pod record and its extension passed by value (no
-// H2D), the normalize maxima and the keys in the same launch (two passes over the L2-resident rows,
-// separated by a barrier), and every output written straight into pinned host memory (no D2H
-// command): [best key u64 | done u64 | total i32 x n (-1 = infeasible) | plugin scores u8 x 4n];
+// qs_score_pod (the framework-embedded path, one call per pod): the pod record and
+// its extension passed by value (no H2D), every output written straight into pinned host memory (no
+// D2H command): [best key u64 | done u64 | packed u32 x n], packed = the four plugin scores (0..100)
+// as bytes {LeastAllocated, Balanced, TaintToleration, NodeAffinity}, 0xFFFFFFFF = infeasible (the
+// host derives the QoS-weighted total from them: 4 bytes per node cross the host link);
 // `done` = seq, stored last with a system-scope release after every thread's system fence, is what
 // the host polls.  A pending row (the previous qs_reserve / qs_unreserve, folded into this launch)
 // is written to the table by thread 0 and used from the argument by the thread that scores it.
+// k_score_pod1 (ONE 1024-thread workgroup, normalize maxima and keys in the same launch, two passes
+// separated by a barrier) is the form without the device words, for tables up to kScorePod1Max.
 constexpr uint32_t kScorePod1Max = 16384;
-__host__ __device__ constexpr size_t score_pack_bytes(uint32_t n) { return 16 + 4 * (size_t)n + 4 * (size_t)n; }
+__host__ __device__ constexpr size_t score_pack_bytes(uint32_t n) { return 16 + 4 * (size_t)n; }
+__device__ __forceinline__ uint32_t pack_scores(bool f, const uint32_t (&sco)[4]) {
+    return f ? (sco[0] | (sco[1] << 8) | (sco[2] << 16) | (sco[3] << 24)) : kScoreInfeasible;
+}
 template <uint32_t F>
 __global__ __launch_bounds__(1024) void k_score_pod1(DevTable t, PodT<F> p, DPodX px, DevCfg c, uint8_t *hout,
                                                      uint64_t seq, uint32_t pidx, HostRow prow) {
@@ -354,8 +359,7 @@ __global__ __launch_bounds__(1024) void k_score_pod1(DevTable t, PodT<F> p, DPod
     __shared__ uint32_t red[2][NW];
     __shared__ uint64_t redk[NW];
     const uint32_t n = t.n, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    int32_t *total = reinterpret_cast<int32_t *>(hout + 16);
-    uint32_t *score = reinterpret_cast<uint32_t *>(hout + 16 + 4 * (size_t)n);
+    uint32_t *packed = reinterpret_cast<uint32_t *>(hout + 16);
     RowT<F> pr;
     RowX prx;
     host_row_regs<F>(prow, pr, prx);
@@ -398,9 +402,7 @@ __global__ __launch_bounds__(1024) void k_score_pod1(DevTable t, PodT<F> p, DPod
         const uint32_t tot = node_total<F>(r, x, p, px, c, mt, ymt, ma, yma, sco);
         const uint64_t key = f ? pack_key(tot + 1, i) : 0ull;
         best = key > best ? key : best;
-        // plugin scores are 0..100: one byte each
-        total[i] = f ? (int32_t)tot : -1;
-        score[i] = f ? (sco[0] | (sco[1] << 8) | (sco[2] << 16) | (sco[3] << 24)) : 0u;
+        packed[i] = pack_scores(f, sco);  // plugin scores are 0..100: one byte each
     }
     best = wave_max_u64(best);
     if (lane == 0) redk[wv] = best;
@@ -479,9 +481,7 @@ __global__ __launch_bounds__(kScorePodGT) void k_score_podg(DevTable t, PodT<F> 
         uint32_t sco[4];
         const uint32_t tot = node_total<F>(r, x, p, px, c, mt, rcp_exact(mt), ma, rcp_exact(ma), sco);
         best = f ? pack_key(tot + 1, i) : 0ull;
-        reinterpret_cast<int32_t *>(hout + 16)[i] = f ? (int32_t)tot : -1;
-        reinterpret_cast<uint32_t *>(hout + 16 + 4 * (size_t)n)[i] =
-            f ? (sco[0] | (sco[1] << 8) | (sco[2] << 16) | (sco[3] << 24)) : 0u;
+        reinterpret_cast<uint32_t *>(hout + 16)[i] = pack_scores(f, sco);
     }
     best = wave_max_u64(best);
     if (lane == 0) redk[wv] = best;
@@ -3464,7 +3464,7 @@ static hipError_t scan_pod_f(const DevTable &t, const void *pods_, const DPodX *
 template <uint32_t F>
 static hipError_t score_pod1_f(const DevTable &t, const void *pod, const DPodX *podx, const DevCfg &c, uint8_t *hout,
                                uint64_t *gs, uint64_t seq, uint32_t pidx, const HostRow &prow, hipStream_t stream) {
-    if (t.n > kScorePod1Max) return hipErrorInvalidValue;
+    if (!gs && t.n > kScorePod1Max) return hipErrorInvalidValue;
     PodT<F> p;
     std::memcpy(&p, pod, sizeof p);
     DPodX px{};

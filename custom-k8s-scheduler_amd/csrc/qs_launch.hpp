@@ -51,12 +51,14 @@ hipError_t launch_scan_pod(const DevTable &t, const void *pods, const DPodX *pod
                            uint64_t *stamps, uint8_t *feas, int32_t *score, int32_t *total,
                            int part, hipStream_t stream);  // part: 1 keys (+norm), 2 commit
 hipError_t launch_rows_to_soa(const DevTable &t, hipStream_t stream);
-// qs_score_pod in ONE launch for tables up to score_pod1_max_nodes(): pod record (DPod / DPodW) and
+// qs_score_pod in ONE launch (two for NormalizeScore profiles): pod record (DPod / DPodW) and
 // extension by value; outputs written into pinned host memory hout (score_pod1_pack_bytes(n) bytes:
-// [best u64 | done u64 | total i32 x n (-1 infeasible) | scores u8 x 4n]), done = seq stored last;
-// pidx < n: the pending row prow is written to the table first (and scored as such).  gs: four zeroed
-// device u64 (the multi-workgroup form's best key, arrival count and normalize maxima; left zeroed).
+// [best u64 | done u64 | packed u32 x n]: four byte scores per node, kScoreInfeasible = infeasible),
+// done = seq stored last; pidx < n: the pending row prow is written to the table first (and scored
+// as such).  gs: four zeroed device u64 (the multi-workgroup form's best key, arrival count and
+// normalize maxima; left zeroed); gs == nullptr: the single-workgroup form, n <= score_pod1_max_nodes().
 uint32_t score_pod1_max_nodes();
+constexpr uint32_t kScoreInfeasible = 0xFFFFFFFFu;  // packed per-node word of an infeasible node
 size_t score_pod1_pack_bytes(uint32_t n);
 hipError_t launch_score_pod1(const DevTable &t, const void *pod, const DPodX *podx, const DevCfg &c, uint8_t *hout,
                              uint64_t *gs, uint64_t seq, uint32_t pidx, const HostRow &prow, hipStream_t stream);

@@ -1,10 +1,16 @@
 // framework.cpp — the framework runtime and scheduling loop of framework.hpp (upstream citations
-// there).  Host logic only: every Filter/Score decision of the QoS plugins comes from the device
-// (qos_gpu.cpp); this file orders, weights and combines them the way upstream's runtime does.
+// there).  Host logic only: the Filter/Score decisions come from the plugins — the device-backed
+// QoS plugins (qos_gpu.cpp) or the CPU reference plugins (cpu_plugins.cpp) — and this file orders,
+// weights and combines them the way upstream's runtime does, with upstream's node Parallelizer.
 #include "framework.hpp"
 
 #include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <condition_variable>
+#include <mutex>
 #include <stdexcept>
+#include <thread>
 
 #include "../../include/qsched.h"
 
@@ -105,6 +111,84 @@ void NodeInfo::RemovePod(const Pod &p, const PodResources &r) {
     ++generation;
 }
 
+// ---- Parallelizer (UP framework/parallelize/parallelism.go) -----------------------------------
+struct Parallelizer::Impl {
+    std::vector<std::thread> th;
+    std::mutex mu;
+    std::condition_variable cv, done;
+    std::atomic<uint64_t> gen{0};
+    bool stop = false;
+    const std::function<void(int)> *fn = nullptr;
+    int n = 0, chunk = 1;
+    std::atomic<int> next{0}, active{0};
+    void chunks() {
+        for (;;) {
+            const int b = next.fetch_add(chunk, std::memory_order_relaxed);
+            if (b >= n) return;
+            const int e = std::min(n, b + chunk);
+            for (int i = b; i < e; ++i) (*fn)(i);
+        }
+    }
+    void worker() {
+        uint64_t seen = 0;
+        for (;;) {
+            // spin a little for the next section (~20 us), then sleep on the condition variable
+            for (int k = 0; k < 2000 && gen.load(std::memory_order_acquire) == seen; ++k) std::this_thread::yield();
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return stop || gen.load(std::memory_order_acquire) != seen; });
+                if (stop) return;
+                seen = gen.load(std::memory_order_acquire);
+            }
+            chunks();
+            if (active.fetch_sub(1, std::memory_order_acq_rel) == 1) {
+                std::lock_guard<std::mutex> g(mu);
+                done.notify_one();
+            }
+        }
+    }
+};
+
+Parallelizer::Parallelizer(int workers) : workers_(std::max(1, workers)), m_(new Impl) {
+    for (int w = 1; w < workers_; ++w) m_->th.emplace_back([this] { m_->worker(); });
+}
+
+Parallelizer::~Parallelizer() {
+    {
+        std::lock_guard<std::mutex> g(m_->mu);
+        m_->stop = true;
+    }
+    m_->cv.notify_all();
+    for (auto &t : m_->th) t.join();
+}
+
+void Parallelizer::Until(int n, const std::function<void(int)> &fn) {
+    if (n <= 0) return;
+    if (workers_ <= 1 || n == 1) {
+        for (int i = 0; i < n; ++i) fn(i);
+        return;
+    }
+    // UP parallelize#chunkSizeFor
+    int chunk = (int)std::sqrt((double)n);
+    chunk = std::min(chunk, n / workers_ + 1);
+    chunk = std::max(chunk, 1);
+    {
+        std::lock_guard<std::mutex> g(m_->mu);
+        m_->fn = &fn;
+        m_->n = n;
+        m_->chunk = chunk;
+        m_->next.store(0, std::memory_order_relaxed);
+        m_->active.store(workers_ - 1, std::memory_order_relaxed);
+        m_->gen.fetch_add(1, std::memory_order_release);
+    }
+    m_->cv.notify_all();
+    m_->chunks();
+    if (m_->active.load(std::memory_order_acquire) != 0) {
+        std::unique_lock<std::mutex> lk(m_->mu);
+        m_->done.wait(lk, [&] { return m_->active.load(std::memory_order_acquire) == 0; });
+    }
+}
+
 // ---- Framework (UP framework/runtime/framework.go) -----------------------------------------
 Framework::Framework(const Profile &p, const Registry &r, Handle *h) : name_(p.scheduler_name) {
     std::map<std::string, std::shared_ptr<Plugin>> inst;  // one instance per plugin per profile
@@ -157,20 +241,39 @@ Status Framework::RunFilterPlugins(CycleState &s, const Pod &p, const NodeInfo &
 }
 
 std::pair<std::vector<int64_t>, Status> Framework::RunScorePlugins(
-    CycleState &s, const Pod &p, const std::vector<const NodeInfo *> &nodes) {
-    std::vector<int64_t> total(nodes.size(), 0);
-    for (auto &[pl, w] : score_) {
-        NodeScoreList list(nodes.size());
-        for (size_t i = 0; i < nodes.size(); ++i) {
-            auto [v, st] = pl->Score(s, p, nodes[i]->node.name);
-            if (!st.IsSuccess()) return {total, st.WithPlugin(pl->Name())};
-            list[i] = {nodes[i]->node.name, v};
+    CycleState &s, const Pod &p, const std::vector<const NodeInfo *> &nodes, Parallelizer *par) {
+    const size_t nn = nodes.size(), np = score_.size();
+    std::vector<int64_t> total(nn, 0);
+    lists_.resize(np);
+    for (auto &l : lists_) l.resize(nn);
+    // every score plugin per node, the nodes in parallel (UP prioritizeNodes -> RunScorePlugins);
+    // the first failing (plugin, node) in node order is reported
+    std::vector<Status> bad(nn);
+    std::atomic<bool> any_bad{false};
+    auto one = [&](int i) {
+        for (size_t k = 0; k < np; ++k) {
+            auto [v, st] = score_[k].first->Score(s, p, nodes[i]->node.name);
+            if (!st.IsSuccess()) {
+                bad[i] = st.WithPlugin(score_[k].first->Name());
+                any_bad.store(true, std::memory_order_relaxed);
+                return;
+            }
+            lists_[k][i] = {nodes[i]->node.name, v};
         }
+    };
+    if (par) par->Until((int)nn, one);
+    else for (size_t i = 0; i < nn; ++i) one((int)i);
+    if (any_bad.load())
+        for (size_t i = 0; i < nn; ++i)
+            if (!bad[i].IsSuccess()) return {total, bad[i]};
+    for (size_t k = 0; k < np; ++k) {
+        auto &[pl, w] = score_[k];
+        NodeScoreList &list = lists_[k];
         if (pl->HasScoreExtensions()) {
             Status st = pl->NormalizeScore(s, p, list);
             if (!st.IsSuccess()) return {total, st.WithPlugin(pl->Name())};
         }
-        for (size_t i = 0; i < nodes.size(); ++i) {
+        for (size_t i = 0; i < nn; ++i) {
             if (list[i].score > MaxNodeScore || list[i].score < MinNodeScore)
                 return {total, Status::AsError("plugin " + pl->Name() + " returns an invalid score " +
                                                std::to_string(list[i].score) + ", it should in the range of [0, 100] after normalizing")};
@@ -194,8 +297,9 @@ void Framework::RunReservePluginsUnreserve(CycleState &s, const Pod &p, const st
 
 // ---- Scheduler (UP schedule_one.go) ----------------------------------------------------------
 Scheduler::Scheduler(const Registry &registry, const std::vector<Profile> &profiles,
-                     std::function<std::string(const Pod &, const PodResources &)> profile_of)
+                     std::function<std::string(const Pod &, const PodResources &)> profile_of, int parallelism)
     : registry_(registry), profile_of_(std::move(profile_of)) {
+    if (parallelism > 1) par_ = std::make_unique<Parallelizer>(parallelism);
     if (profiles.empty()) throw std::invalid_argument("at least one profile");
     for (const auto &p : profiles) fw_[p.scheduler_name] = std::make_unique<Framework>(p, registry_, this);
     if (!profile_of_) {
@@ -274,13 +378,25 @@ ScheduleResult Scheduler::ScheduleOne(const QueuedPodInfo &qp) {
     std::vector<const NodeInfo *> feasible;
     std::vector<int> feasible_ix;
     std::map<std::string, int> reasons;
+    // findNodesThatPassFilters: the Filter plugins of every node, the nodes in parallel; the
+    // results are then taken in node order (feasible list, reason counts, first error)
+    const int nn = (int)nodes_.size();
+    fstat_.assign(nn, Status::OK());
+    std::vector<uint8_t> skip(nn, 0);
+    for (int i = 0; i < nn; ++i)
+        skip[i] = !pfr.all_nodes && !pfr.node_names.count(nodes_[i].node.name);
+    auto filter_one = [&](int i) {
+        if (!skip[i]) fstat_[i] = fw.RunFilterPlugins(state, qp.pod, nodes_[i]);
+    };
+    if (par_) par_->Until(nn, filter_one);
+    else for (int i = 0; i < nn; ++i) filter_one(i);
     for (size_t i = 0; i < nodes_.size(); ++i) {
-        if (!pfr.all_nodes && !pfr.node_names.count(nodes_[i].node.name)) {
+        if (skip[i]) {
             ++reasons["node(s) didn't satisfy plugin(s) [" + st.Plugin() + "]"];
             continue;
         }
         ++res.evaluated_nodes;
-        Status fs = fw.RunFilterPlugins(state, qp.pod, nodes_[i]);
+        const Status &fs = fstat_[i];
         if (fs.IsSuccess()) {
             feasible.push_back(&nodes_[i]);
             feasible_ix.push_back((int)i);
@@ -298,7 +414,7 @@ ScheduleResult Scheduler::ScheduleOne(const QueuedPodInfo &qp) {
     }
     int pick = 0;
     if (feasible.size() > 1) {  // prioritizeNodes + deterministic selectHost (spec S7)
-        auto [total, sst] = fw.RunScorePlugins(state, qp.pod, feasible);
+        auto [total, sst] = fw.RunScorePlugins(state, qp.pod, feasible, par_.get());
         if (!sst.IsSuccess()) {
             res.status = sst;
             return res;

@@ -111,6 +111,26 @@ struct NodeInfo {
 };
 NodeInfo NewNodeInfo(const Node &n);
 
+// ---- Parallelizer (UP framework/parallelize/parallelism.go) -----------------------------------
+// Until(n, fn) runs fn(i) for i in [0, n) on `workers` threads (the caller is one of them) in chunks
+// of chunkSizeFor(n) = min(floor(sqrt(n)), n / workers + 1) indices, as upstream's workqueue-based
+// Parallelizer does (DefaultParallelism = 16).  Workers spin briefly for the next section before
+// sleeping (a scheduling cycle runs two sections per pod back to back).  workers <= 1: inline.
+class Parallelizer {
+   public:
+    explicit Parallelizer(int workers = 16);
+    ~Parallelizer();
+    Parallelizer(const Parallelizer &) = delete;
+    Parallelizer &operator=(const Parallelizer &) = delete;
+    int Workers() const { return workers_; }
+    void Until(int n, const std::function<void(int)> &fn);
+
+   private:
+    struct Impl;
+    int workers_;
+    std::unique_ptr<Impl> m_;
+};
+
 // ---- plugins (UP framework/interface.go) -------------------------------------------------------
 struct PreFilterResult {
     bool all_nodes = true;            // nil NodeNames upstream
@@ -195,8 +215,10 @@ class Framework {
     Status RunFilterPlugins(CycleState &s, const Pod &p, const NodeInfo &n);
     // weighted totals per feasible node (index-aligned with `nodes`); errors if a plugin returns
     // a score outside [0, 100] after normalization (UP RunScorePlugins)
+    // (par: the node-parallel Score pass runs every score plugin per node on it, UP prioritizeNodes)
     std::pair<std::vector<int64_t>, Status> RunScorePlugins(CycleState &s, const Pod &p,
-                                                            const std::vector<const NodeInfo *> &nodes);
+                                                            const std::vector<const NodeInfo *> &nodes,
+                                                            Parallelizer *par = nullptr);
     Status RunReservePluginsReserve(CycleState &s, const Pod &p, const std::string &node);
     void RunReservePluginsUnreserve(CycleState &s, const Pod &p, const std::string &node);
 
@@ -207,6 +229,7 @@ class Framework {
     std::vector<std::shared_ptr<FilterPlugin>> filter_;
     std::vector<std::pair<std::shared_ptr<ScorePlugin>, int32_t>> score_;
     std::vector<std::shared_ptr<ReservePlugin>> reserve_;
+    std::vector<NodeScoreList> lists_;  // per score plugin, reused across cycles
 };
 
 // ---- the scheduling loop (UP schedule_one.go) ---------------------------------------------------
@@ -223,8 +246,10 @@ struct ScheduleResult {
 class Scheduler : public Handle {
    public:
     // profile_of(pod) picks the profile (upstream: pod.Spec.SchedulerName)
+    // parallelism: workers of findNodesThatPassFilters / prioritizeNodes (upstream default 16; 1 runs
+    // them inline, as the device-backed QoSGPU plugins want: their Filter / Score are lookups)
     Scheduler(const Registry &registry, const std::vector<Profile> &profiles,
-              std::function<std::string(const Pod &, const PodResources &)> profile_of);
+              std::function<std::string(const Pod &, const PodResources &)> profile_of, int parallelism = 1);
     void AddNode(const Node &n);      // appended: its row index is the current node count
     void UpdateNode(const Node &n);   // allocatable / labels / taints changed (Generation bump)
     void AddPod(const Pod &p);        // enqueue
@@ -245,6 +270,8 @@ class Scheduler : public Handle {
     std::vector<QueuedPodInfo> queue_;
     std::vector<std::string> ext_names_;
     int64_t arrivals_ = 0;
+    std::unique_ptr<Parallelizer> par_;
+    std::vector<Status> fstat_;  // per-node Filter results of the current cycle
 };
 
 // UP framework/types.go#FitError message: "0/N nodes are available: <count> <reason>, ..."

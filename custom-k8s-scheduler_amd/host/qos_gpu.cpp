@@ -107,11 +107,10 @@ Status GpuBackend::Evaluate(const Handle &h, const Pod &pod, const PodResources 
         if (!st.IsSuccess()) return st;
         intern_.pod_masks(pod, &rec);  // tolerations over every taint interned by the sync
         const size_t n = h.NodeInfos().size();
-        out->feasible.assign(n, 0);
-        out->scores.assign(4 * n, 0);
-        out->total.assign(n, -1);
-        if (qs_score_pod(ctx_, &rec, out->feasible.data(), out->scores.data(), out->total.data(), &out->best) != QS_OK)
-            return Status::AsError(err("qs_score_pod"));
+        const uint32_t *pk = nullptr;
+        if (qs_score_pod_packed(ctx_, &rec, &pk, &out->best) != QS_OK) return Status::AsError(err("qs_score_pod_packed"));
+        out->packed.assign(pk, pk + (pk ? n : 0));
+        out->packed.resize(n, 0xFFFFFFFFu);
         return Status::OK();
     } catch (const std::exception &e) {
         return Status::AsError(std::string("QoSGPU: ") + e.what());
@@ -158,8 +157,8 @@ class QoSGPUPlugin final : public PreFilterPlugin, public FilterPlugin, public R
         auto *c = cycle_of(s);
         if (!c) return Status::AsError("QoSGPU: PreFilter did not run");
         const int i = h_->NodeIndex(ni.node.name);
-        if (i < 0 || (size_t)i >= c->feasible.size()) return Status::AsError("QoSGPU: unknown node " + ni.node.name);
-        if (c->feasible[i]) return Status::OK();
+        if (i < 0 || (size_t)i >= c->packed.size()) return Status::AsError("QoSGPU: unknown node " + ni.node.name);
+        if (c->feasible((size_t)i)) return Status::OK();
         return reasons(s, pod, ni);
     }
 
@@ -230,8 +229,8 @@ class QoSGPUComponent final : public ScorePlugin {
         auto *c = cycle_of(s);
         if (!c) return {0, Status::AsError(name_ + ": QoSGPU PreFilter did not run")};
         const int i = h_->NodeIndex(node);
-        if (i < 0 || 4 * (size_t)i + 3 >= c->scores.size()) return {0, Status::AsError(name_ + ": unknown node " + node)};
-        return {c->scores[4 * (size_t)i + k_], Status::OK()};
+        if (i < 0 || (size_t)i >= c->packed.size()) return {0, Status::AsError(name_ + ": unknown node " + node)};
+        return {c->score((size_t)i, k_), Status::OK()};
     }
 
    private:

@@ -28,12 +28,16 @@
 namespace qsfw {
 
 // Per-cycle device results (CycleState key "QoSGPU").
+// One word per node as qs_score_pod_packed returns it (0xFFFFFFFF = infeasible, else the four plugin
+// scores as bytes): 4 bytes per node copied out of the library's pinned buffer per cycle, and the
+// per-node Filter / Score lookups decode their node's word.
 struct QoSGPUCycle : StateData {
     qs_pod rec{};
-    std::vector<uint8_t> feasible;
-    std::vector<int32_t> scores;  // [n][4]: LeastAllocated, Balanced, TaintToleration, NodeAffinity
-    std::vector<int32_t> total;   // spec S6 total with the library config's weights
+    std::vector<uint32_t> packed;
     int32_t best = -1;            // spec S7 choice of the library config
+    bool feasible(size_t i) const { return packed[i] != 0xFFFFFFFFu; }
+    // k: 0 LeastAllocated, 1 Balanced, 2 TaintToleration, 3 NodeAffinity (0 where infeasible)
+    int32_t score(size_t i, int k) const { return feasible(i) ? (int32_t)((packed[i] >> (8 * k)) & 255u) : 0; }
 };
 
 class GpuBackend {

@@ -221,6 +221,16 @@ class Scheduler:
                                         ctypes.byref(best)))
         return dict(feasible=feas, scores=score, total=total, best=best.value)
 
+    def score_pod_packed(self, pod):
+        """qs_score_pod_packed: (best, packed) with packed a copy of the n per-node words (0xFFFFFFFF
+        = infeasible, else the four plugin scores as bytes, LeastAllocated in the low byte)."""
+        p = np.array([pod], POD_DTYPE) if isinstance(pod, np.void) else pods_to_struct(pod)[:1]
+        best = ctypes.c_int32(-2)
+        ptr = ctypes.POINTER(ctypes.c_uint32)()
+        self._chk(self.lib.qs_score_pod_packed(self.ctx, _ptr(p), ctypes.byref(ptr), ctypes.byref(best)))
+        packed = np.ctypeslib.as_array(ptr, shape=(self.n,)).copy() if self.n and ptr else np.zeros(0, np.uint32)
+        return best.value, packed
+
     def score_buffers(self):
         """Output arrays for score_pod(..., out=...) sized to the current table (feasible is a bool
         array the library fills with 0 / 1 bytes)."""

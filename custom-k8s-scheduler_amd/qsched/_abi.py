@@ -137,6 +137,7 @@ _SIGS = {
     "qs_reserve": (ctypes.c_int, [_P, ctypes.c_uint32, _P]),
     "qs_unreserve": (ctypes.c_int, [_P, ctypes.c_uint32, _P]),
     "qs_score_pod": (ctypes.c_int, [_P, _P, _P, _P, _P, _P]),
+    "qs_score_pod_packed": (ctypes.c_int, [_P, _P, _P, _P]),
     "qs_schedule_stream": (ctypes.c_int, [_P, _P, ctypes.c_uint32, ctypes.c_int, _P, _P]),
     "qs_stream_prepare": (ctypes.c_int, [_P, _P, ctypes.c_uint32, _P]),
     "qs_stream_run": (ctypes.c_int, [_P, _P, ctypes.c_int, _P]),

@@ -225,6 +225,12 @@ QS_API qs_status qs_unreserve(qs_ctx *ctx, uint32_t node, const qs_pod *pod);
  * QoS-weighted total per node (-1 where infeasible); best: node index of spec S7 or -1. */
 QS_API qs_status qs_score_pod(qs_ctx *ctx, const qs_pod *pod, uint8_t *feasible_n, int32_t *score_n,
                        int32_t *total_n, int32_t *best);
+/* The same call without the per-node copy-out: *packed_n (nullable) points at n context-owned words,
+ * valid until the next call on ctx, one per node: 0xFFFFFFFF = infeasible, else the four normalized
+ * plugin scores as bytes (LeastAllocated | Balanced << 8 | TaintToleration << 16 | NodeAffinity << 24).
+ * The words are what the kernel wrote into pinned host memory, so a plugin's per-node Filter / Score
+ * lookups read them in place (UP framework/interface.go#ScorePlugin.Score is called per node). */
+QS_API qs_status qs_score_pod_packed(qs_ctx *ctx, const qs_pod *pod, const uint32_t **packed_n, int32_t *best);
 
 /* ---- exact stream ---- */
 QS_API qs_status qs_schedule_stream(qs_ctx *ctx, const qs_pod *pods, uint32_t p, qs_mode mode,

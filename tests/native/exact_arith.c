@@ -2,6 +2,10 @@
  * (spec/semantics.md S10), checked against true integer / IEEE division.
  *   floor_div(n, y = RN(1/d)) == n / d           (LeastAllocated, normalize, weight combine)
  *   fraction(a, r, y = RN(1/a)) == min(RN(r/a),1) (BalancedAllocation, Markstein quotient)
+ *   wide layout (memory in f64 bytes, 1 <= a <= 2^46):
+ *   least_requested_w(a, reqd, RN(1/a)) == ((a - reqd) * 100) / a   (f64 quotient + one fma-exact
+ *                                                                      integer correction)
+ *   fraction_w(a, r, RN(1/a)) == min(RN(r/a), 1)                     (the same Markstein quotient)
  * Usage: exact_arith <mode> ; prints "ok <count>" or the first counter-example.  Test infra. */
 #include <math.h>
 #include <stdint.h>
@@ -27,6 +31,21 @@ static double rcp_int(int32_t a, float y0f) {
     e = fma(-A, y, 1.0);
     return fma(y, e, y);
 }
+static uint32_t least_requested_w(double a, double reqd, double ya) {
+    const double rq = reqd < a ? reqd : a;
+    const double n = (a - rq) * 100.0;
+    double q = trunc(n * ya);
+    const double r = fma(-q, a, n); /* exact: an integer below 2a in magnitude */
+    q = r < 0.0 ? q - 1.0 : q;
+    q = (r >= a && a > 0.0) ? q + 1.0 : q;
+    return reqd > a ? 0u : (uint32_t)q;
+}
+static double fraction_w(double a, double r, double y) {
+    const double q0 = r * y;
+    const double rem = fma(-q0, a, r);
+    const double q = fma(rem, y, q0);
+    return r >= a ? 1.0 : q;
+}
 static uint64_t sm = 0x5EED1234ULL;
 static uint64_t rnd(void) {
     uint64_t z = (sm += 0x9E3779B97F4A7C15ULL);
@@ -48,6 +67,19 @@ static int check_frac(int32_t a, int32_t r) {
     double w = want > 1 ? 1 : want;
     checks++;
     if (fraction(a, r, y) != w) { printf("FRAC a=%d r=%d got %.17g want %.17g\n", a, r, fraction(a, r, y), w); return 1; }
+    return 0;
+}
+static int check_wide(int64_t a, int64_t r) {
+    double A = (double)a, R = (double)r, y = 1.0 / A;
+    checks += 2;
+    if (r <= a) {
+        uint32_t want = (uint32_t)(((a - r) * 100) / a);
+        uint32_t got = least_requested_w(A, R, y);
+        if (got != want) { printf("LAW a=%lld r=%lld got %u want %u\n", (long long)a, (long long)r, got, want); return 1; }
+    }
+    volatile double want = R / A;
+    double w = want > 1 ? 1 : want;
+    if (fraction_w(A, R, y) != w) { printf("FRACW a=%lld r=%lld\n", (long long)a, (long long)r); return 1; }
     return 0;
 }
 int main(int argc, char **argv) {
@@ -77,6 +109,23 @@ int main(int argc, char **argv) {
                 checks++;
                 if (rcp_int(a, y0) != want) { printf("RCP a=%d y0=%.9g got %.17g want %.17g\n", a, y0, rcp_int(a, y0), want); return 1; }
             }
+        }
+    } else if (mode == 4) { /* wide layout: random a over every binade up to 2^46, r near a, near
+                               multiples of a / 100, and uniform; all-ones significands */
+        for (int k = 0; k < 12000000; k++) {
+            int e = 1 + (int)(rnd() % 46);
+            int64_t a = (int64_t)((rnd() & ((1ULL << e) - 1)) | (1ULL << (e - 1)));
+            if (k % 8 == 0) a = (int64_t)((1ULL << e) - 1);
+            if (a < 1) a = 1;
+            int64_t r;
+            switch (k % 4) {
+                case 0: r = (int64_t)(rnd() % ((uint64_t)a + 1)); break;
+                case 1: r = a - (int64_t)(rnd() % 3); break;
+                case 2: { int64_t m = (int64_t)(rnd() % 101); r = a - (a * m) / 100 + (int64_t)(rnd() % 3) - 1; break; }
+                default: r = (int64_t)(rnd() % 1024); break;
+            }
+            if (r < 0) r = 0;
+            if (check_wide(a, r)) return 1;
         }
     } else { /* small divisors (weight sums, normalize maxima): n/d <= 100 exhaustive */
         for (uint32_t d = 1; d <= 131070; d += (d < 2048 ? 1 : 97)) {

@@ -6,6 +6,8 @@
 // spec/semantics.md (the reference holds no fixtures: parity unpinned).
 //
 //   test_framework --cpu   host logic only (quantities, interning, pod requests, QoS sort, FitError)
+//                          and the CPU reference plugins (host/cpu_plugins.cpp): scores vs the
+//                          oracle's scorers, and whole ScheduleOne loops vs the oracle
 //   test_framework --gpu   the QoSGPU plugins on the device: filter/score tables, and the whole
 //                          ScheduleOne loop on a config-4 cluster built from k8s objects, checked
 //                          pod-by-pod against qs_schedule_stream and the CPU oracle.
@@ -15,7 +17,9 @@
 #include <string>
 #include <vector>
 
+#include "../../custom-k8s-scheduler_amd/host/cpu_plugins.hpp"
 #include "../../custom-k8s-scheduler_amd/host/qos_gpu.hpp"
+#include "../../tools/synth_objects.hpp"
 extern "C" {
 #include "../../oracle/qs_oracle.h"
 }
@@ -301,78 +305,12 @@ static void test_gpu_taint_affinity_scores() {
 }
 
 // ---- the whole loop on a config-4 cluster built from k8s objects (spec/synth.md G2/G3) --------
-static uint64_t sm_at(uint64_t seed, uint64_t c) {
-    uint64_t z = seed + (c + 1) * 0x9E3779B97F4A7C15ULL;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
-    return z ^ (z >> 31);
-}
-static uint32_t pick(uint64_t seed, uint64_t c, uint32_t k) { return (uint32_t)((sm_at(seed, c) >> 33) % k); }
-
-static void synth_objects(uint64_t seed, uint32_t n, uint32_t p, std::vector<Node> *nodes, std::vector<Pod> *pods) {
-    static const int64_t kNodeCpu[6] = {4000, 8000, 16000, 32000, 64000, 96000}, kMpc[3] = {2, 4, 8};
-    static const int64_t kPodCpu[6] = {500, 1000, 1500, 2000, 4000, 8000}, kPodMemMi[7] = {128, 256, 512, 1024, 2048, 4096, 8192};
-    static const int64_t kGpu[4] = {1, 2, 4, 8};
-    for (uint32_t i = 0; i < n; ++i) {
-        const uint64_t c = 8ULL * i;
-        const int64_t cpu = kNodeCpu[pick(seed, c, 6)], mpc = kMpc[pick(seed, c + 1, 3)];
-        auto w = MakeNode("node-" + std::to_string(i));
-        ResourceList cap = {{kCPU, std::to_string(cpu) + "m"}, {kMemory, std::to_string(cpu / 1000 * mpc) + "Gi"}, {kPods, "110"}};
-        const bool gpu = pick(seed, c + 2, 10) == 0, maint = pick(seed, c + 3, 20) == 0;
-        const int zone = (int)pick(seed, c + 4, 10);
-        const char *pool = gpu ? "gpu" : (pick(seed, c + 5, 2) ? "highmem" : "general");
-        const bool ssd = pick(seed, c + 6, 2) == 0;
-        if (gpu) { cap["amd.com/gpu"] = "8"; w.Taint("gpu", "true", kNoSchedule); }
-        if (maint) w.Taint("maint", "true", kPreferNoSchedule);
-        w.Capacity(cap).Label("zone", "z" + std::to_string(zone)).Label("pool", pool).Label("disktype", ssd ? "ssd" : "hdd");
-        nodes->push_back(w.Obj());
-    }
-    for (uint32_t j = 0; j < p; ++j) {
-        const uint64_t c = 8ULL * n + 16ULL * j;
-        const uint32_t qd = pick(seed, c, 10);
-        const std::string cpu = std::to_string(kPodCpu[pick(seed, c + 1, 6)]) + "m";
-        const int64_t mem_mi = kPodMemMi[pick(seed, c + 2, 7)];
-        const std::string mem = std::to_string(mem_mi) + "Mi", mem2 = std::to_string(2 * mem_mi) + "Mi";
-        const uint32_t memmode = pick(seed, c + 3, 4), limmode = pick(seed, c + 4, 2);
-        const std::string cpu2 = std::to_string(2 * kPodCpu[pick(seed, c + 1, 6)]) + "m";
-        ResourceList req, lim;
-        if (qd < 2) {
-            req = {{kCPU, cpu}, {kMemory, mem}};
-            lim = req;
-        } else if (qd < 7) {
-            req = {{kCPU, cpu}};
-            if (memmode != 0) req[kMemory] = mem;
-            if (limmode == 1) {
-                lim = {{kCPU, cpu2}};
-                if (memmode != 0) lim[kMemory] = mem2;
-            }
-        }
-        auto w = MakePod("pod-" + std::to_string(j));
-        if (pick(seed, c + 5, 20) == 0) {
-            req["amd.com/gpu"] = std::to_string(kGpu[pick(seed, c + 6, 4)]);
-            w.Toleration("gpu", "Equal", "true", kNoSchedule).NodeSelector({{"pool", "gpu"}});
-        }
-        if (pick(seed, c + 7, 5) == 0) {
-            const int za = (int)pick(seed, c + 8, 10), zb = (za + 1 + (int)pick(seed, c + 9, 9)) % 10;
-            w.NodeAffinityIn("zone", {"z" + std::to_string(za), "z" + std::to_string(zb)});
-        }
-        if (pick(seed, c + 10, 5) == 0) {
-            const uint32_t which = pick(seed, c + 11, 3);
-            if (which == 0 || which == 2) w.PreferredTerm(50, {{{"disktype", "In", {"ssd"}}}});
-            if (which == 1 || which == 2) w.PreferredTerm(20, {{{"pool", "In", {"highmem"}}}});
-        }
-        if (pick(seed, c + 12, 10) == 0) w.Toleration("maint", "Equal", "true", kPreferNoSchedule);
-        w.ReqLim(req, lim);
-        pods->push_back(w.Obj());
-    }
-}
-
 static void test_gpu_schedule_one_loop_parity() {
     const uint32_t n = 600, p = 14000;  // ~23 pods per node: the cluster fills up
     const uint64_t seed = 0x5EED0004;
     std::vector<Node> nodes;
     std::vector<Pod> pods;
-    synth_objects(seed, n, p, &nodes, &pods);
+    synth_objects(4, seed, n, p, &nodes, &pods);
     const qs_config cfg = default_cfg(true, true);
     auto backend = std::make_shared<GpuBackend>(cfg);
     Scheduler sched(QoSRegistry(backend), QoSProfiles(cfg), QoSProfileOf);
@@ -433,13 +371,85 @@ static void test_gpu_schedule_one_loop_parity() {
     CHECK(unsched > 0 && unsched < (int)p);
 }
 
+// ---- the CPU reference plugins (host/cpu_plugins.cpp) ------------------------------------------
+// One pod on one node through the CPU plugins' Filter / Score, against the oracle's scorers.
+static void test_cpu_plugin_scores() {
+    qs_config cfg = default_cfg(true, true);
+    struct Tc {
+        const char *cpu, *mem, *rcpu, *rmem;
+    } tcs[] = {{"4000m", "8Gi", "1000m", "2Gi"}, {"16", "64Gi", "3500m", "7Gi"}, {"2", "1Gi", "100m", "2Gi"}};
+    for (const auto &tc : tcs) {
+        Scheduler sched(CPURegistry(cfg), CPUProfiles(cfg), CPUProfileOf, 1);
+        sched.AddNode(MakeNode("n0").Capacity({{kCPU, tc.cpu}, {kMemory, tc.mem}, {kPods, "110"}}).Obj());
+        Pod pod = MakePod("p").ReqLim({{kCPU, tc.rcpu}, {kMemory, tc.rmem}}, {}).Obj();
+        auto reg = CPURegistry(cfg);
+        auto fit = std::dynamic_pointer_cast<ScorePlugin>(reg[kNodeResourcesFit](&sched));
+        auto bal = std::dynamic_pointer_cast<ScorePlugin>(reg[kNodeResourcesBalancedAllocation](&sched));
+        auto flt = std::dynamic_pointer_cast<FilterPlugin>(reg[kNodeResourcesFit](&sched));
+        CycleState st;
+        const PodResources r = ComputePodResources(pod);
+        const NodeInfo &ni = sched.NodeInfos()[0];
+        const int64_t la = fit->Score(st, pod, "n0").first, ba = bal->Score(st, pod, "n0").first;
+        CHECK_EQ(la, or_least_allocated(ni.allocatable.milli_cpu, r.nz_cpu, ni.allocatable.memory, r.nz_mem, 1, 1));
+        CHECK_EQ(ba, or_balanced(ni.allocatable.milli_cpu, r.cpu, ni.allocatable.memory, r.mem));
+        const bool fits = r.cpu <= ni.allocatable.milli_cpu && r.mem <= ni.allocatable.memory;
+        const Status fs = flt->Filter(st, pod, ni);
+        CHECK_EQ(fs.IsSuccess(), fits);
+        if (!fits) CHECK(fs.Message().find("Insufficient memory") != std::string::npos);
+    }
+}
+
+// The whole ScheduleOne loop with the CPU plugins (16-worker Parallelizer for config 2, 4 for config
+// 4) on spec/synth.md clusters built as k8s objects, pod by pod against the oracle.
+static void cpu_loop_parity(int config, uint32_t n, uint32_t p, int workers) {
+    const uint64_t seed = 0x5EED0000ull + (uint64_t)config;
+    std::vector<Node> nodes;
+    std::vector<Pod> pods;
+    synth_objects(config, seed, n, p, &nodes, &pods);
+    const qs_config cfg = default_cfg(config == 4, config == 4);
+    Scheduler sched(CPURegistry(cfg), CPUProfiles(cfg), CPUProfileOf, workers);
+    for (const auto &x : nodes) sched.AddNode(x);
+    for (const auto &x : pods) sched.AddPod(x);
+    const auto res = sched.Run();
+    std::vector<int32_t> loop(p, -2);
+    for (const auto &r : res) loop[r.arrival] = r.node_index;
+    std::vector<int64_t> o[10];
+    for (auto &v : o) v.assign(n, 0);
+    std::vector<int64_t> oae(2 * n), ore(2 * n);
+    std::vector<uint64_t> oth(n), ots(n), olb(2 * n);
+    or_nodes on{n, o[0].data(), o[1].data(), oae.data(), o[2].data(), o[3].data(), o[4].data(), ore.data(),
+                o[5].data(), o[6].data(), o[7].data(), oth.data(), ots.data(), olb.data(), nullptr};
+    std::vector<int64_t> prc(p), prm(p), pre(2 * p), pzc(p), pzm(p);
+    std::vector<int32_t> pq(p), ppr(p), pnr(p), pnp(p), ppw(4 * p);
+    std::vector<uint64_t> pth(p), pts(p), psel(2 * p), prt(8 * p), ppt(8 * p);
+    or_pods op{p, prc.data(), prm.data(), pre.data(), pzc.data(), pzm.data(), pq.data(), ppr.data(), pth.data(),
+               pts.data(), psel.data(), pnr.data(), pnp.data(), prt.data(), ppt.data(), ppw.data(), nullptr, nullptr};
+    or_generate(config, seed, &on, &op);
+    or_config oc{1, 1, {1, 2, 3}, {1, 1, 1}, 3, 2, cfg.enable_taint, cfg.enable_affinity, 0, 1};
+    std::vector<int32_t> oracle(p);
+    or_schedule(&oc, &on, &op, oracle.data(), nullptr, nullptr, 4);
+    int diff = 0, unsched = 0;
+    for (uint32_t j = 0; j < p; ++j) {
+        diff += loop[j] != oracle[j];
+        unsched += loop[j] < 0;
+    }
+    std::printf("  CPU plugins, config %d: %u pods on %u nodes (%d workers), %d unschedulable, %d differ from the oracle\n",
+                config, p, n, workers, unsched, diff);
+    CHECK_EQ(diff, 0);
+    if (config == 4) CHECK(unsched > 0 && unsched < (int)p);
+}
+static void test_cpu_loop_config2() { cpu_loop_parity(2, 300, 9000, 16); }
+static void test_cpu_loop_config4() { cpu_loop_parity(4, 400, 9000, 4); }
+
 int main(int argc, char **argv) {
     const bool gpu = argc > 1 && std::strcmp(argv[1], "--gpu") == 0;
     std::vector<Case> cases;
     if (!gpu) {
         cases = {{"quantity", test_quantity}, {"tolerations", test_tolerations},
                  {"requirements", test_requirements}, {"interner", test_interner},
-                 {"pod_resources", test_pod_resources}, {"qos_sort_fit_error", test_qos_sort_and_fit_error}};
+                 {"pod_resources", test_pod_resources}, {"qos_sort_fit_error", test_qos_sort_and_fit_error},
+                 {"cpu_plugin_scores", test_cpu_plugin_scores}, {"cpu_loop_config2", test_cpu_loop_config2},
+                 {"cpu_loop_config4", test_cpu_loop_config4}};
     } else {
         cases = {{"gpu_least_allocated", test_gpu_least_allocated}, {"gpu_balanced", test_gpu_balanced},
                  {"gpu_fit_filter", test_gpu_fit_filter}, {"gpu_taint_affinity_scores", test_gpu_taint_affinity_scores},

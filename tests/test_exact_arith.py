@@ -5,7 +5,11 @@ tests/native/exact_arith.c restates the two division formulas the gfx950 kernels
 (fma, -ffp-contract=off) and compares them with true integer and IEEE division: exhaustively over
 every allocatable value of spec/synth.md, exhaustively for small divisors, and on 20M random pairs
 over the whole compacted range [1, 2^24); and the scan kernel's reciprocal RN(1/a) (f32 estimate +
-two f64 Newton steps) exhaustively over [1, 2^24) for every estimate within 2 f32 ulps.  The GPU parity tests then confirm the device agrees.
+two f64 Newton steps) exhaustively over [1, 2^24) for every estimate within 2 f32 ulps.  Mode 4: the
+wide layout's LeastAllocated (f64 quotient + one fma-exact integer correction) and Markstein
+BalancedAllocation quotient on 12M pairs over every binade up to 2^46 bytes (all-ones significands,
+requests near the allocatable and near multiples of a / 100).  The GPU parity tests then confirm the
+device agrees.
 """
 import os
 import subprocess
@@ -23,7 +27,7 @@ def exe(tmp_path_factory):
     return out
 
 
-@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3, 4])
 def test_division_formulas_exact(exe, mode):
     r = subprocess.run([exe, str(mode)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout

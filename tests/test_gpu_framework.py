@@ -46,11 +46,12 @@ def test_score_pod_parity(layout, config, n):
             np.testing.assert_array_equal(got["scores"][feas], sc[feas])
 
 
-@pytest.mark.parametrize("n", [1, 255, 257, 4096, 16384])
+@pytest.mark.parametrize("n", [1, 255, 257, 4096, 16384, 16385, 50000, 70001])
 def test_score_pod_grid_edges_reused_buffers(n):
     """The multi-workgroup score launch (one node per thread, ceil(n/256) workgroups, the last
-    arrival publishing best + done) at workgroup-count edges up to the one-launch limit, with the
-    outputs unpacked 16 nodes at a time (tails 1, 15, 1, 0, 0) into caller buffers reused across
+    arrival publishing best + done) at workgroup-count edges and beyond round 3's 16,384-node
+    one-launch limit (50,000 = config 3's table; 70,001 keeps a SoA copy too), with the packed outputs
+    unpacked 16 nodes at a time (tails 1, 15, 1, 0, 0, 1, 0, 1) into caller buffers reused across
     calls and Reserves; every call diffed against the oracle and against a fresh-buffer call."""
     from oracle import oracle as O
     nodes, pods = synth_generate(2, n, 12)
@@ -176,3 +177,23 @@ def test_hbm_resident_scan_parity(oracle):
         st.free()
     o = run_oracle(oracle, nodes, pods, {}, nthreads=16)
     assert np.array_equal(pl, o[0]) and np.array_equal(keys, o[1])
+
+
+@pytest.mark.parametrize("config,n", [(2, 5000), (4, 3000), (2, 20001)])
+def test_score_pod_packed_words(config, n):
+    """qs_score_pod_packed: the kernel's per-node words read in place (no copy-out) decode to the
+    oracle's feasibility and plugin scores, the best node matches, and qs_score_pod's arrays are
+    the same words unpacked (totals = the QoS-weighted sums)."""
+    nodes, pods = synth_generate(config, n, 12)
+    cfg = CFG4 if config == 4 else {}
+    with Scheduler(cfg) as s:
+        s.load_nodes(nodes)
+        for j in range(0, 12, 3):
+            best, pk = s.score_pod_packed(pods[j])
+            feas, sc, total, obest = oracle_scores(nodes, pods, j, cfg or None)
+            assert best == obest
+            assert np.array_equal(pk != 0xFFFFFFFF, feas)
+            dec = np.stack([(pk >> (8 * k)) & 255 for k in range(4)], axis=1).astype(np.int64)
+            np.testing.assert_array_equal(dec[feas], sc[feas])
+            got = s.score_pod(pods[j])
+            assert np.array_equal(got["feasible"], feas) and np.array_equal(got["total"], total)

@@ -133,11 +133,12 @@ def test_resident_stream_timeout_drains_on_device(monkeypatch):
         mid = s.read_nodes()
         for k in before:
             assert np.array_equal(mid[k], before[k]), k
-        s.save_table()
         stats = st.run()
         assert stats["resident"] == 0 and stats["device_faults"] == 1
         pl, keys = st.results()
-        s.restore_table()
+        st.free()
+        s.load_nodes(nodes)  # the same context, from the empty cluster again
+        st = s.prepare(pods)
         stats3 = st.run()
         assert stats3["resident"] == 1
         pl3, keys3 = st.results()
@@ -156,21 +157,20 @@ def test_resident_stream_second_timeout_sticks(monkeypatch):
     on = {k: v.copy() for k, v in nodes.items()}
     o, ok, _ = O.schedule(on, pods_from_struct(pods), nthreads=16)
     with Scheduler({"engine": "lookahead"}) as s:
-        s.load_nodes(nodes)
-        st = s.prepare(pods)
-        s.save_table()
         monkeypatch.setenv("QS_INJECT_FAULT", "resident_stall_always")
         seen = []
         for _ in range(5):
-            s.restore_table()
+            s.load_nodes(nodes)  # from the empty cluster each time (a timeout drops the snapshot)
+            st = s.prepare(pods)
             try:
                 stats = st.run()
             except QschedError as e:
                 assert "resident lookahead stream timed out" in str(e)
                 seen.append("timeout")
+                st.free()
                 continue
             seen.append("resident" if stats["resident"] else "per-window")
             pl, keys = st.results()
+            st.free()
             assert np.array_equal(pl, o) and np.array_equal(keys, ok)
-        st.free()
     assert seen == ["timeout", "per-window", "timeout", "per-window", "per-window"], seen

@@ -4,7 +4,9 @@
 // followed by qs_reserve of the chosen node.  Arrival order on a spec/synth.md config-2 cluster;
 // placements diffed against the CPU oracle (test infrastructure: oracle/liboracle.so).
 //
-//   fw_latency [nodes] [pods] [outputs: 1 all arrays, 0 best only]  ->  one JSON line
+//   fw_latency [nodes] [pods] [outputs: 1 all arrays, 0 best only, 2 packed words read in place]
+//   ->  one JSON line.  Mode 2 is qs_score_pod_packed plus one pass over the n words (the per-node
+//   Filter / Score lookups a plugin makes: here a count of the feasible nodes).
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -16,10 +18,24 @@ extern "C" {
 #include "../oracle/qs_oracle.h"
 }
 
+static qs_ctx *g_ctx = nullptr;
+static qs_ctx *ctx_of() { return g_ctx; }
+
 int main(int argc, char **argv) {
     const uint32_t n = argc > 1 ? (uint32_t)atoi(argv[1]) : 5000;
     const uint32_t p = argc > 2 ? (uint32_t)atoi(argv[2]) : 2000;
-    const bool outputs = argc > 3 ? atoi(argv[3]) != 0 : true;
+    const int mode = argc > 3 ? atoi(argv[3]) : 1;
+    const bool outputs = mode == 1;
+    uint64_t feasible_seen = 0;
+    // one call in the chosen mode
+    auto score = [&](const qs_pod *pod, int32_t *best, uint8_t *f, int32_t *sc, int32_t *tot) -> qs_status {
+        if (mode != 2) return qs_score_pod(ctx_of(), pod, f, sc, tot, best);
+        const uint32_t *pk = nullptr;
+        const qs_status st = qs_score_pod_packed(ctx_of(), pod, &pk, best);
+        if (st == QS_OK && pk)
+            for (uint32_t i = 0; i < n; ++i) feasible_seen += pk[i] != 0xFFFFFFFFu;
+        return st;
+    };
     std::vector<int64_t> col[10];
     for (auto &v : col) v.assign(n, 0);
     std::vector<int64_t> ae(2 * n), re(2 * n);
@@ -32,29 +48,29 @@ int main(int argc, char **argv) {
     if (qs_synth_generate(2, 0x5EED0002ull, n, p, &out, pods.data()) != QS_OK) return 2;
     qs_config cfg;
     qs_config_default(&cfg);
-    qs_ctx *ctx = nullptr;
-    if (qs_open(&cfg, 0, &ctx) != QS_OK) return 3;
+    if (qs_open(&cfg, 0, &g_ctx) != QS_OK) return 3;
+    qs_ctx *ctx = g_ctx;
     qs_node_soa in{col[0].data(), col[1].data(), ae.data(), col[2].data(), col[3].data(), col[4].data(),
                    re.data(), col[5].data(), col[6].data(), col[7].data(), th.data(), ts.data(), lb.data(),
                    zone.data()};
     if (qs_nodes_load(ctx, &in, n) != QS_OK) return 4;
     std::vector<uint8_t> feas(n);
-    std::vector<int32_t> score(4 * (size_t)n), total(n), placement(p);
+    std::vector<int32_t> scores(4 * (size_t)n), total(n), placement(p);
     std::vector<double> lat(p);
     using clk = std::chrono::steady_clock;
     // warm-up (module load, first-touch of the pinned output pages): score-only calls, which leave
     // the table unchanged; a plugin process pays this once, not per pod
     for (uint32_t j = 0; j < 32 && p > 0; ++j) {
         int32_t best = -2;
-        if (qs_score_pod(ctx, &pods[0], outputs ? feas.data() : nullptr, outputs ? score.data() : nullptr,
-                         outputs ? total.data() : nullptr, &best) != QS_OK)
+        if (score(&pods[0], &best, outputs ? feas.data() : nullptr, outputs ? scores.data() : nullptr,
+                  outputs ? total.data() : nullptr) != QS_OK)
             return 5;
     }
     for (uint32_t j = 0; j < p; ++j) {
         const auto t0 = clk::now();
         int32_t best = -2;
-        if (qs_score_pod(ctx, &pods[j], outputs ? feas.data() : nullptr, outputs ? score.data() : nullptr,
-                         outputs ? total.data() : nullptr, &best) != QS_OK) {
+        if (score(&pods[j], &best, outputs ? feas.data() : nullptr, outputs ? scores.data() : nullptr,
+                  outputs ? total.data() : nullptr) != QS_OK) {
             std::fprintf(stderr, "qs_score_pod: %s\n", qs_last_error(ctx));
             return 5;
         }
@@ -92,7 +108,8 @@ int main(int argc, char **argv) {
     for (double v : lat) sum += v;
     std::printf("{\"nodes\": %u, \"pods\": %u, \"outputs\": %s, \"p50_us\": %.2f, \"p99_us\": %.2f, \"mean_us\": %.2f, "
                 "\"max_us\": %.2f, \"pods_per_s\": %.1f, \"placements_match\": %s}\n",
-                n, p, outputs ? "\"feasible+scores+totals\"" : "\"best only\"", pct(0.5), pct(0.99), sum / p, s.back(),
+                n, p, mode == 1 ? "\"feasible+scores+totals\"" : mode == 2 ? "\"packed words read in place\"" : "\"best only\"",
+                pct(0.5), pct(0.99), sum / p, s.back(),
                 p / (sum * 1e-6), match ? "true" : "false");
     return match ? 0 : 1;
 }
