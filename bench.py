@@ -71,7 +71,7 @@ def parse(argv=None):
                     help="skip the end-to-end, framework-path and wide-layout legs")
     ap.add_argument("--transport", default="mailbox", choices=["mailbox", "rccl"],
                     help="sharded exchange (N > 1): peer-memory mailbox over xGMI, or RCCL all-gather")
-    ap.add_argument("--leg", default=None, choices=["wide", "config3", "config4", "config5", "framework"],
+    ap.add_argument("--leg", default=None, choices=["config2", "wide", "config3", "config4", "config5", "framework"],
                     help="run only this sub-leg on one GPU and print its JSON object (iteration probe, "
                          "not the bench line)")
     ap.add_argument("--dry-run", action="store_true",

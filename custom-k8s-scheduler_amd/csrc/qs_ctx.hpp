@@ -189,12 +189,16 @@ constexpr size_t kMbListSlot = kMbRanks * 64 * 64 * 8;
 constexpr size_t kMbPartSlot = kMbRanks * kMbPartPerRank * 16;
 // Resident sharded stream, after the per-window regions: hello[16] (each rank's run
 // sequence, the in-launch entry barrier), flags[4 slots][32 pods][16 ranks] and shard lists
-// [4 slots][32 pods][16 ranks][64] u64 (window w uses slot w % 4).
+// [4 slots][32 pods][16 ranks][64] u64 (window w uses slot w % 4), then the normalizing profiles'
+// partial-maxima flags and partials of the same shape.
 constexpr size_t kMbResSlots = 4, kMbResPods = 32;
 constexpr size_t kMbResHello = kMbFlags + kMbSlots * (kMbListSlot + kMbPartSlot);
 constexpr size_t kMbResFlags = kMbResHello + 256;
 constexpr size_t kMbResLists = kMbResFlags + kMbResSlots * kMbResPods * kMbRanks * 8;
-constexpr size_t kMbBytes = kMbResLists + kMbResSlots * kMbResPods * kMbRanks * 64 * 8;
+// normalizing profiles: flags[4 slots][32 pods][16 ranks] u64 and partial maxima [4][32][16] uint4
+constexpr size_t kMbResNFlags = kMbResLists + kMbResSlots * kMbResPods * kMbRanks * 64 * 8;
+constexpr size_t kMbResNorm = kMbResNFlags + kMbResSlots * kMbResPods * kMbRanks * 8;
+constexpr size_t kMbBytes = kMbResNorm + kMbResSlots * kMbResPods * kMbRanks * 16;
 inline uint64_t *mbox_lists(qs_ctx *c, uint32_t slot) {
     return reinterpret_cast<uint64_t *>(static_cast<char *>(c->mbox.p) + kMbFlags + slot * kMbListSlot);
 }

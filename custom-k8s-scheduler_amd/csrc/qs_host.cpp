@@ -1384,7 +1384,7 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                 // unsharded contexts, and mailbox-sharded ones for Fit + Balanced (+ extended)
                 // profiles: there the selectors exchange every pod's shard list through the peers'
                 // mailboxes inside the launch (RCCL cannot be called in a kernel)
-                const bool res_transport = c->world == 1 ? !mbox && !c->comm : mbox && !norm;
+                const bool res_transport = c->world == 1 ? !mbox && !c->comm : mbox;
                 const bool res_allowed = c->res_timeouts < 2 && !c->res_cooldown;
                 const bool resident = overlap && res_transport && res_allowed && !diag_on &&
                                       !(renv && renv[0] == '0') && rgeo.G > 0 && coresident;
@@ -1411,10 +1411,10 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                     // select's), double-buffered by window parity
                     const size_t rcw = std::max<size_t>(1, (size_t)rgeo.K * rgeo.G * rgeo.L);
                     c->clists.ensure(8 * rcw * 2);
-                    ResShard rsh{1u, 0u, 0ull, nullptr, 0ull, 0ull, 0ull};
+                    ResShard rsh{1u, 0u, 0ull, nullptr, 0ull, 0ull, 0ull, 0ull, 0ull};
                     if (c->world > 1)
                         rsh = ResShard{(uint32_t)c->world, (uint32_t)c->rank, seq_run, c->mbox_peers.as<char *>(),
-                                       kMbResHello, kMbResFlags, kMbResLists};
+                                       kMbResHello, kMbResFlags, kMbResLists, kMbResNFlags, kMbResNorm};
                     // test hook: a selector that never delivers window 3 (one-shot), so the
                     // in-kernel timeout drain runs (tests/test_gpu_recovery.py)
                     DevCfg dcr = c->dc;  // (the launch's copy: the hook never sticks to the context)

@@ -149,13 +149,13 @@ hipError_t launch_la_window(const DevTable &t, const void *pods, const DPodX *po
 LaGeom la_stream_res_plan(const LaGeom &geo, uint32_t feat, uint32_t n, uint32_t cus, uint32_t per_cu) {
     LaGeom r = geo;
     r.G = 0;
-    // compact Fit + Balanced (+ extended) profiles, and the normalizing ones (K <= kResNormK)
-    // sharded (geo.W > 1 ranks, one shard each): Fit + Balanced (+ extended) only, W * L <= 512
+    // Fit + Balanced (+ extended) profiles, and the normalizing ones (K <= kResNormK), both layouts;
+    // sharded (geo.W > 1 ranks, one shard each): W * L <= 512
     const uint32_t fl = feat & ~kFeatWide;  // both row layouts
     const bool fit = fl == 0 || fl == kFeatExt;
     const bool norm = (feat & kFeatNorm) != 0 && geo.K <= kResNormK;
     const bool shard_ok = geo.W == 1 ? geo.nv == 1 && geo.epl == 1
-                                     : fit && geo.nv == 1 && geo.K <= 32 && geo.W * geo.L <= (uint32_t)kResBS;
+                                     : geo.nv == 1 && geo.K <= 32 && geo.W * geo.L <= (uint32_t)kResBS;
     if (!((fit || norm) && shard_ok && geo.waves == 4 && geo.L <= 64 && n > 0 && cus > geo.K)) return r;
     n = (n + geo.W - 1) / geo.W;  // this rank's node range
     const bool two = per_cu >= 2 && fit;

@@ -1949,6 +1949,67 @@ __device__ __forceinline__ bool res_cross_merge(uint64_t *lbuf, uint32_t L, uint
     return true;
 }
 
+// Sharded normalizing profiles: this rank's partial maxima of window pod k (over its node range,
+// combined from its G chunk partials) go to EVERY rank's mailbox (norm[w % 4][k][rank], system-scope
+// stores, then a system fence and the tagged flag nflags[w % 4][k][rank] = seq << 32 | w + 1), sent by
+// the pod's chunk-0 task; every chunk task of the pod then waits (bounded) for all W ranks' flags in
+// its own mailbox and combines the W partials into the pod's global NormInfo (max, and the counts of
+// the ranks attaining it: the order does not matter).  Slot reuse as for the lists (res_cross_merge):
+// a rank writes window w after resolving w - 2, which needed every rank's lists of w - 2, produced
+// after every chunk task of those ranks had left window w - 4.  Thread 0 only; false on a timeout.
+__device__ __forceinline__ bool res_norm_exchange(const NormInfo &part, uint32_t k, uint32_t w, uint32_t g,
+                                                  const ResShard &rsh, bool &hello_ok, NormInfo &out,
+                                                  uint32_t *werr, uint64_t first_ticks) {
+    const uint32_t W = rsh.W;
+    const uint64_t tag = (rsh.seq << 32) | (uint64_t)(w + 1);
+    const size_t cell = ((size_t)(w & 3) * 32 + k) * 16;  // [slot][pod][rank] index base
+    const uint64_t bound = (w == 0 || !hello_ok) && first_ticks ? first_ticks : kResWaitTicks;
+    auto sys_poll = [&](const uint64_t *p, uint64_t want) -> bool {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < want) {
+            __builtin_amdgcn_s_sleep(1);
+            if (load_coh_u32(werr) != 0u) return false;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > bound) {
+                __hip_atomic_store((gu32 *)werr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                return false;
+            }
+        }
+        return true;
+    };
+    const char *own = rsh.peers[rsh.rank];
+    if (!hello_ok) {
+        for (uint32_t r = 0; r < W; ++r)
+            if (!sys_poll(reinterpret_cast<const uint64_t *>(own + rsh.hello) + r, rsh.seq)) return false;
+        hello_ok = true;
+    }
+    if (g == 0) {
+        const uint64_t lo = (uint64_t)part.mt | ((uint64_t)part.ct << 32), hi = (uint64_t)part.ma | ((uint64_t)part.ca << 32);
+        for (uint32_t r = 0; r < W; ++r) {
+            uint64_t *dst = reinterpret_cast<uint64_t *>(rsh.peers[r] + rsh.norm) + 2 * (cell + rsh.rank);
+            __hip_atomic_store(dst, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(dst + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        __threadfence_system();
+        for (uint32_t r = 0; r < W; ++r)
+            __hip_atomic_store(reinterpret_cast<uint64_t *>(rsh.peers[r] + rsh.nflags) + cell + rsh.rank, tag,
+                               __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    NormInfo nf{0, 0, 0, 0};
+    for (uint32_t r = 0; r < W; ++r) {
+        if (!sys_poll(reinterpret_cast<const uint64_t *>(own + rsh.nflags) + cell + r, tag)) return false;
+        const uint64_t *src = reinterpret_cast<const uint64_t *>(own + rsh.norm) + 2 * (cell + r);
+        const uint64_t lo = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint64_t hi = __hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint32_t qx = (uint32_t)lo, qy = (uint32_t)(lo >> 32), qz = (uint32_t)hi, qw = (uint32_t)(hi >> 32);
+        if (qx > nf.mt) { nf.mt = qx; nf.ct = 0; }
+        if (qx == nf.mt) nf.ct += qy;
+        if (qz > nf.ma) { nf.ma = qz; nf.ca = 0; }
+        if (qz == nf.ma) nf.ca += qw;
+    }
+    out = nf;
+    return true;
+}
+
 // Normalizing profiles (TaintToleration / NodeAffinity): a task first scores everything but the
 // normalized parts and the chunk's partial maxima {mt, ct, ma, ca} over its feasible nodes,
 // publishes the partial (sc1, ticket nticket[w&1][k]), waits until all G chunks of its pod have
@@ -2041,6 +2102,7 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
                 }
                 if (lane == 0) { nred[2][w8] = ct; nred[3][w8] = ca; }
                 __syncthreads();
+                __shared__ NormInfo nfx;  // sharded: the pod's global maxima (thread 0 -> the block)
                 if (G == 1) {
                     nf = NormInfo{mt, 0, ma, 0};
 #pragma unroll
@@ -2070,6 +2132,18 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
                         if (qz > nf.ma) { nf.ma = qz; nf.ca = 0; }
                         if (qz == nf.ma) nf.ca += qw;
                     }
+                }
+                if (rsh.W > 1) {  // nf covers this rank's node range: combine with every rank's
+                    if (tid == 0) {
+                        NormInfo gnf{0, 0, 0, 0};
+                        okflag = res_norm_exchange(nf, k, w, g, rsh, hello_ok, gnf, c.werr, c.first_ticks) ? 1u : 0u;
+                        nfx = gnf;
+                    }
+                    __syncthreads();
+                    if (!okflag) return;
+                    nf = nfx;
+                    hello_ok = true;
+                    __syncthreads();  // (nfx / okflag reused by the next task)
                 }
                 const double ymt = rcp_exact(nf.mt), yma = rcp_exact(nf.ma);
 #pragma unroll
@@ -2302,6 +2376,42 @@ __device__ __forceinline__ uint64_t res_rescan_wait(const uint64_t *red_k) {
     return ks;
 }
 
+// Wave D's rule for the winner of window pod i (non-normalizing profiles): the slot keys of waves
+// A / B picked by pod i-1's winner pv (B's where that slot won), the new slot pv created read from
+// wave C's key at its source lane, the best clean list entry unless pv took its node; one 64-lane
+// max; then which slot won (ballot on the slot nodes didx) or which lane's candidate becomes the
+// new slot.  nd / didx: the slots after pv.  Waves A and B evaluate it too (Fit + Balanced
+// profiles), so the winner of pod i-1 is in their registers when step i starts.
+template <bool K32>
+__device__ __forceinline__ ResPub res_argmax(int lane, uint64_t a, uint64_t b, uint64_t cl, uint64_t e1,
+                                             const ResPub &pv, uint32_t nd, uint32_t didx) {
+    const bool pnew = pv.ks != 0 && pv.slot < 0;
+    const uint64_t sc = (lane == pv.slot) ? b : a;
+    uint64_t fk = ((uint32_t)lane < nd && sc) ? (sc | (uint64_t)(0xFFFFFFFFu - didx)) : 0ull;
+    const int srcl = pv.src >= 0 ? pv.src : 0;
+    const uint64_t cw = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(cl >> 32), srcl) << 32) |
+                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)cl, srcl);
+    if (pnew && (uint32_t)lane == pv.nd_old) fk = cw;
+    const uint64_t cand = (pv.ks != 0 && e1 != 0 && key_node(e1) == pv.w) ? 0ull : e1;
+    const uint64_t best = fk > cand ? fk : cand;
+    uint64_t ks;
+    if (K32) {
+        const uint32_t tv = (uint32_t)(best >> 32);
+        const uint32_t k32 = tv ? (tv << 22) | (0x3FFFFFu - key_node(best)) : 0u;
+        const uint32_t m = wave_max_u32_dpp(k32);
+        ks = m ? (((uint64_t)(m >> 22) << 32) | (uint64_t)(0xFFFFFFFFu - (0x3FFFFFu - (m & 0x3FFFFFu)))) : 0ull;
+    } else {
+        ks = wave_max_u64(best);
+    }
+    ResPub np{ks, ks ? key_node(ks) : 0xFFFFFFFFu, -1, -1, nd, {0, 0}};
+    if (ks) {
+        const uint64_t own = __ballot((uint32_t)lane < nd && didx == np.w);
+        if (own) np.slot = (int32_t)__builtin_ctzll(own);
+        else np.src = (int32_t)__builtin_ctzll(__ballot(cand == ks));
+    }
+    return np;
+}
+
 template <uint32_t F, bool K32>
 __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable &t, const PodT<F> *__restrict__ pods,
                                                    const DevCfg &c, uint32_t P, uint32_t K, uint32_t nwin,
@@ -2463,7 +2573,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                         }
                     }
                     pv = np;
-                    if (lane == 0) pub[par] = np;
+                    if (NORM && lane == 0) pub[par] = np;  // (A / B of other profiles compute it themselves)
                     if ((uint32_t)lane == i) {
                         res_key = ks;
                         if (stamps) res_stamp = __builtin_amdgcn_s_memrealtime();
@@ -2572,19 +2682,26 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
             return (act && f) ? ((uint64_t)(tot + 1) << 32) : 0ull;
         };
         uint32_t snew = 0;  // NORM: the static of a slot created by the applied winner
+        // non-normalizing profiles: wave D's argmax evaluated here as well (res_argmax) — pvk = the
+        // winner of the previous pod, ndk / didxk the slots as wave D keeps them — and the staged row
+        // of pvk's new slot read with the step's first LDS reads (stg / stgx)
+        ResPub pvk = none;
+        uint32_t ndk = 0, didxk = 0xFFFFFFFFu;
+        RowT<F> stg = empty_row<F>();
+        int4 stgx = make_int4(0, 0, 0, 0);
         auto apply = [&](const ResPub &pv, int pp, const PodT<F> &pprev) {
             if (pv.ks == 0) return;
             if (pv.slot >= 0) {
                 if (lane == pv.slot) reserve(S, SX, pprev, +1);
             } else {
                 if ((uint32_t)lane == pv.nd_old) {
-                    S = stage[pp][pv.src];
+                    if constexpr (NORM) S = stage[pp][pv.src];
+                    else S = stg;
                     if constexpr (NORM) {
                         SX = stagexN[pp][pv.src];
                         snew = stS[pp][pv.src];
                     } else if (F & kFeatExt) {
-                        const int4 e = stagex[pp][pv.src];
-                        SX.ae0 = e.x; SX.re0 = e.y; SX.ae1 = e.z; SX.re1 = e.w;
+                        SX.ae0 = stgx.x; SX.re0 = stgx.y; SX.ae1 = stgx.z; SX.re1 = stgx.w;
                     }
                     reserve(S, SX, pprev, +1);
                 }
@@ -2618,7 +2735,17 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
             for (uint32_t i = 0; i < kend; ++i) {
                 QS_RSTAMP_BEGIN()
                 const int par = i & 1, pp = par ^ 1;
-                ResPub pv = read_pub(&pub[pp]);
+                ResPub pv;
+                uint64_t ka = 0, kb = 0, kc = 0, k1 = 0;
+                if constexpr (NORM) {
+                    pv = read_pub(&pub[pp]);
+                } else {
+                    pv = pvk;  // the winner of pod i-1, evaluated by this wave in step i-1
+                    const int srcl = pv.src >= 0 ? pv.src : 0;
+                    stg = stage[pp][srcl];
+                    if (F & kFeatExt) stgx = stagex[pp][srcl];
+                    ka = keyA[pp][lane]; kb = keyB[pp][lane]; kc = keyC[pp][lane]; k1 = C1[pp][lane];
+                }
                 const PodT<F> pn1 = wp[i + 1];
                 const uint32_t tst = NORM ? Tcur[min(i + 1, kResNormK - 1) * kResTStride + lane] : 0u;
                 PodN pnn{};
@@ -2627,6 +2754,14 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                 if (NORM && i > 0 && pv.slot == -2) {  // D stopped at pod i-1
                     rescan_ab(i - 1, w & 1);
                     pv = read_pub(&pub[pp]);
+                }
+                if constexpr (!NORM) {  // pod i's winner (wave D's rule), applied in step i+1
+                    const ResPub np = res_argmax<K32>(lane, ka, kb, kc, k1, pv, ndk, didxk);
+                    if (np.ks && np.slot < 0) {
+                        if ((uint32_t)lane == ndk) didxk = np.w;
+                        ++ndk;
+                    }
+                    pvk = np;
                 }
                 const uint32_t nd0 = nd;
                 QS_RSTAMP_MARK(0)
@@ -2654,8 +2789,15 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                 QS_RSTAMP_END()
                 __syncthreads();
             }
-            if (NORM && read_pub(&pub[(kend - 1) & 1]).slot == -2) rescan_ab(kend - 1, w & 1);
-            apply(read_pub(&pub[(kend - 1) & 1]), (kend - 1) & 1, pprev);
+            if constexpr (NORM) {
+                if (read_pub(&pub[(kend - 1) & 1]).slot == -2) rescan_ab(kend - 1, w & 1);
+                apply(read_pub(&pub[(kend - 1) & 1]), (kend - 1) & 1, pprev);
+            } else {
+                const int srcl = pvk.src >= 0 ? pvk.src : 0;
+                stg = stage[(kend - 1) & 1][srcl];
+                if (F & kFeatExt) stgx = stagex[(kend - 1) & 1][srcl];
+                apply(pvk, (kend - 1) & 1, pprev);
+            }
             __syncthreads();  // B2 (D's slot ranks and nodes)
             const uint32_t rk = xrank[lane];
             const bool keep = (uint32_t)lane < nd && rk != 0xFFFFFFFFu;
@@ -2668,6 +2810,11 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
             if (wv == 1) pend = w + 1;
             __syncthreads();  // B3
             nd = (uint32_t)__popcll(__ballot(keep));
+            if constexpr (!NORM) {  // the next window's inherited slots as wave D numbers them
+                ndk = nd;
+                didxk = (uint32_t)lane < nd ? dnode[lane] : 0xFFFFFFFFu;
+                pvk = none;
+            }
             if ((uint32_t)lane < nd) {
                 S = carry[lane];
                 if constexpr (NORM) {
@@ -3090,8 +3237,8 @@ static hipError_t la_stream_res_f(const DevTable &t, const void *pods, const DPo
                                   unsigned long long *nfall, int32_t *on, uint64_t *ok, uint64_t *st, void *ctl,
                                   uint32_t sel_blocks, uint64_t *rdiag, const ResShard &rsh, hipStream_t stream) {
     const uint32_t K = geo.K, G = geo.G, L = geo.L, nwin = (P + K - 1) / K;
-    // sharded: Fit + Balanced profiles, W * L <= 512 keys per cross merge, K <= 32 pods per slot
-    if (rsh.W > 1 && ((F & kFeatNorm) || rsh.W * L > (uint32_t)kResBS || K > 32 || rsh.W > 16 || !rsh.peers))
+    // sharded: W * L <= 512 keys per cross merge, K <= 32 pods per slot
+    if (rsh.W > 1 && (rsh.W * L > (uint32_t)kResBS || K > 32 || rsh.W > 16 || !rsh.peers))
         return hipErrorInvalidValue;
     const uint32_t E2 = geo.e2;  // a pod's G*L <= 512 * E2 chunk keys, E2 per merging thread
     if (G * L > E2 * (uint32_t)kResBS || (E2 == 2 && (F & kFeatNorm))) return hipErrorInvalidValue;

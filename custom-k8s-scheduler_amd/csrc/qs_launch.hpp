@@ -99,14 +99,18 @@ size_t la_stream_res_ctl_bytes();
 // Workgroups of that launch guaranteed co-resident on `cus` CUs (occupancy query, one per CU of margin).
 uint32_t la_stream_res_max_blocks(const LaGeom &geo, uint32_t feat, uint32_t n, uint32_t cus);
 // Resident sharded stream: rank `rank` of W selects its node range and exchanges
-// every pod's shard list through the peer-memory mailboxes (peers[r] = rank r's mailbox base as
+// every pod's shard list (and, normalizing profiles, its partial maxima) through the peer-memory mailboxes (peers[r] = rank r's mailbox base as
 // mapped here; hello / flags / lists = byte offsets of the resident regions in every mailbox);
 // seq tags this run's flags.  W = 1: unsharded (peers unused).
+// Normalizing profiles also exchange each pod's partial maxima {mt, ct, ma, ca} over the rank's node
+// range in the launch: nflags / norm = offsets of [4 slots][32 pods][16 ranks] u64 flags and uint4
+// partials.
 struct ResShard {
     uint32_t W, rank;
     uint64_t seq;
     char *const *peers;
     uint64_t hello, flags, lists;
+    uint64_t nflags, norm;
 };
 // Normalizing profiles (TaintToleration / NodeAffinity) also pass the pod extension records (podx),
 // npart (2 x K x G uint4 partial maxima), norm (2 x 64 NormInfo), stat (2 x K x 128 u32 entry

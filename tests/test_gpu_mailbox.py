@@ -15,21 +15,27 @@ pytestmark = pytest.mark.gpu
 CFG4 = dict(enable_taint=1, enable_affinity=1)
 
 
-def _rank(rank, world, qin, qout, cfg, config, n, p, resident="1"):
+def _rank(rank, world, qin, qout, cfg, config, n, p, resident="1", delay=0.0, wide=False):
     import sys
     import os
+    import time
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [root, os.path.join(root, "custom-k8s-scheduler_amd")]
     os.environ["QS_RESIDENT"] = resident
     import qsched
+    import torch
 
     try:
-        nodes, pods = qsched.synth_generate(config, n, p)
-        with qsched.Scheduler(dict(cfg, engine="lookahead"), device=0, shard=(rank, world, None)) as s:
+        nodes, pods = make_cluster(qsched, config, n, p, wide)
+        # one GPU per rank when the box has them (cross-device mailbox over xGMI), else both on GPU 0
+        dev = rank if torch.cuda.device_count() >= world else 0
+        with qsched.Scheduler(dict(cfg, engine="lookahead"), device=dev, shard=(rank, world, None)) as s:
             qout.put(("h", rank, s.mailbox_export()))
             s.mailbox_connect(qin.get(timeout=120))
             s.load_nodes(nodes)
             st = s.prepare(pods)
+            if delay and rank == 1:  # this rank enters its run late: rank 0's first window waits for it
+                time.sleep(delay)
             stats = st.run()
             pl, keys = st.results()
             st.free()
@@ -39,13 +45,26 @@ def _rank(rank, world, qin, qout, cfg, config, n, p, resident="1"):
         qout.put(("e", rank, repr(e)))
 
 
-def run_world(world, cfg, config, n, p, resident="1"):
+def make_cluster(qsched, config, n, p, wide=False):
+    """spec/synth.md cluster; wide: odd-Ki node memory and decimal pod requests (the wide layout)."""
+    nodes, pods = qsched.synth_generate(config, n, p)
+    if wide:
+        rng = np.random.default_rng(n + p)
+        nodes["alloc_mem"][:] = (rng.integers(64 << 20, 768 << 20, n) | 1) * 1024
+        dec = rng.choice([100 * 10**6, 512 * 10**6, 10**9, 3 * 10**9], p)
+        has = pods["req_mem"] > 0
+        pods["req_mem"] = np.where(has, dec, 0)
+        pods["nz_mem"] = np.where(has, dec, 209715200)
+    return nodes, pods
+
+
+def run_world(world, cfg, config, n, p, resident="1", delay=0.0, wide=False):
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     qout = ctx.Queue()
     qins = [ctx.Queue() for _ in range(world)]
-    procs = [ctx.Process(target=_rank, args=(r, world, qins[r], qout, cfg, config, n, p, resident))
+    procs = [ctx.Process(target=_rank, args=(r, world, qins[r], qout, cfg, config, n, p, resident, delay, wide))
              for r in range(world)]
     for pr in procs:
         pr.start()
@@ -69,25 +88,30 @@ def run_world(world, cfg, config, n, p, resident="1"):
     return results
 
 
-@pytest.mark.parametrize("cfg,config,n,p,resident",
-                         [({}, 2, 3000, 12000, "1"), ({}, 2, 3000, 12000, "0"), ({}, 3, 12000, 20000, "1"),
-                          (CFG4, 4, 2000, 6000, "1")],
-                         ids=["config2-resident", "config2-per-window", "config3-resident", "config4"])
-def test_mailbox_world2_two_processes(oracle, cfg, config, n, p, resident):
-    """Fit + Balanced profiles run the SHARDED RESIDENT stream by default (each
-    rank's selectors score its node range and exchange every pod's shard list through the peers'
-    mailboxes inside the one launch); QS_RESIDENT=0 keeps the per-window mailbox exchange, and the
-    normalizing profile (config 4) always runs per window when sharded."""
-    from qsched import pods_from_struct, synth_generate
+@pytest.mark.parametrize("cfg,config,n,p,resident,delay,wide",
+                         [({}, 2, 3000, 12000, "1", 0.0, False), ({}, 2, 3000, 12000, "0", 0.0, False),
+                          ({}, 3, 12000, 20000, "1", 0.0, False), (CFG4, 4, 2000, 6000, "1", 0.0, False),
+                          (CFG4, 4, 400, 9000, "1", 0.0, False), (CFG4, 4, 2000, 6000, "0", 0.0, False),
+                          ({}, 2, 3000, 12000, "1", 1.0, False), ({}, 2, 3000, 9000, "1", 0.0, True)],
+                         ids=["config2-resident", "config2-per-window", "config3-resident", "config4-resident",
+                              "config4-tight-resident", "config4-per-window", "config2-late-rank", "wide-resident"])
+def test_mailbox_world2_two_processes(oracle, cfg, config, n, p, resident, delay, wide):
+    """Every profile runs the SHARDED RESIDENT stream by default (each rank's
+    selectors score its node range and exchange every pod's shard list — and, for TaintToleration /
+    NodeAffinity, its partial maxima — through the peers' mailboxes inside the one launch);
+    QS_RESIDENT=0 keeps the per-window mailbox exchange.  late-rank: rank 1 enters its run 1 s after
+    rank 0 (the first window's waits are bounded at 5 s); wide: the f64 memory layout."""
+    from qsched import pods_from_struct
+    import qsched
 
-    res = run_world(2, cfg, config, n, p, resident)
-    nodes, pods = synth_generate(config, n, p)
+    res = run_world(2, cfg, config, n, p, resident, delay, wide)
+    nodes, pods = make_cluster(qsched, config, n, p, wide)
     on = {k: v.copy() for k, v in nodes.items()}
     o_pl, o_keys, _ = oracle.schedule(on, pods_from_struct(pods), cfg, nthreads=16)
     for rank in range(2):
         pl, keys, final, eng, res_flag = res[rank]
         assert eng == "lookahead"
-        assert res_flag == (1 if (resident == "1" and not cfg) else 0), rank
+        assert res_flag == (1 if resident == "1" else 0), rank
         bad = np.nonzero(pl != o_pl)[0]
         assert bad.size == 0, f"rank {rank}: {bad.size} placements differ, first at pod {bad[0]}"
         assert np.array_equal(keys, o_keys), rank
