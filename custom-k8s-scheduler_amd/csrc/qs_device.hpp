@@ -363,6 +363,40 @@ __device__ __forceinline__ void store_row_coh(const DevTable &t, __amdgpu_buffer
     }
 }
 
+// The selectors' reads of compact rows, split so that a lane issues the loads of several nodes
+// before it decodes any (res_selector: one memory round trip for a group of nodes instead of one
+// per node): the dynamic quads q0 / q1 (and q3 with extended resources) by sc1 buffer loads (an
+// index past the table reads zeros), and the reciprocals recomputed in registers (rcp_int below:
+// RN(1/a) exactly, for a < 2^24) instead of loaded.
+struct RowQ {
+    u32x4 a, b, e;
+};
+template <uint32_t F>
+__device__ __forceinline__ RowQ load_row_q(__amdgpu_buffer_rsrc_t rs, uint32_t i) {
+    static_assert((F & kFeatWide) == 0, "compact rows only");
+    // aux: sc1, and volatile (bit 31) so the compiler neither drops nor sinks a load into the
+    // conditional block that consumes it: the group's loads stay issued back to back
+    constexpr int kAux = 16 | (int)(1u << 31);
+    RowQ q;
+    q.a = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(i * sizeof(DRow)), 0, kAux);
+    q.b = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(i * sizeof(DRow) + 16), 0, kAux);
+    q.e = u32x4{0u, 0u, 0u, 0u};
+    if (F & kFeatExt) q.e = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(i * sizeof(DRow) + 48), 0, kAux);
+    return q;
+}
+__device__ __forceinline__ double rcp_int(int32_t a);
+template <uint32_t F>
+__device__ __forceinline__ Row decode_row_q(const RowQ &q, RowX &x) {
+    Row r;
+    r.ac = (int32_t)q.a.x; r.am = (int32_t)q.a.y; r.rc = (int32_t)q.a.z; r.rm = (int32_t)q.a.w;
+    r.zc = (int32_t)q.b.x; r.zm = (int32_t)q.b.y; r.np = (int32_t)q.b.z; r.mp = (int32_t)q.b.w;
+    r.yc = r.ac ? rcp_int(r.ac) : 0.0;  // (as the host's RN(1/alloc), 0 where alloc == 0)
+    r.ym = r.am ? rcp_int(r.am) : 0.0;
+    x = RowX{};
+    if (F & kFeatExt) { x.ae0 = (int32_t)q.e.x; x.re0 = (int32_t)q.e.y; x.ae1 = (int32_t)q.e.z; x.re1 = (int32_t)q.e.w; }
+    return r;
+}
+
 // Reserve (spec S7; UP framework/types.go#NodeInfo.update(+1))
 template <class R, class P>
 __device__ __forceinline__ void reserve(R &r, RowX &x, const P &p, int sign) {

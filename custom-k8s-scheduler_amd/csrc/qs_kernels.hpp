@@ -425,7 +425,7 @@ __global__ __launch_bounds__(1024) void k_score_pod1(DevTable t, PodT<F> p, DPod
 // has finished).  Same host layout as k_score_pod1.  NormalizeScore profiles first run
 // k_score_podg_max (same grid: the feasible nodes' taint / affinity raw maxima into gs[2] / gs[3]);
 // the kernel boundary makes them visible to every workgroup here.
-constexpr uint32_t kScorePodGT = 256;
+constexpr uint32_t kScorePodGT = 1024;  // (fewer workgroups: fewer arrivals on the one counter)
 template <uint32_t F>
 __global__ __launch_bounds__(kScorePodGT) void k_score_podg_max(DevTable t, PodT<F> p, DPodX px, uint64_t *gs,
                                                                 uint32_t pidx, HostRow prow) {
@@ -485,7 +485,10 @@ __global__ __launch_bounds__(kScorePodGT) void k_score_podg(DevTable t, PodT<F> 
     }
     best = wave_max_u64(best);
     if (lane == 0) redk[wv] = best;
-    __threadfence_system();  // this workgroup's host-memory stores before its arrival
+    // this workgroup's host-memory stores before its arrival: every storing wave drains its own
+    // stores, the barrier, then thread 0's system-scope release on the arrival counter (one
+    // write-back per workgroup instead of a system fence in every thread)
+    drain_stores();
     __syncthreads();
     if (tid == 0) {
 #pragma unroll
@@ -736,6 +739,7 @@ __device__ __forceinline__ NormInfo norm_reduce(const uint4 *__restrict__ npart,
 // [nv][kw][G][L] that k_la_merge reduces to one top-L per pod and shard.  Normalizing profiles
 // first combine the k_la_norm partials (uniform per pod: scalar loads) and block (0, k, 0) of
 // this process publishes the pod's NormInfo for the resolver.
+constexpr int kSelB = 4;  // compact rows whose loads a selector lane issues together (la_select_block, res_selector)
 template <int BS, int E, uint32_t F>
 __device__ __forceinline__ void la_select_block(uint32_t bid, const DevTable &t, const PodT<F> *__restrict__ pods,
                                                 const DPodX *__restrict__ podx, const DevCfg &c,
@@ -769,6 +773,31 @@ __device__ __forceinline__ void la_select_block(uint32_t bid, const DevTable &t,
     const double ymt = rcp_exact(nf.mt), yma = rcp_exact(nf.ma);
     const uint32_t base = b.start + (uint32_t)w * E * kWave + lane;
     uint32_t tv[E];
+    if constexpr ((F & (kFeatWide | kFeatNorm)) == 0) {
+        // compact Fit + Balanced (+ext) rows: the loads of kSelB nodes issued together, then the
+        // nodes scored one after another (res_selector's form; one round trip per group)
+        const __amdgpu_buffer_rsrc_t rs = row_rsrc<F>(t);
+#pragma unroll
+        for (int j0 = 0; j0 < E; j0 += kSelB) {
+            constexpr int B = E < kSelB ? E : kSelB;
+            RowQ q[B];
+#pragma unroll
+            for (int bb = 0; bb < B && j0 + bb < E; ++bb) q[bb] = load_row_q<F>(rs, base + (j0 + bb) * kWave);
+#pragma unroll
+            for (int bb = 0; bb < B && j0 + bb < E; ++bb) {
+                const int j = j0 + bb;
+                const uint32_t idx = base + j * kWave;
+                tv[j] = 0;
+                if (idx < b.end) {
+                    RowX x;
+                    const Row r = decode_row_q<F>(q[bb], x);
+                    const bool f = feasible<F>(r, x, p, px) && (!aa || aa_ok(t, p.flags, idx));
+                    const uint32_t tot = node_total<F>(r, x, p, px, c, nf.mt, ymt, nf.ma, yma, nullptr);
+                    tv[j] = f ? tot + 1 : 0;
+                }
+            }
+        }
+    } else {
 #pragma unroll
     for (int j = 0; j < E; ++j) {
         const uint32_t idx = base + j * kWave;
@@ -780,6 +809,7 @@ __device__ __forceinline__ void la_select_block(uint32_t bid, const DevTable &t,
             const uint32_t tot = node_total<F>(r, x, p, px, c, nf.mt, ymt, nf.ma, yma, nullptr);
             tv[j] = f ? tot + 1 : 0;
         }
+    }
     }
     uint64_t *out = G == 1 ? lists + (size_t)b.v * sh.RS + (size_t)b.k * GLp
                            : clists + (((size_t)b.vs * sh.kw + b.k) * G + b.g) * L;
@@ -2062,6 +2092,43 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
                 const DPodX px = load_vgpr(podx + s0 + k);
                 uint32_t raw[E];  // (taint raw | affinity raw << 16), 0xFFFFFFFF = infeasible / outside
                 uint32_t mt = 0, ma = 0;
+                if constexpr ((F & kFeatWide) == 0) {
+                    // compact rows: a lane issues the loads of kSelB nodes (rows and masks) before it
+                    // decodes any (one round trip per group instead of one per node), then scores them
+                    // one after another
+#pragma unroll
+                    for (int j0 = 0; j0 < E; j0 += kSelB) {
+                        constexpr int B = E < kSelB ? E : kSelB;
+                        RowQ q[B];
+                        DMask mk[B];
+#pragma unroll
+                        for (int b = 0; b < B && j0 + b < E; ++b) {
+                            const uint32_t idx = base + (j0 + b) * kWave;
+                            q[b] = load_row_q<F>(rs, idx);
+                            mk[b] = t.masks[idx < end ? idx : start];
+                        }
+#pragma unroll
+                        for (int b = 0; b < B && j0 + b < E; ++b) {  // one node after another (bounded registers)
+                            const int j = j0 + b;
+                            tv[j] = 0;
+                            raw[j] = 0xFFFFFFFFu;
+                            if (base + j * kWave < end) {
+                                RowX x;
+                                const Row r = decode_row_q<F>(q[b], x);
+                                x.th = mk[b].th; x.ts = mk[b].ts; x.lb0 = mk[b].lb0; x.lb1 = mk[b].lb1;
+                                if (feasible<F>(r, x, p, px)) {
+                                    const uint32_t rt = (F & kFeatTaint) ? taint_raw(x, px) : 0u;
+                                    const uint32_t ra = (F & kFeatAffinity) ? affinity_raw(x, p, px) : 0u;
+                                    raw[j] = rt | (ra << 16);
+                                    mt = rt > mt ? rt : mt;
+                                    ma = ra > ma ? ra : ma;
+                                    tv[j] = __umul24((uint32_t)p.wfit, la_score(r, p, cv)) +
+                                            __umul24((uint32_t)p.wbal, ba_score(r, p, cv));
+                                }
+                            }
+                        }
+                    }
+                } else {
 #pragma unroll
                 for (int j = 0; j < E; ++j) {
                     const uint32_t idx = base + j * kWave;
@@ -2082,6 +2149,7 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
                                     __umul24((uint32_t)p.wbal, ba_score(r, p, cv));
                         }
                     }
+                }
                 }
                 // the chunk's maxima and the counts of feasible nodes attaining them
                 mt = wave_max_u32(mt);
@@ -2152,6 +2220,27 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
                     if (F & kFeatTaint) tot += __umul24((uint32_t)cv.wtt, tt_norm(raw[j] & 0xFFFFu, nf.mt, ymt));
                     if (F & kFeatAffinity) tot += __umul24((uint32_t)cv.wna, na_norm(raw[j] >> 16, nf.ma, yma));
                     tv[j] = raw[j] != 0xFFFFFFFFu ? tot + 1 : 0u;
+                }
+            } else if constexpr ((F & kFeatWide) == 0) {
+                const DPodX px{};
+#pragma unroll
+                for (int j0 = 0; j0 < E; j0 += kSelB) {  // kSelB nodes' loads in flight, as above
+                    constexpr int B = E < kSelB ? E : kSelB;
+                    RowQ q[B];
+#pragma unroll
+                    for (int b = 0; b < B && j0 + b < E; ++b) q[b] = load_row_q<F>(rs, base + (j0 + b) * kWave);
+#pragma unroll
+                    for (int b = 0; b < B && j0 + b < E; ++b) {  // one node after another (bounded registers)
+                        const int j = j0 + b;
+                        tv[j] = 0;
+                        if (base + j * kWave < end) {
+                            RowX x;
+                            const Row r = decode_row_q<F>(q[b], x);
+                            const bool f = feasible<F>(r, x, p, px);
+                            const uint32_t tot = node_total<F>(r, x, p, px, cv, 0, 0.0, 0, 0.0, nullptr);
+                            tv[j] = f ? tot + 1 : 0;
+                        }
+                    }
                 }
             } else {
                 const DPodX px{};
