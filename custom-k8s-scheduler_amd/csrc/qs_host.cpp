@@ -1366,9 +1366,14 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                     c->cus = cu;
                 }
                 // two selector workgroups per CU when the occupancy check admits them, else one
-                LaGeom rgeo = la_stream_res_plan(geo, c->dc.feat, n, (uint32_t)c->cus, 2);
+                // (normalizing profiles: the resident resolver is the four-wave one whatever the
+                // per-window geometry picked — sharded contexts keep the single-wave kernel there,
+                // epl > 1 — unless QS_NORM_WAVES=1 pins the single-wave path)
+                LaGeom pgeo = geo;
+                if (norm && overlap && !(nw && nw[0] == '1')) pgeo.waves = 4;
+                LaGeom rgeo = la_stream_res_plan(pgeo, c->dc.feat, n, (uint32_t)c->cus, 2);
                 if (rgeo.G > 0 && rgeo.K * rgeo.G + 1 > la_stream_res_max_blocks(rgeo, c->dc.feat, n, (uint32_t)c->cus))
-                    rgeo = la_stream_res_plan(geo, c->dc.feat, n, (uint32_t)c->cus, 1);
+                    rgeo = la_stream_res_plan(pgeo, c->dc.feat, n, (uint32_t)c->cus, 1);
                 // one selector workgroup per (pod, chunk) task of a window, at most one per
                 // remaining CU (they loop over the tasks otherwise); QS_RES_SEL overrides
                 static const char *senv = getenv("QS_RES_SEL");

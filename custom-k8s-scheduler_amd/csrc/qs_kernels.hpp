@@ -2465,42 +2465,6 @@ __device__ __forceinline__ uint64_t res_rescan_wait(const uint64_t *red_k) {
     return ks;
 }
 
-// Wave D's rule for the winner of window pod i (non-normalizing profiles): the slot keys of waves
-// A / B picked by pod i-1's winner pv (B's where that slot won), the new slot pv created read from
-// wave C's key at its source lane, the best clean list entry unless pv took its node; one 64-lane
-// max; then which slot won (ballot on the slot nodes didx) or which lane's candidate becomes the
-// new slot.  nd / didx: the slots after pv.  Waves A and B evaluate it too (Fit + Balanced
-// profiles), so the winner of pod i-1 is in their registers when step i starts.
-template <bool K32>
-__device__ __forceinline__ ResPub res_argmax(int lane, uint64_t a, uint64_t b, uint64_t cl, uint64_t e1,
-                                             const ResPub &pv, uint32_t nd, uint32_t didx) {
-    const bool pnew = pv.ks != 0 && pv.slot < 0;
-    const uint64_t sc = (lane == pv.slot) ? b : a;
-    uint64_t fk = ((uint32_t)lane < nd && sc) ? (sc | (uint64_t)(0xFFFFFFFFu - didx)) : 0ull;
-    const int srcl = pv.src >= 0 ? pv.src : 0;
-    const uint64_t cw = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(cl >> 32), srcl) << 32) |
-                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)cl, srcl);
-    if (pnew && (uint32_t)lane == pv.nd_old) fk = cw;
-    const uint64_t cand = (pv.ks != 0 && e1 != 0 && key_node(e1) == pv.w) ? 0ull : e1;
-    const uint64_t best = fk > cand ? fk : cand;
-    uint64_t ks;
-    if (K32) {
-        const uint32_t tv = (uint32_t)(best >> 32);
-        const uint32_t k32 = tv ? (tv << 22) | (0x3FFFFFu - key_node(best)) : 0u;
-        const uint32_t m = wave_max_u32_dpp(k32);
-        ks = m ? (((uint64_t)(m >> 22) << 32) | (uint64_t)(0xFFFFFFFFu - (0x3FFFFFu - (m & 0x3FFFFFu)))) : 0ull;
-    } else {
-        ks = wave_max_u64(best);
-    }
-    ResPub np{ks, ks ? key_node(ks) : 0xFFFFFFFFu, -1, -1, nd, {0, 0}};
-    if (ks) {
-        const uint64_t own = __ballot((uint32_t)lane < nd && didx == np.w);
-        if (own) np.slot = (int32_t)__builtin_ctzll(own);
-        else np.src = (int32_t)__builtin_ctzll(__ballot(cand == ks));
-    }
-    return np;
-}
-
 template <uint32_t F, bool K32>
 __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable &t, const PodT<F> *__restrict__ pods,
                                                    const DevCfg &c, uint32_t P, uint32_t K, uint32_t nwin,
@@ -2662,7 +2626,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                         }
                     }
                     pv = np;
-                    if (NORM && lane == 0) pub[par] = np;  // (A / B of other profiles compute it themselves)
+                    if (lane == 0) pub[par] = np;
                     if ((uint32_t)lane == i) {
                         res_key = ks;
                         if (stamps) res_stamp = __builtin_amdgcn_s_memrealtime();
@@ -2771,26 +2735,19 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
             return (act && f) ? ((uint64_t)(tot + 1) << 32) : 0ull;
         };
         uint32_t snew = 0;  // NORM: the static of a slot created by the applied winner
-        // non-normalizing profiles: wave D's argmax evaluated here as well (res_argmax) — pvk = the
-        // winner of the previous pod, ndk / didxk the slots as wave D keeps them — and the staged row
-        // of pvk's new slot read with the step's first LDS reads (stg / stgx)
-        ResPub pvk = none;
-        uint32_t ndk = 0, didxk = 0xFFFFFFFFu;
-        RowT<F> stg = empty_row<F>();
-        int4 stgx = make_int4(0, 0, 0, 0);
         auto apply = [&](const ResPub &pv, int pp, const PodT<F> &pprev) {
             if (pv.ks == 0) return;
             if (pv.slot >= 0) {
                 if (lane == pv.slot) reserve(S, SX, pprev, +1);
             } else {
                 if ((uint32_t)lane == pv.nd_old) {
-                    if constexpr (NORM) S = stage[pp][pv.src];
-                    else S = stg;
+                    S = stage[pp][pv.src];
                     if constexpr (NORM) {
                         SX = stagexN[pp][pv.src];
                         snew = stS[pp][pv.src];
                     } else if (F & kFeatExt) {
-                        SX.ae0 = stgx.x; SX.re0 = stgx.y; SX.ae1 = stgx.z; SX.re1 = stgx.w;
+                        const int4 e = stagex[pp][pv.src];
+                        SX.ae0 = e.x; SX.re0 = e.y; SX.ae1 = e.z; SX.re1 = e.w;
                     }
                     reserve(S, SX, pprev, +1);
                 }
@@ -2824,17 +2781,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
             for (uint32_t i = 0; i < kend; ++i) {
                 QS_RSTAMP_BEGIN()
                 const int par = i & 1, pp = par ^ 1;
-                ResPub pv;
-                uint64_t ka = 0, kb = 0, kc = 0, k1 = 0;
-                if constexpr (NORM) {
-                    pv = read_pub(&pub[pp]);
-                } else {
-                    pv = pvk;  // the winner of pod i-1, evaluated by this wave in step i-1
-                    const int srcl = pv.src >= 0 ? pv.src : 0;
-                    stg = stage[pp][srcl];
-                    if (F & kFeatExt) stgx = stagex[pp][srcl];
-                    ka = keyA[pp][lane]; kb = keyB[pp][lane]; kc = keyC[pp][lane]; k1 = C1[pp][lane];
-                }
+                ResPub pv = read_pub(&pub[pp]);
                 const PodT<F> pn1 = wp[i + 1];
                 const uint32_t tst = NORM ? Tcur[min(i + 1, kResNormK - 1) * kResTStride + lane] : 0u;
                 PodN pnn{};
@@ -2843,14 +2790,6 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                 if (NORM && i > 0 && pv.slot == -2) {  // D stopped at pod i-1
                     rescan_ab(i - 1, w & 1);
                     pv = read_pub(&pub[pp]);
-                }
-                if constexpr (!NORM) {  // pod i's winner (wave D's rule), applied in step i+1
-                    const ResPub np = res_argmax<K32>(lane, ka, kb, kc, k1, pv, ndk, didxk);
-                    if (np.ks && np.slot < 0) {
-                        if ((uint32_t)lane == ndk) didxk = np.w;
-                        ++ndk;
-                    }
-                    pvk = np;
                 }
                 const uint32_t nd0 = nd;
                 QS_RSTAMP_MARK(0)
@@ -2878,15 +2817,8 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                 QS_RSTAMP_END()
                 __syncthreads();
             }
-            if constexpr (NORM) {
-                if (read_pub(&pub[(kend - 1) & 1]).slot == -2) rescan_ab(kend - 1, w & 1);
-                apply(read_pub(&pub[(kend - 1) & 1]), (kend - 1) & 1, pprev);
-            } else {
-                const int srcl = pvk.src >= 0 ? pvk.src : 0;
-                stg = stage[(kend - 1) & 1][srcl];
-                if (F & kFeatExt) stgx = stagex[(kend - 1) & 1][srcl];
-                apply(pvk, (kend - 1) & 1, pprev);
-            }
+            if (NORM && read_pub(&pub[(kend - 1) & 1]).slot == -2) rescan_ab(kend - 1, w & 1);
+            apply(read_pub(&pub[(kend - 1) & 1]), (kend - 1) & 1, pprev);
             __syncthreads();  // B2 (D's slot ranks and nodes)
             const uint32_t rk = xrank[lane];
             const bool keep = (uint32_t)lane < nd && rk != 0xFFFFFFFFu;
@@ -2899,11 +2831,6 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
             if (wv == 1) pend = w + 1;
             __syncthreads();  // B3
             nd = (uint32_t)__popcll(__ballot(keep));
-            if constexpr (!NORM) {  // the next window's inherited slots as wave D numbers them
-                ndk = nd;
-                didxk = (uint32_t)lane < nd ? dnode[lane] : 0xFFFFFFFFu;
-                pvk = none;
-            }
             if ((uint32_t)lane < nd) {
                 S = carry[lane];
                 if constexpr (NORM) {
@@ -3018,6 +2945,24 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                 // masked by D, which then never names that lane as a new slot's source.
                 const uint32_t en_node = en ? key_node(en) : 0u;
                 uint32_t dword = dirty[en_node >> 5];
+                // compact Fit + Balanced rows: pod i+1's candidate row, issued first — its address
+                // needs the entry only (a dirty entry's row is loaded and never used), so the load
+                // has the whole step to arrive (config 3: +8%).  The normalizing and wide rows keep
+                // the late issue below (their larger rows held in flight across the step cost more
+                // than the latency they hide: config 4 -16%, wide -9% measured).
+                constexpr bool kEarly = !NORM && (F & kFeatWide) == 0;
+                RowT<F> rn = r1;
+                RowX xn = x1;
+                if (!kEarly) {
+                } else if (i + 1 < kend) {
+                    rn = load_row<F>(t, en_node);
+                    xn = load_rowx<F>(t, en_node);
+                } else if (pref) {
+                    // last pod: the next window's first candidate rows (its entries arrived meanwhile;
+                    // a node dirtied from here on is masked out at the boundary)
+                    rn = load_row<F>(t, pe0 ? key_node(pe0) : 0u);
+                    xn = load_rowx<F>(t, pe0 ? key_node(pe0) : 0u);
+                }
                 const PodT<F> pn1 = wp[i + 1];
                 const uint32_t kn = min(i + 1, kend - 1);
                 NormInfo nf{0, 0, 0, 0};
@@ -3062,20 +3007,24 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                     const bool dirt = ((dword >> (en_node & 31)) & 1u) != 0;
                     c1 = (en != 0 && !dirt) ? en : 0ull;  // pod i+1 against the dirty set through pod i-1
                     C1[par][lane] = c1;
-                    r1 = load_row<F>(t, c1 ? key_node(c1) : 0u);
-                    x1 = load_rowx<F>(t, c1 ? key_node(c1) : 0u);
+                    if constexpr (!kEarly) {
+                        rn = load_row<F>(t, c1 ? key_node(c1) : 0u);
+                        xn = load_rowx<F>(t, c1 ? key_node(c1) : 0u);
+                    }
                     if constexpr (decltype(lm)::value == 2) {
                         en = eZ;
                     } else {
                         en = ent(lists, i + 3, kend);
                         if constexpr (decltype(lm)::value == 1) eZ = ent(lists, i + 4, kend);
                     }
-                } else if (pref) {
+                } else if (!kEarly && pref) {
                     // last pod: the next window's first candidate rows (its entries arrived meanwhile;
                     // a node dirtied from here on is masked out at the boundary)
-                    r1 = load_row<F>(t, pe0 ? key_node(pe0) : 0u);
-                    x1 = load_rowx<F>(t, pe0 ? key_node(pe0) : 0u);
+                    rn = load_row<F>(t, pe0 ? key_node(pe0) : 0u);
+                    xn = load_rowx<F>(t, pe0 ? key_node(pe0) : 0u);
                 }
+                r1 = rn;
+                x1 = xn;
                 // NORM: this parity's pair now holds pod i+2's statics (the next window's pod
                 // i+2-kend when prefetched)
                 if (i + 2 < kend) stat_load(c1s1, c1s2, stats, i + 2, kend);
