@@ -2730,11 +2730,16 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                 if (act && !f) fl = holder_flags<F>(st, pn.nf.mt, pn.nf.ma);
                 return ((act && f) ? ((uint64_t)(tot + 1) << 32) : 0ull) | fl;
             }
+#ifdef QS_EXP_CHEAP_AB  // timing experiment only (wrong placements): no key arithmetic in A / B
+            return act ? ((uint64_t)(((uint32_t)(r.rc + q.rc) & 511u) + 1) << 32) : 0ull;
+#endif
             const bool f = feasible<F>(r, x, q, px);
             const uint32_t tot = node_total<F>(r, x, q, px, cv, 0, 0.0, 0, 0.0, nullptr);
             return (act && f) ? ((uint64_t)(tot + 1) << 32) : 0ull;
         };
         uint32_t snew = 0;  // NORM: the static of a slot created by the applied winner
+        // (the new slot's row is read from LDS at pv.src: a per-lane readlane of the own-lane staged
+        // rows instead was measured slower, A / B +90 busy cycles a step)
         auto apply = [&](const ResPub &pv, int pp, const PodT<F> &pprev) {
             if (pv.ks == 0) return;
             if (pv.slot >= 0) {
@@ -2990,8 +2995,13 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                     tot = norm_total<F>(cr, pn1, cv, c1s1, nf.mt, yr.x, nf.ma, yr.y);
                     if (!f) fl = holder_flags<F>(c1s1, nf.mt, nf.ma);
                 } else {
+#ifdef QS_EXP_CHEAP_C  // timing experiment only (wrong placements): no key arithmetic in C
+                    f = true;
+                    tot = (uint32_t)(cr.rc + pn1.rc) & 511u;
+#else
                     f = feasible<F>(cr, crx, pn1, px);
                     tot = node_total<F>(cr, crx, pn1, px, cv, 0, 0.0, 0, 0.0, nullptr);
+#endif
                 }
                 QS_RSTAMP_MARK(1)
                 stage[par][lane] = r1;
