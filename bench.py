@@ -284,6 +284,15 @@ def pmc_traffic(kernel_prefix):
     return None
 
 
+_T0 = time.time()
+
+
+def progress(msg):
+    """A phase line on stderr (the JSON line alone goes to stdout): a full run takes minutes, and
+    the GPU pool takes a command silent for 3 minutes to be hung."""
+    print(f"bench [{time.time() - _T0:6.1f} s] {msg}", file=sys.stderr, flush=True)
+
+
 def host_info():
     """The box the CPU arms ran on (north_star: "core count stated")."""
     model = None
@@ -299,7 +308,32 @@ def host_info():
     except AttributeError:
         usable = None
     return {"cpu_model": model, "nproc": os.cpu_count(), "usable_cpus": usable,
-            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+            "cgroup_cpus": cgroup_cpus(), "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+
+
+def cgroup_cpus():
+    """CPUs' worth of time the cgroup grants (cgroup v2 cpu.max quota / period; None = no quota).
+    The GPU box's affinity mask shows every CPU of the machine while its share is 16: OpenMP at the
+    mask's width oversubscribes the quota (ROUND 4: the 256-thread arm did not finish in 3 min)."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else max(1, -(-int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    try:  # cgroup v1
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else max(1, -(-q // per))
+    except (OSError, ValueError):
+        return None
+
+
+def effective_cpus():
+    """min(affinity mask, cgroup quota, OMP_NUM_THREADS when the environment sets the share)."""
+    h = host_info()
+    omp = h["omp_num_threads"]
+    cands = [x for x in (h["usable_cpus"], h["cgroup_cpus"], int(omp) if omp and omp.isdigit() else None) if x]
+    return min(cands) if cands else (os.cpu_count() or 16)
 
 
 def cpu_baseline(nodes, pods, n_nodes, n_pods, sample, threads=1, gpu_placement=None, repeats=5):
@@ -313,7 +347,8 @@ def cpu_baseline(nodes, pods, n_nodes, n_pods, sample, threads=1, gpu_placement=
     sample = n_pods if whole else sample
     sub = qsched.pods_from_struct(pods[:sample])
     times, placement = [], None
-    for _ in range(repeats):
+    for r in range(repeats):
+        progress(f"cpu baseline: {sample:,} pods, {threads} thread(s), run {r + 1} of {repeats}")
         on = {k: v.copy() for k, v in nodes.items()}
         t0 = time.perf_counter()
         pl, _, _ = O.schedule(on, sub, nthreads=threads)
@@ -344,7 +379,8 @@ def cpu_baseline_framework(n_nodes=5000, sample=4000, threads=16, repeats=5):
     import subprocess
     exe = os.path.join(ROOT, "custom-k8s-scheduler_amd", "cpu_framework")
     runs = []
-    for _ in range(repeats):
+    for rr in range(repeats):
+        progress(f"cpu framework baseline: run {rr + 1} of {repeats}")
         r = subprocess.run([exe, "2", str(n_nodes), str(sample), str(threads)], capture_output=True, text=True,
                            timeout=300)
         runs.append(json.loads(r.stdout.strip().splitlines()[-1]))
@@ -699,19 +735,25 @@ def main():
         print(json.dumps(run_leg(cx, a, a.leg)), flush=True)
         return 0
     workload = a.workload if a.workload != "auto" else ("config2" if cx.world == 1 else "config3")
+    progress(f"{workload}: timed stream ({a.steps} steps, {a.warmup} warmup)")
     if cx.world > 1 and workload == "config3":
         m = measure_sharded(cx, a, workload)
     else:
         m = measure(cx, a, workload, a.steps, a.warmup)
     c3 = c4 = c5 = scan = None
     if cx.world == 1 and workload == "config2" and not a.no_config3:
+        progress("config3 leg")
         c3 = measure(cx, a, "config3", 1, 1, with_diag=False)
+        progress("config4 leg")
         c4 = measure(cx, a, "config4", 3, 1, with_diag=False)
+        progress("config5 leg")
         c5 = measure(cx, a, "config5", 3, 1, with_diag=False)
     if cx.world == 1 and not a.no_scan:
+        progress("scan roofline leg")
         scan = scan_roofline(cx, a)
     e2e = fw = wide = None
     if cx.world == 1 and workload == "config2" and not a.no_extra:
+        progress("end-to-end, framework and wide legs")
         e2e = e2e_leg(cx, m["nodes"], m["pods"], m["placement"])
         fw = framework_leg(cx)
         wide = wide_leg(cx, a)
@@ -747,8 +789,10 @@ def main():
             if m["transport_tried"]:
                 out["config"]["transport_fallback_from"] = m["transport_tried"]
         if m["sharded"] or (cx.world == 1 and not a.no_cpu):
+            progress("oracle check of the timed stream")
             out["check"] = check_stream(m)
         if c3 is not None:
+            progress("oracle checks of the config 3 / 4 / 5 legs")
             out["config3"] = {"workload": c3["desc"] + " (1 GPU: the N=1 point of the curve)",
                               "value": round(c3["value"], 1), "unit": "pods/s",
                               "evals_per_s": round(c3["value"] * c3["n_nodes"], 1),
@@ -782,10 +826,14 @@ def main():
             out["cpu_baseline_parallel"] = cpu_baseline(m["nodes"], m["pods"], m["n_nodes"], m["n_pods"],
                                                         a.cpu_sample, threads=16,
                                                         gpu_placement=m["placement"])
-            usable = host_info()["usable_cpus"] or os.cpu_count() or 16
+            usable = effective_cpus()
             if usable != 16:  # the OpenMP arm at every CPU this process may use (a bounded sample)
                 out["cpu_baseline_parallel_nproc"] = cpu_baseline(m["nodes"], m["pods"], m["n_nodes"], m["n_pods"],
                                                                   20000, threads=usable)
+            else:
+                out["cpu_baseline_parallel_nproc"] = {
+                    "skipped": "this process may use 16 CPUs (affinity / cgroup quota / OMP_NUM_THREADS): "
+                               "the nproc arm is cpu_baseline_parallel", "host": host_info()}
             out["cpu_baseline_framework"] = cpu_baseline_framework()
         print(json.dumps(out), flush=True)
     if cx.dist is not None:
