@@ -690,9 +690,13 @@ def framework_leg(cx, n_nodes=5000, n_pods=5000):
                              "placements_match": bool(np.array_equal(placement, ref))}}
     import subprocess
     exe = os.path.join(ROOT, "custom-k8s-scheduler_amd", "fw_latency")
-    for outputs, key in ((1, "native"), (0, "native_best_only")):
+    # mode 1: every per-node output copied out; 0: best key only; 2: the packed per-node words read in
+    # place (qs_score_pod_packed, §4.6); the 50,000-node rows: any table size takes the same launch
+    for nn, npods, outputs, key in ((n_nodes, n_pods, 1, "native"), (n_nodes, n_pods, 0, "native_best_only"),
+                                    (n_nodes, n_pods, 2, "native_packed"), (50000, 3000, 2, "native_50k_packed"),
+                                    (50000, 3000, 1, "native_50k")):
         try:
-            r = subprocess.run([exe, str(n_nodes), str(n_pods), str(outputs)], capture_output=True, text=True,
+            r = subprocess.run([exe, str(nn), str(npods), str(outputs)], capture_output=True, text=True,
                                timeout=120)
             out[key] = json.loads(r.stdout.strip().splitlines()[-1])
         except Exception as e:  # reported, not fatal: the ctypes numbers stand
