@@ -257,3 +257,19 @@ def test_world2_measure_fails_on_one_rank(fail):
         p.join(60)
         assert p.exitcode == 0
     assert res == [(0, "rccl", ["mailbox"]), (1, "rccl", ["mailbox"])]
+
+
+def test_cpu_arms_capped_by_the_process_share(monkeypatch):
+    """The nproc OpenMP arm uses the smallest of the affinity mask, the cgroup quota and
+    OMP_NUM_THREADS (round 4: the GPU box's mask shows 256 CPUs against a 16-CPU share)."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    monkeypatch.setattr(bench, "cgroup_cpus", lambda: 16)
+    monkeypatch.setenv("OMP_NUM_THREADS", "64")
+    monkeypatch.setattr(bench.os, "sched_getaffinity", lambda pid: set(range(256)))
+    assert bench.effective_cpus() == 16
+    monkeypatch.setattr(bench, "cgroup_cpus", lambda: None)
+    assert bench.effective_cpus() == 64
+    monkeypatch.delenv("OMP_NUM_THREADS")
+    assert bench.effective_cpus() == 256
