@@ -2950,23 +2950,22 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                 // masked by D, which then never names that lane as a new slot's source.
                 const uint32_t en_node = en ? key_node(en) : 0u;
                 uint32_t dword = dirty[en_node >> 5];
-                // compact Fit + Balanced rows: pod i+1's candidate row, issued first — its address
-                // needs the entry only (a dirty entry's row is loaded and never used), so the load
-                // has the whole step to arrive (config 3: +8%).  The normalizing and wide rows keep
-                // the late issue below (their larger rows held in flight across the step cost more
-                // than the latency they hide: config 4 -16%, wide -9% measured).
-                constexpr bool kEarly = !NORM && (F & kFeatWide) == 0;
+                // Fit + Balanced (+ext) rows, both layouts: pod i+1's candidate row, issued first — its
+                // address needs the entry only (a dirty entry's row is loaded and never used), so the
+                // load has the whole step to arrive; one unconditional load (the last pod: the next
+                // window's first candidate when prefetched, else node 0's row, never used), because a
+                // load under a branch left the compiler's wait tracking conservative — it waited for the
+                // just-issued rows early in the step (wide: -9 % with the branch, +3 % without;
+                // config 2 +1.5 %, config 3 +1 %).  The normalizing rows keep the late issue below
+                // (their larger rows and statics held across the step measured -16 %).
+                constexpr bool kEarly = !NORM;
                 RowT<F> rn = r1;
                 RowX xn = x1;
-                if (!kEarly) {
-                } else if (i + 1 < kend) {
-                    rn = load_row<F>(t, en_node);
-                    xn = load_rowx<F>(t, en_node);
-                } else if (pref) {
-                    // last pod: the next window's first candidate rows (its entries arrived meanwhile;
-                    // a node dirtied from here on is masked out at the boundary)
-                    rn = load_row<F>(t, pe0 ? key_node(pe0) : 0u);
-                    xn = load_rowx<F>(t, pe0 ? key_node(pe0) : 0u);
+                if constexpr (kEarly) {
+                    // (last pod: a node dirtied from here on is masked out at the boundary)
+                    const uint32_t ln = i + 1 < kend ? en_node : (pref && pe0 ? key_node(pe0) : 0u);
+                    rn = load_row<F>(t, ln);
+                    xn = load_rowx<F>(t, ln);
                 }
                 const PodT<F> pn1 = wp[i + 1];
                 const uint32_t kn = min(i + 1, kend - 1);
