@@ -2950,23 +2950,17 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                 // masked by D, which then never names that lane as a new slot's source.
                 const uint32_t en_node = en ? key_node(en) : 0u;
                 uint32_t dword = dirty[en_node >> 5];
-                // Fit + Balanced (+ext) rows, both layouts: pod i+1's candidate row, issued first — its
-                // address needs the entry only (a dirty entry's row is loaded and never used), so the
-                // load has the whole step to arrive; one unconditional load (the last pod: the next
-                // window's first candidate when prefetched, else node 0's row, never used), because a
-                // load under a branch left the compiler's wait tracking conservative — it waited for the
-                // just-issued rows early in the step (wide: -9 % with the branch, +3 % without;
-                // config 2 +1.5 %, config 3 +1 %).  The normalizing rows keep the late issue below
-                // (their larger rows and statics held across the step measured -16 %).
-                constexpr bool kEarly = !NORM;
-                RowT<F> rn = r1;
-                RowX xn = x1;
-                if constexpr (kEarly) {
-                    // (last pod: a node dirtied from here on is masked out at the boundary)
-                    const uint32_t ln = i + 1 < kend ? en_node : (pref && pe0 ? key_node(pe0) : 0u);
-                    rn = load_row<F>(t, ln);
-                    xn = load_rowx<F>(t, ln);
-                }
+                // pod i+1's candidate row, issued first: its address needs the entry only (a dirty
+                // entry's row is loaded and never used), so the load has the whole step to arrive.
+                // One unconditional load (the last pod: the next window's first candidate when
+                // prefetched, else node 0's row, never used; a node dirtied from here on is masked
+                // out at the boundary): issued at the step's end, or under a branch, the compiler's
+                // wait tracking waited for the rows early in the next step (measured: config 2 +1.5 %,
+                // config 3 +1 %, wide +3 %, config 4 +3.6 % against the late issue; -9 % / -16 % for
+                // wide / config 4 with the load under a branch).
+                const uint32_t ln = i + 1 < kend ? en_node : (pref && pe0 ? key_node(pe0) : 0u);
+                const RowT<F> rn = load_row<F>(t, ln);
+                const RowX xn = load_rowx<F>(t, ln);
                 const PodT<F> pn1 = wp[i + 1];
                 const uint32_t kn = min(i + 1, kend - 1);
                 NormInfo nf{0, 0, 0, 0};
@@ -3016,21 +3010,12 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                     const bool dirt = ((dword >> (en_node & 31)) & 1u) != 0;
                     c1 = (en != 0 && !dirt) ? en : 0ull;  // pod i+1 against the dirty set through pod i-1
                     C1[par][lane] = c1;
-                    if constexpr (!kEarly) {
-                        rn = load_row<F>(t, c1 ? key_node(c1) : 0u);
-                        xn = load_rowx<F>(t, c1 ? key_node(c1) : 0u);
-                    }
                     if constexpr (decltype(lm)::value == 2) {
                         en = eZ;
                     } else {
                         en = ent(lists, i + 3, kend);
                         if constexpr (decltype(lm)::value == 1) eZ = ent(lists, i + 4, kend);
                     }
-                } else if (!kEarly && pref) {
-                    // last pod: the next window's first candidate rows (its entries arrived meanwhile;
-                    // a node dirtied from here on is masked out at the boundary)
-                    rn = load_row<F>(t, pe0 ? key_node(pe0) : 0u);
-                    xn = load_rowx<F>(t, pe0 ? key_node(pe0) : 0u);
                 }
                 r1 = rn;
                 x1 = xn;
