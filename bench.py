@@ -74,6 +74,8 @@ def parse(argv=None):
     ap.add_argument("--leg", default=None, choices=["config2", "wide", "config3", "config4", "config5", "framework"],
                     help="run only this sub-leg on one GPU and print its JSON object (iteration probe, "
                          "not the bench line)")
+    ap.add_argument("--rccl-sample", type=int, default=20000,
+                    help="pods of the per-pod RCCL all-reduce leg (config-3 cluster; 0 = skip the leg)")
     ap.add_argument("--dry-run", action="store_true",
                     help="print the launch plan (torchrun argv for --gpus N > 1) and exit, no GPU touched")
     return ap.parse_args(argv)
@@ -496,6 +498,65 @@ def measure_sharded(cx, a, workload):
     raise SystemExit(f"bench.py: every transport failed: {tried}")
 
 
+def measure_rccl_per_pod(cx, a):
+    """SURVEY.md §8(e) C1, RCCL as-is: the config-3 cluster (50,000 nodes) and a
+    bounded sample of its pod stream (the first --rccl-sample arrivals, same generator) on the per-pod
+    all-reduce engine: each rank scans its node shard per pod and the ranks max-reduce one packed
+    8-byte key with ncclAllReduce (QS_ENGINE_ALLREDUCE).  One warm-up and one timed step, MAX over
+    ranks; reported beside the sharded line as the labelled baseline of the lookahead transports.
+    Every rank runs the same collectives whatever fails locally (run_phase / agree)."""
+    gen, n_nodes, _, _ = WORKLOADS["config3"]
+    sample = a.rccl_sample
+    nodes, pods = qsched.synth_generate(gen, n_nodes, sample)
+    cfg = {"engine": "allreduce"}
+    s = run_phase(cx, lambda: qsched.Scheduler(cfg, device=cx.local,
+                                               shard=cx.shard() if cx.world > 1 else (0, 1, qsched.dist_unique_id())))
+    try:
+        def setup():
+            s.load_nodes(nodes)
+            st_ = s.prepare(pods)
+            s.save_table()
+            return st_
+        st = run_phase(cx, setup)
+        err, last = None, None
+        cx.barrier()
+        try:
+            s.restore_table()
+            st.run()
+        except Exception as e:
+            err = e
+        cx.barrier()
+        t0 = time.perf_counter()
+        if err is None:
+            try:
+                s.restore_table()
+                last = st.run()
+            except Exception as e:
+                err = e
+        cx.barrier()
+        dt = time.perf_counter() - t0
+        agree(cx, err)
+        elapsed = cx.max(dt)
+        placement, _ = run_phase(cx, st.results)
+        st.free()
+    finally:
+        s.close()
+    return {"variant": "RCCL as-is: per pod one ncclAllReduce(count 1, ncclUint64, ncclMax) of the packed "
+                       "(score, node) key over the node shards (SURVEY.md section 8(e) C1, QS_ENGINE_ALLREDUCE)",
+            "workload": f"config3 cluster ({n_nodes:,} nodes), first {sample:,} pods of its stream",
+            "value": round(sample / elapsed, 1), "unit": "pods/s", "ms_per_step": round(elapsed * 1e3, 3),
+            "us_per_pod": round(elapsed / sample * 1e6, 3), "steps": 1, "engine": last["engine_used"],
+            "n_gpus": cx.world, "nodes": nodes, "pods": pods, "placement": placement}
+
+
+def check_rccl_sample(r):
+    """The per-pod all-reduce sample against the oracle's incremental exact stream."""
+    from oracle import oracle as O
+    on = {k: v.copy() for k, v in r.pop("nodes").items()}
+    ref, _, _ = O.schedule_incremental(on, qsched.pods_from_struct(r.pop("pods")), {}, nthreads=16)
+    return bool(np.array_equal(r.pop("placement"), ref))
+
+
 def check_stream(m):
     """Correctness of a timed leg: the oracle over the WHOLE stream, diffed
     against the GPU's placements, per-pod keys and final table, plus qsched.checks' size-independent
@@ -744,6 +805,14 @@ def main():
         m = measure_sharded(cx, a, workload)
     else:
         m = measure(cx, a, workload, a.steps, a.warmup)
+    rccl = None
+    if workload == "config3" or (cx.world == 1 and not a.no_config3):
+        if a.rccl_sample > 0:
+            progress(f"per-pod RCCL all-reduce leg ({a.rccl_sample} pods)")
+            try:
+                rccl = measure_rccl_per_pod(cx, a)
+            except Exception as e:  # reported, not fatal (every rank fails it at the same point)
+                rccl = {"error": repr(e)[:300]}
     c3 = c4 = c5 = scan = None
     if cx.world == 1 and workload == "config2" and not a.no_config3:
         progress("config3 leg")
@@ -795,6 +864,10 @@ def main():
         if m["sharded"] or (cx.world == 1 and not a.no_cpu):
             progress("oracle check of the timed stream")
             out["check"] = check_stream(m)
+        if rccl is not None:
+            if "placement" in rccl:
+                rccl["placements_match"] = check_rccl_sample(rccl)
+            out["rccl_per_pod"] = rccl
         if c3 is not None:
             progress("oracle checks of the config 3 / 4 / 5 legs")
             out["config3"] = {"workload": c3["desc"] + " (1 GPU: the N=1 point of the curve)",

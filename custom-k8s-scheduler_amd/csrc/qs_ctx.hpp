@@ -177,6 +177,9 @@ inline ShardPlan shard_plan(const qs_ctx *c) {
 void exchange_lists(qs_ctx *c, uint64_t *lists, size_t per_rank_entries, hipStream_t stream);
 // The same in-place all-gather for 32-bit words (normalizing profiles' partial maxima).
 void exchange_u32(qs_ctx *c, uint32_t *buf, size_t per_rank_words, hipStream_t stream);
+// In-place max all-reduces of the per-pod engine QS_ENGINE_ALLREDUCE.
+void allreduce_max_u64(qs_ctx *c, uint64_t *buf, size_t count, hipStream_t stream);
+void allreduce_max_u32(qs_ctx *c, uint32_t *buf, size_t count, hipStream_t stream);
 // {count, nodes[64]} dirty-set hand-off between overlapped lookahead windows (+ pad)
 constexpr size_t kDioWords = 68;
 // Mailbox layout (bytes from the base): flags [2 phases][16 ranks] u64 | lists [3 slots][16 ranks]

@@ -16,6 +16,7 @@
 namespace qs {
 
 constexpr int kWave = 64;
+#define QS_BAL_MAX 4  // entries of the BalancedAllocation resource list (QS_MAX_SCORE_RES)
 
 // ---- device node table: one 64-byte row per node (+ a 32-byte mask row) -----------------------
 // Row-major so that a lane gathering one node (the resolver's candidate / dirty rows) touches one
@@ -71,7 +72,10 @@ struct DevTable {
 };
 
 // kFeatWide selects the wide row / pod layout (DRowW, DPodW); the host sets it with kFeatExt.
-enum FeatBits : uint32_t { kFeatTaint = 1u, kFeatAffinity = 2u, kFeatExt = 4u, kFeatWide = 8u };
+// kFeatRes selects the configurable scoring-resource form of LeastAllocated / BalancedAllocation
+// (spec S5 "Scoring resources": extended resources in the lists, lists other than {cpu, memory});
+// the host sets it with kFeatExt.
+enum FeatBits : uint32_t { kFeatTaint = 1u, kFeatAffinity = 2u, kFeatExt = 4u, kFeatWide = 8u, kFeatRes = 16u };
 
 // pod flags: bits 0-1 QoS, 4-6 required terms, 8-10 preferred terms, 12-13 anti-affinity kind,
 // 16-25 app group (spec S11)
@@ -92,6 +96,11 @@ struct DevCfg {
     int32_t wtt, wna;            // TaintToleration / NodeAffinity plugin weights
     uint32_t feat;               // kFeat* bits
     uint32_t ba_skip_be;         // balanced_skip_besteffort
+    // kFeatRes only: LeastAllocated weights of the extended resources (0 = not in the list; wc / wm
+    // likewise for cpu / memory) and the BalancedAllocation list in order, 4 bits per entry
+    // (1 cpu, 2 memory, 3 ext0, 4 ext1; 0 ends the list)
+    int32_t we0, we1;
+    uint32_t bal;
     // Overlapped lookahead windows: the resolver of window w waits in-kernel for
     // ready >= (epoch << 32 | w + 1), published by k_ready_set after window w's select chain,
     // instead of a cross-stream event per window.  nullptr: no wait (the launch is ordered).
@@ -536,10 +545,45 @@ __device__ __forceinline__ double fraction_w(double a, double r, double y) {
 }
 
 // ---- spec S5/S6: QoS-weighted total of one feasible node ------------------------------------
+// floor(num / den) of a weighted mean of scores 0..100 (num = sum of score x weight < 2^24, den = the
+// weight sum < 2^18, num / den <= 100): the f32 estimate is within 100 * 2^-22 < 1 of num / den, so it
+// truncates to the floor or a neighbour; the exact remainder num - q den (|.| < 2^25) moves it by
+// one.  den == 0 (no resource counted) scores 0, as upstream's weightSum == 0.
+__device__ __forceinline__ uint32_t div_small(uint32_t num, uint32_t den) {
+    const float d = (float)(den | (uint32_t)(den == 0u));
+    int32_t q = (int32_t)((float)num * __builtin_amdgcn_rcpf(d));
+    const int32_t r = (int32_t)num - q * (int32_t)den;
+    q = r < 0 ? q - 1 : q;
+    q = r >= (int32_t)den ? q + 1 : q;
+    return den ? (uint32_t)q : 0u;
+}
+// Correctly rounded f64 square root (Go math.Sqrt, SQRTSD): LLVM's gfx950 expansion of llvm.sqrt.f64
+// (scaling, v_rsq_f64, two Newton steps, the fma residual correction), checked bit for bit against
+// the host's sqrt on 33 M inputs by tests/native/sqrt_sweep.hip (tests/test_gpu_sqrt.py).
+__device__ __forceinline__ double sqrt_rn(double v) { return __builtin_sqrt(v); }
+
+// Extended-resource terms of the configurable lists (UP resource_allocation.go#
+// calculateResourceAllocatableRequest): an extended resource counts only where the node has it and
+// the pod requests it (scalar resource with podRequest == 0 -> (0, 0)); it is Requested (not
+// NonZeroRequested) + the request in both plugins.  RN(1/alloc) from rcp_int (alloc < 2^24).
+struct ExtTerms {
+    bool h0, h1;
+    double y0, y1;
+};
+template <class P>
+__device__ __forceinline__ ExtTerms ext_terms(const RowX &x, const P &p) {
+    ExtTerms e;
+    e.h0 = (x.ae0 != 0) & (p.re0 != 0);
+    e.h1 = (x.ae1 != 0) & (p.re1 != 0);
+    e.y0 = rcp_int(x.ae0 | (int32_t)(x.ae0 == 0));
+    e.y1 = rcp_int(x.ae1 | (int32_t)(x.ae1 == 0));
+    return e;
+}
+
 // LeastAllocated (UP least_allocated.go#leastResourceScorer), NonZeroRequested + pod nz.
 // Branch-free: a resource with alloc == 0 contributes weight 0 (its score is 0 as well).
-template <class R, class P>
-__device__ __forceinline__ uint32_t la_score(const R &r, const P &p, const DevCfg &c) {
+template <uint32_t F, class R, class P>
+__device__ __forceinline__ uint32_t la_score(const R &r, const RowX &x, const P &p, const DevCfg &c) {
     const bool hc = r.ac != 0, hm = r.am != 0;
     const uint32_t sc_c = least_requested(r.ac, r.zc + p.zc, r.yc);
     uint32_t sc_m;
@@ -547,27 +591,72 @@ __device__ __forceinline__ uint32_t la_score(const R &r, const P &p, const DevCf
     else sc_m = least_requested(r.am, r.zm + p.zm, r.ym);
     const uint32_t wce = hc ? (uint32_t)c.wc : 0u, wme = hm ? (uint32_t)c.wm : 0u;
     const uint32_t num = __umul24(sc_c, wce) + __umul24(sc_m, wme);
-    const uint32_t den = wce + wme;
-    // select the weight-sum reciprocal with bit masks (a ternary on the kernel-argument doubles
-    // was lowered to a per-lane load from the kernarg segment, stalling on vmcnt(0))
-    const uint64_t mb = 0ull - (uint64_t)(hc & hm), mc = 0ull - (uint64_t)(hc & !hm),
-                   mm = 0ull - (uint64_t)(!hc & hm);
-    const double yd = __builtin_bit_cast(
-        double, (__builtin_bit_cast(uint64_t, c.yd_both) & mb) |
-                    (__builtin_bit_cast(uint64_t, c.yd_c) & mc) | (__builtin_bit_cast(uint64_t, c.yd_m) & mm));
-    (void)den;  // den == 0 means num == 0 and yd == 0.0: floor_div gives 0 without a branch
-    return floor_div(num, yd);
+    if constexpr ((F & kFeatRes) != 0) {
+        // the configured list (spec S5 "Scoring resources"): cpu / memory weights 0 when absent,
+        // the extended columns' terms where counted, then the weighted mean
+        const ExtTerms e = ext_terms(x, p);
+        const uint32_t s0 = least_requested(x.ae0, x.re0 + p.re0, e.y0);
+        const uint32_t s1 = least_requested(x.ae1, x.re1 + p.re1, e.y1);
+        const uint32_t w0 = e.h0 ? (uint32_t)c.we0 : 0u, w1 = e.h1 ? (uint32_t)c.we1 : 0u;
+        return div_small(num + __umul24(s0, w0) + __umul24(s1, w1), wce + wme + w0 + w1);
+    } else {
+        (void)x;
+        // select the weight-sum reciprocal with bit masks (a ternary on the kernel-argument doubles
+        // was lowered to a per-lane load from the kernarg segment, stalling on vmcnt(0))
+        const uint64_t mb = 0ull - (uint64_t)(hc & hm), mc = 0ull - (uint64_t)(hc & !hm),
+                       mm = 0ull - (uint64_t)(!hc & hm);
+        const double yd = __builtin_bit_cast(
+            double, (__builtin_bit_cast(uint64_t, c.yd_both) & mb) |
+                        (__builtin_bit_cast(uint64_t, c.yd_c) & mc) | (__builtin_bit_cast(uint64_t, c.yd_m) & mm));
+        // den == 0 means num == 0 and yd == 0.0: floor_div gives 0 without a branch
+        return floor_div(num, yd);
+    }
 }
 // BalancedAllocation (UP balanced_allocation.go#balancedResourceScorer), Requested + pod req
-template <class R, class P>
-__device__ __forceinline__ uint32_t ba_score(const R &r, const P &p, const DevCfg &c) {
+template <uint32_t F, class R, class P>
+__device__ __forceinline__ uint32_t ba_score(const R &r, const RowX &x, const P &p, const DevCfg &c) {
     const bool hc = r.ac != 0, hm = r.am != 0;
     const double f0 = fraction(r.ac, r.rc + p.rc, r.yc);
     double f1;
     if constexpr (std::is_same<R, RowW>::value) f1 = fraction_w(r.am, r.rm + p.rm, r.ym);
     else f1 = fraction(r.am, r.rm + p.rm, r.ym);
     double sd = 0.0;
-    if (hc & hm) sd = __builtin_fabs((f0 - f1) / 2);
+    if constexpr ((F & kFeatRes) != 0) {
+        // the configured list in its order (c.bal, 4 bits per entry; the ids are wave-uniform):
+        // included fractions summed in list order, a skipped entry adds an exact +0.0
+        const ExtTerms e = ext_terms(x, p);
+        const double fe0 = fraction(x.ae0, x.re0 + p.re0, e.y0), fe1 = fraction(x.ae1, x.re1 + p.re1, e.y1);
+        double fj[QS_BAL_MAX], fa = 0.0, fb = 0.0, tot = 0.0;
+        bool ij[QS_BAL_MAX];
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int j = 0; j < QS_BAL_MAX; ++j) {
+            const uint32_t id = (c.bal >> (4 * j)) & 7u;
+            fj[j] = id == 1u ? f0 : id == 2u ? f1 : id == 3u ? fe0 : fe1;
+            ij[j] = id == 1u ? hc : id == 2u ? hm : id == 3u ? e.h0 : id == 4u ? e.h1 : false;
+            fa = (ij[j] & (cnt == 0u)) ? fj[j] : fa;
+            fb = (ij[j] & (cnt == 1u)) ? fj[j] : fb;
+            tot = tot + (ij[j] ? fj[j] : 0.0);
+            cnt += ij[j] ? 1u : 0u;
+        }
+        if (cnt == 2u) {
+            sd = __builtin_fabs((fa - fb) / 2);
+        } else if (cnt > 2u) {
+            const double dn = (double)cnt;
+            const double mean = tot / dn;  // IEEE division (-ffp-contract=off, no fast-math)
+            double s = 0.0;
+#pragma unroll
+            for (int j = 0; j < QS_BAL_MAX; ++j) {
+                const double d = fj[j] - mean;
+                const double sq = d * d;
+                s = s + (ij[j] ? sq : 0.0);
+            }
+            sd = sqrt_rn(s / dn);
+        }
+    } else {
+        (void)x;
+        if (hc & hm) sd = __builtin_fabs((f0 - f1) / 2);
+    }
     const double scaled = (1 - sd) * 100.0;
     uint32_t ba = (uint32_t)(int32_t)scaled;  // int64() truncation toward zero
     if (c.ba_skip_be && (p.flags & 3u) == 0) ba = 0;
@@ -588,7 +677,7 @@ template <uint32_t F, class R, class P>
 __device__ __forceinline__ uint32_t node_total(const R &r, const RowX &x, const P &p,
                                                const DPodX &px, const DevCfg &c, uint32_t mt,
                                                double ymt, uint32_t ma, double yma, uint32_t *sc) {
-    const uint32_t la = la_score(r, p, c), ba = ba_score(r, p, c);
+    const uint32_t la = la_score<F>(r, x, p, c), ba = ba_score<F>(r, x, p, c);
     uint32_t total = __umul24((uint32_t)p.wfit, la) + __umul24((uint32_t)p.wbal, ba);
     uint32_t tt = 0, na = 0;
     if (F & kFeatTaint) {
@@ -606,9 +695,10 @@ __device__ __forceinline__ uint32_t node_total(const R &r, const RowX &x, const 
 // node_total of a normalizing profile with the node's static part given as static_raw (resident
 // stream's waves A/B/C): the same sums in the same order.
 template <uint32_t F, class R, class P>
-__device__ __forceinline__ uint32_t norm_total(const R &r, const P &p, const DevCfg &c, uint32_t st, uint32_t mt,
-                                               double ymt, uint32_t ma, double yma) {
-    uint32_t total = __umul24((uint32_t)p.wfit, la_score(r, p, c)) + __umul24((uint32_t)p.wbal, ba_score(r, p, c));
+__device__ __forceinline__ uint32_t norm_total(const R &r, const RowX &x, const P &p, const DevCfg &c, uint32_t st,
+                                               uint32_t mt, double ymt, uint32_t ma, double yma) {
+    uint32_t total = __umul24((uint32_t)p.wfit, la_score<F>(r, x, p, c)) +
+                     __umul24((uint32_t)p.wbal, ba_score<F>(r, x, p, c));
     if (F & kFeatTaint) total += __umul24((uint32_t)c.wtt, tt_norm((st >> 1) & 127u, mt, ymt));
     if (F & kFeatAffinity) total += __umul24((uint32_t)c.wna, na_norm(st >> 8, ma, yma));
     return total;

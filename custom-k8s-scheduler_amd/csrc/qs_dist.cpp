@@ -38,6 +38,14 @@ void exchange_u32(qs_ctx *c, uint32_t *buf, size_t per_rank_words, hipStream_t s
                           c->comm, stream));
 }
 
+// The as-is RCCL baseline: one latency-bound max all-reduce per pod, in place.
+void allreduce_max_u64(qs_ctx *c, uint64_t *buf, size_t count, hipStream_t stream) {
+    NCCLCHK(ncclAllReduce(buf, buf, count, ncclUint64, ncclMax, c->comm, stream));
+}
+void allreduce_max_u32(qs_ctx *c, uint32_t *buf, size_t count, hipStream_t stream) {
+    NCCLCHK(ncclAllReduce(buf, buf, count, ncclUint32, ncclMax, c->comm, stream));
+}
+
 // ---- peer-memory mailbox: one hop per exchange instead of a ring ----------
 // Block p writes this rank's block into rank p's mailbox over xGMI (p == rank: only the zero
 // padding of its own lists), then publishes flag[phase][rank] = seq there with a system-scope

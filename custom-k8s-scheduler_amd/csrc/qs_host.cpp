@@ -16,6 +16,7 @@
 #include <atomic>
 #include <chrono>
 #include <cmath>
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -53,20 +54,86 @@ void check_cfg(const qs_config &c) {
     }
     if (c.w_taint < 0 || c.w_affinity < 0 || c.w_taint > 65535 || c.w_affinity > 65535)
         fail(QS_EINVAL, "plugin weights must be in [0, 65535]");
+    // scoring-resource lists (UP apis/config/validation/validation_pluginargs.go#validateResources:
+    // known resource, no duplicates, weight 1..100)
+    if (c.n_fit_resources < 0 || c.n_fit_resources > QS_MAX_SCORE_RES)
+        fail(QS_EINVAL, "n_fit_resources must be in [0, 4]");
+    if (c.n_balanced_resources < 0 || c.n_balanced_resources > QS_MAX_SCORE_RES)
+        fail(QS_EINVAL, "n_balanced_resources must be in [0, 4]");
+    uint32_t seen = 0;
+    for (int i = 0; i < c.n_fit_resources; i++) {
+        const int32_t r = c.fit_resources[i].resource;
+        if (r < QS_RES_CPU || r > QS_RES_EXT1) fail(QS_EINVAL, "fit_resources: unknown resource");
+        if (seen & (1u << r)) fail(QS_EINVAL, "fit_resources: duplicate resource");
+        seen |= 1u << r;
+        if (c.fit_resources[i].weight < 1 || c.fit_resources[i].weight > 100)
+            fail(QS_EINVAL, "fit_resources: weight must be in [1, 100]");
+    }
+    seen = 0;
+    for (int i = 0; i < c.n_balanced_resources; i++) {
+        const int32_t r = c.balanced_resources[i];
+        if (r < QS_RES_CPU || r > QS_RES_EXT1) fail(QS_EINVAL, "balanced_resources: unknown resource");
+        if (seen & (1u << r)) fail(QS_EINVAL, "balanced_resources: duplicate resource");
+        seen |= 1u << r;
+    }
     // total + 1 must fit the 32-bit score half of the packed key (spec S6/S7)
     const int64_t tmax = 100 * (wmax + (c.enable_taint ? c.w_taint : 0) +
                                 (c.enable_affinity ? c.w_affinity : 0));
     if (tmax >= 0x7FFFFFFF) fail(QS_EINVAL, "weighted total would overflow the packed key");
 }
 
+// LeastAllocated weight per scoring resource (index qs_resource; 0 = not in the list): the list,
+// or the default [cpu: fit_weight_cpu, memory: fit_weight_mem]
+void fit_weights(const qs_config &c, int64_t w[5]) {
+    for (int r = 0; r < 5; r++) w[r] = 0;
+    if (c.n_fit_resources == 0) {
+        w[QS_RES_CPU] = c.fit_weight_cpu;
+        w[QS_RES_MEMORY] = c.fit_weight_mem;
+        return;
+    }
+    for (int i = 0; i < c.n_fit_resources; i++) w[c.fit_resources[i].resource] = c.fit_resources[i].weight;
+}
+
+// The BalancedAllocation list as 4-bit ids in list order (DevCfg::bal); default [cpu, memory].
+uint32_t balanced_ids(const qs_config &c) {
+    if (c.n_balanced_resources == 0) return QS_RES_CPU | (QS_RES_MEMORY << 4);
+    uint32_t b = 0;
+    for (int i = 0; i < c.n_balanced_resources; i++) b |= (uint32_t)c.balanced_resources[i] << (4 * i);
+    return b;
+}
+
+// Does a stream (or pod) need the resource-list form of the scorers (kFeatRes, spec S5 "Scoring
+// resources")?  Not when the lists reduce to the two-resource form the default kernels compute:
+// LeastAllocated over cpu / memory with any weights, BalancedAllocation over exactly {cpu, memory}
+// (its two-fraction std is symmetric in the order).  Extended resources drop out of both lists when
+// no pod of the stream requests them (a scalar resource with podRequest == 0 is skipped).
+uint32_t res_feat(const qs_config &c, bool has_ext) {
+    int64_t w[5];
+    fit_weights(c, w);
+    bool generic = has_ext && (w[QS_RES_EXT0] != 0 || w[QS_RES_EXT1] != 0);
+    uint32_t set = 0;
+    const uint32_t b = balanced_ids(c);
+    for (int i = 0; i < QS_MAX_SCORE_RES; i++) {
+        const uint32_t id = (b >> (4 * i)) & 15u;
+        if (id == QS_RES_CPU || id == QS_RES_MEMORY || (has_ext && id >= QS_RES_EXT0)) set |= 1u << id;
+    }
+    generic |= set != ((1u << QS_RES_CPU) | (1u << QS_RES_MEMORY));
+    return generic ? (kFeatRes | kFeatExt) : 0u;
+}
+
 DevCfg make_devcfg(const qs_config &c) {
     DevCfg d{};
-    d.wc = (int32_t)c.fit_weight_cpu;
-    d.wm = (int32_t)c.fit_weight_mem;
+    int64_t w[5];
+    fit_weights(c, w);
+    d.wc = (int32_t)w[QS_RES_CPU];
+    d.wm = (int32_t)w[QS_RES_MEMORY];
+    d.we0 = (int32_t)w[QS_RES_EXT0];
+    d.we1 = (int32_t)w[QS_RES_EXT1];
+    d.bal = balanced_ids(c);
     auto rcp = [](int64_t v) { return v > 0 ? 1.0 / (double)v : 0.0; };  // RN_f64(1/v)
-    d.yd_both = rcp(c.fit_weight_cpu + c.fit_weight_mem);
-    d.yd_c = rcp(c.fit_weight_cpu);
-    d.yd_m = rcp(c.fit_weight_mem);
+    d.yd_both = rcp(w[QS_RES_CPU] + w[QS_RES_MEMORY]);
+    d.yd_c = rcp(w[QS_RES_CPU]);
+    d.yd_m = rcp(w[QS_RES_MEMORY]);
     // a disabled plugin weighs 0 (the kernels of the normalizing class evaluate both plugins; the
     // pod records of a disabled plugin are neutral, see compact_pod / compact_podx)
     d.wtt = c.enable_taint ? c.w_taint : 0;
@@ -949,8 +1016,12 @@ qs_status qs_unreserve(qs_ctx *c, uint32_t node, const qs_pod *p) { return reser
 // four byte scores per node, 0xFFFFFFFF = infeasible) into the caller's arrays, 16 nodes per step as
 // vectors: feasible = not the sentinel, the four int32 plugin scores (0 where infeasible) and the
 // QoS-weighted total (w = {wfit, wbal, wtt, wna}: the sums node_total forms, -1 where infeasible).
-static void unpack_scores(const uint32_t *pk, uint32_t n, const uint32_t w[4], uint8_t *feas, int32_t *score,
-                          int32_t *total) {
+// Widening of the packed per-node words into qs_score_pod's arrays (only the planes asked for), 16
+// nodes per iteration with clang vector types.  The body is compiled three times — for AVX-512BW,
+// AVX2 and the baseline — and the widest one the host CPU supports is picked once (round 5: the
+// copy-out form was 5-7 us of the 5,000-node call and ~40 us of the 50,000-node one, SSE2 only).
+__attribute__((always_inline)) static inline void unpack_body(const uint32_t *pk, uint32_t n, const uint32_t w[4],
+                                                              uint8_t *feas, int32_t *score, int32_t *total) {
     typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
     typedef int32_t i32x16 __attribute__((ext_vector_type(16)));
     typedef uint8_t u8x16 __attribute__((ext_vector_type(16)));
@@ -990,6 +1061,33 @@ static void unpack_scores(const uint32_t *pk, uint32_t n, const uint32_t w[4], u
                          : -1;
     }
 }
+__attribute__((target("avx512f,avx512bw,avx512vl"))) static void unpack_avx512(const uint32_t *pk, uint32_t n,
+                                                                               const uint32_t w[4], uint8_t *feas,
+                                                                               int32_t *score, int32_t *total) {
+    unpack_body(pk, n, w, feas, score, total);
+}
+__attribute__((target("avx2"))) static void unpack_avx2(const uint32_t *pk, uint32_t n, const uint32_t w[4],
+                                                        uint8_t *feas, int32_t *score, int32_t *total) {
+    unpack_body(pk, n, w, feas, score, total);
+}
+static void unpack_base(const uint32_t *pk, uint32_t n, const uint32_t w[4], uint8_t *feas, int32_t *score,
+                        int32_t *total) {
+    unpack_body(pk, n, w, feas, score, total);
+}
+static void unpack_scores(const uint32_t *pk, uint32_t n, const uint32_t w[4], uint8_t *feas, int32_t *score,
+                          int32_t *total) {
+    using Fn = void (*)(const uint32_t *, uint32_t, const uint32_t *, uint8_t *, int32_t *, int32_t *);
+    static const Fn fn = [] {
+#if !defined(__HIP_DEVICE_COMPILE__)  // (this TU is also parsed for the device; the probe is host-only)
+        __builtin_cpu_init();
+        if (getenv("QS_UNPACK_BASE")) return (Fn)unpack_base;
+        if (__builtin_cpu_supports("avx512bw") && __builtin_cpu_supports("avx512vl")) return (Fn)unpack_avx512;
+        if (__builtin_cpu_supports("avx2")) return (Fn)unpack_avx2;
+#endif
+        return (Fn)unpack_base;
+    }();
+    fn(pk, n, w, feas, score, total);
+}
 
 // The one-launch score of one pod into the context's pinned buffer: pod by value,
 // the previous Reserve's row folded in, outputs written by the kernel into pinned host memory,
@@ -1014,8 +1112,9 @@ static const uint32_t *score_pod_launch(qs_ctx *c, const qs_pod *pod, uint32_t w
         wts[0] = q->wfit; wts[1] = q->wbal;
     }
     DevCfg dc = c->dc;
-    dc.feat = feat_of(c->cfg) | ((pod->req_ext[0] || pod->req_ext[1]) ? kFeatExt : 0u) |
-              (c->wide ? kFeatWide | kFeatExt : 0u);
+    const bool pod_ext = pod->req_ext[0] || pod->req_ext[1];
+    dc.feat = feat_of(c->cfg) | (pod_ext ? kFeatExt : 0u) | (c->wide ? kFeatWide | kFeatExt : 0u) |
+              res_feat(c->cfg, pod_ext);
     wts[2] = (dc.feat & kFeatTaint) ? (uint32_t)dc.wtt : 0u;
     wts[3] = (dc.feat & kFeatAffinity) ? (uint32_t)dc.wna : 0u;
     if (n == 0 || !c->dev_valid) {
@@ -1092,8 +1191,10 @@ qs_status qs_stream_prepare(qs_ctx *c, const qs_pod *pods, uint32_t p, qs_stream
         s->shift = c->shift;
         s->wide = c->wide;
         s->feat = feat_of(c->cfg) | (c->wide ? kFeatWide | kFeatExt : 0u);
-        for (uint32_t j = 0; j < p; j++)
-            if (pods[j].req_ext[0] || pods[j].req_ext[1]) { s->feat |= kFeatExt; break; }
+        bool has_ext = false;
+        for (uint32_t j = 0; j < p && !has_ext; j++) has_ext = pods[j].req_ext[0] || pods[j].req_ext[1];
+        if (has_ext) s->feat |= kFeatExt;
+        s->feat |= res_feat(c->cfg, has_ext);
         s->order = qos_order(pods, p, c->cfg.qos_sort != 0);
         const size_t rb = pod_record_bytes(c->wide);
         std::vector<uint8_t> dp(rb * std::max<uint32_t>(p, 1));
@@ -1165,6 +1266,36 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                     kt.end(1, c->stream);
                     HIPCHK(launch_scan_pod(c->dt, dp, dx, k, c->dc, c->scratch.p, on, ok, st,
                                            nullptr, nullptr, nullptr, 2, c->stream));
+                }
+                batches = P;
+            } else if (eng == QS_ENGINE_ALLREDUCE) {
+                // SURVEY.md §8(e) C1 as-is: per pod every rank scans its contiguous node shard over the
+                // rows, one ncclAllReduce(u64 max) of the packed key (C2: the two normalize maxima
+                // first), and every rank applies the same Reserve to its replicated table
+                if (!c->comm)
+                    fail(QS_ESTATE, "the all-reduce engine needs an RCCL communicator (qs_open_shard with an id)");
+                DevTable dt = c->dt;
+                std::memset(&dt.soa, 0, sizeof dt.soa);  // rows only (the SoA copy is marked stale below)
+                const uint32_t sh[2] = {(uint32_t)((uint64_t)n * c->rank / c->world),
+                                        (uint32_t)((uint64_t)n * (c->rank + 1) / c->world)};
+                HIPCHK(hipMemsetAsync(c->scratch.p, 0, scan_scratch_bytes(), c->stream));
+                HIPCHK(hipMemcpyAsync(static_cast<char *>(c->scratch.p) + offsetof(ScanHead, lo), sh, 8,
+                                      hipMemcpyHostToDevice, c->stream));
+                ScanHead *sc = c->scratch.as<ScanHead>();
+                const bool norm = (c->dc.feat & (kFeatTaint | kFeatAffinity)) != 0;
+                for (uint32_t k = 0; k < P; k++) {
+                    kt.begin(1, c->stream);
+                    if (norm) {
+                        HIPCHK(launch_scan_pod(dt, dp, dx, k, c->dc, c->scratch.p, on, ok, st, nullptr, nullptr,
+                                               nullptr, 8, c->stream));
+                        allreduce_max_u32(c, &sc->mt, 2, c->stream);
+                    }
+                    HIPCHK(launch_scan_pod(dt, dp, dx, k, c->dc, c->scratch.p, on, ok, st, nullptr, nullptr,
+                                           nullptr, 16 | 32, c->stream));
+                    allreduce_max_u64(c, reinterpret_cast<uint64_t *>(&sc->best), 1, c->stream);
+                    HIPCHK(launch_scan_pod(dt, dp, dx, k, c->dc, c->scratch.p, on, ok, st, nullptr, nullptr,
+                                           nullptr, 64, c->stream));
+                    kt.end(1, c->stream);
                 }
                 batches = P;
             } else {
@@ -1427,6 +1558,9 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                     const char *inj = getenv("QS_INJECT_FAULT");
                     dcr.inject = (inject_once(c, "resident_stall", kInjResidentStall) ||
                                   (inj && std::strcmp(inj, "resident_stall_always") == 0)) ? 1u : 0u;
+                    // (QS_INJECT_FAULT=resident_skew: this rank's selectors of windows 40-43 start 3 ms
+                    // late, so the ranks of a sharded run drift apart in the middle of the stream)
+                    if (inj && std::strcmp(inj, "resident_skew") == 0) dcr.inject = 2u;
                     // sharded: window 0's waits cover a peer still in host-side prepare (5 s)
                     dcr.first_ticks = c->world > 1 ? 500000000ull : 0ull;
                     // QS_RES_DIAG=1: the resolver's time split (list waits / window bodies / between)
@@ -1551,6 +1685,9 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                                                      "the context falls back to stream events");
             }
         }
+        // a resident run that finished without a timeout: only CONSECUTIVE resident timeouts keep
+        // the context on per-window launches (qs_ctx.hpp)
+        if (eng == QS_ENGINE_LOOKAHEAD && c->last_resident) c->res_timeouts = 0;
         if (eng == QS_ENGINE_LOOKAHEAD && c->nfall.p) {
             uint64_t h[2] = {0, 0};
             HIPCHK(hipMemcpy(h, c->nfall.p, 16, hipMemcpyDeviceToHost));

@@ -63,6 +63,9 @@ static uint32_t feat_class(uint32_t feat) {
 hipError_t launch_persistent(const DevTable &t, const void *pods, const DPodX *podx, uint32_t P,
                              const DevCfg &c, int32_t *on, uint64_t *ok, uint64_t *st,
                              hipStream_t stream) {
+    if (c.feat & kFeatRes)
+        return t.wrows ? res_wide_persistent(t, pods, podx, P, c, on, ok, st, stream)
+                       : res_compact_persistent(t, pods, podx, P, c, on, ok, st, stream);
     if (t.wrows) return wide_persistent(t, pods, podx, P, c, on, ok, st, stream);
     switch (feat_class(c.feat)) {
         case 0: return persistent_f<0>(t, pods, podx, P, c, on, ok, st, stream);
@@ -74,6 +77,8 @@ hipError_t launch_persistent(const DevTable &t, const void *pods, const DPodX *p
 }
 
 uint32_t persistent_max_nodes(uint32_t feat) {
+    if (feat & kFeatRes)
+        return (feat & kFeatWide) ? res_wide_persistent_max_nodes(feat) : res_compact_persistent_max_nodes(feat);
     if (feat & kFeatWide) return wide_persistent_max_nodes(feat);
     switch (feat_class(feat)) {
         case 0: return persistent_cap<0>();
@@ -92,6 +97,9 @@ hipError_t launch_scan_pod(const DevTable &t, const void *pods, const DPodX *pod
                            const DevCfg &c, void *scratch, int32_t *on, uint64_t *ok, uint64_t *st,
                            uint8_t *feas, int32_t *score, int32_t *total, int part,
                            hipStream_t stream) {
+    if (c.feat & kFeatRes)
+        return t.wrows ? res_wide_scan_pod(t, pods, podx, s, c, scratch, on, ok, st, feas, score, total, part, stream)
+                       : res_compact_scan_pod(t, pods, podx, s, c, scratch, on, ok, st, feas, score, total, part, stream);
     if (t.wrows) return wide_scan_pod(t, pods, podx, s, c, scratch, on, ok, st, feas, score, total, part, stream);
     switch (feat_class(c.feat)) {
         case 0: return scan_pod_f<0>(t, pods, podx, s, c, scratch, on, ok, st, feas, score, total, part, stream);
@@ -107,6 +115,9 @@ uint32_t score_pod1_max_nodes() { return kScorePod1Max; }
 size_t score_pod1_pack_bytes(uint32_t n) { return score_pack_bytes(n); }
 hipError_t launch_score_pod1(const DevTable &t, const void *pod, const DPodX *podx, const DevCfg &c, uint8_t *hout,
                              uint64_t *gs, uint64_t seq, uint32_t pidx, const HostRow &prow, hipStream_t stream) {
+    if (c.feat & kFeatRes)
+        return t.wrows ? res_wide_score_pod1(t, pod, podx, c, hout, gs, seq, pidx, prow, stream)
+                       : res_compact_score_pod1(t, pod, podx, c, hout, gs, seq, pidx, prow, stream);
     if (t.wrows) return wide_score_pod1(t, pod, podx, c, hout, gs, seq, pidx, prow, stream);
     switch (feat_class(c.feat)) {
         case 0: return score_pod1_f<0>(t, pod, podx, c, hout, gs, seq, pidx, prow, stream);
@@ -133,6 +144,9 @@ hipError_t launch_la_window(const DevTable &t, const void *pods, const DPodX *po
                             hipStream_t stream, int part) {
     if (bf.dprev && geo.waves == 1 && !(c.feat & kFeatNorm)) return hipErrorInvalidValue;
     if ((c.feat & kFeatNorm) && diag && geo.waves != 4) return hipErrorInvalidValue;
+    if (c.feat & kFeatRes)
+        return t.wrows ? res_wide_la_window(t, pods, podx, s0, P, c, geo, bf, on, ok, st, diag, stream, part)
+                       : res_compact_la_window(t, pods, podx, s0, P, c, geo, bf, on, ok, st, diag, stream, part);
     if (t.wrows) return wide_la_window(t, pods, podx, s0, P, c, geo, bf, on, ok, st, diag, stream, part);
     if (c.feat & kFeatNorm)
         return la_window_f<kFeatExt | kFeatTaint | kFeatAffinity>(t, pods, podx, s0, P, c, geo, bf, on, ok, st, diag, stream, part);
@@ -151,7 +165,7 @@ LaGeom la_stream_res_plan(const LaGeom &geo, uint32_t feat, uint32_t n, uint32_t
     r.G = 0;
     // Fit + Balanced (+ extended) profiles, and the normalizing ones (K <= kResNormK), both layouts;
     // sharded (geo.W > 1 ranks, one shard each): W * L <= 512
-    const uint32_t fl = feat & ~kFeatWide;  // both row layouts
+    const uint32_t fl = feat & ~(kFeatWide | kFeatRes);  // both row layouts, either scoring form
     const bool fit = fl == 0 || fl == kFeatExt;
     const bool norm = (feat & kFeatNorm) != 0 && geo.K <= kResNormK;
     const bool shard_ok = geo.W == 1 ? geo.nv == 1 && geo.epl == 1
@@ -184,7 +198,9 @@ size_t la_stream_res_ctl_bytes() { return kResCtlBytes; }
 // CU can exceed what the hardware admits by one workgroup (MI355X_MICROARCH.md, residency), so one
 // is taken off whenever the API allows two or more.
 uint32_t la_stream_res_max_blocks(const LaGeom &geo, uint32_t feat, uint32_t n, uint32_t cus) {
-    const int per = (feat & kFeatWide)  ? wide_la_stream_res_per_cu(geo, feat, n)
+    const int per = (feat & kFeatRes)   ? ((feat & kFeatWide) ? res_wide_la_stream_res_per_cu(geo, feat, n)
+                                                              : res_compact_la_stream_res_per_cu(geo, feat, n))
+                    : (feat & kFeatWide)  ? wide_la_stream_res_per_cu(geo, feat, n)
                     : (feat & kFeatNorm)  ? la_stream_res_per_cu<kFeatExt | kFeatTaint | kFeatAffinity>(geo, n)
                     : (feat & kFeatExt) ? la_stream_res_per_cu<kFeatExt>(geo, n)
                                         : la_stream_res_per_cu<0>(geo, n);
@@ -204,6 +220,10 @@ hipError_t launch_la_stream_res(const DevTable &t, const void *pods, const DPodX
                                 const ResShard &rsh, hipStream_t stream) {
     if (geo.G == 0 || (uint64_t)t.n * (t.wrows ? sizeof(DRowW) : sizeof(DRow)) >= (1ull << 31))
         return hipErrorInvalidValue;
+    if (c.feat & kFeatRes)
+        return (t.wrows ? res_wide_la_stream_res : res_compact_la_stream_res)(
+            t, pods, podx, c, P, geo, lists0, clists0, lwords, cwords, npart, norm, stat, nfall, on, ok, st, ctl,
+            sel_blocks, rdiag, rsh, stream);
     if (t.wrows)
         return wide_la_stream_res(t, pods, podx, c, P, geo, lists0, clists0, lwords, cwords, npart, norm, stat, nfall, on,
                                   ok, st, ctl, sel_blocks, rdiag, rsh, stream);

@@ -22,6 +22,16 @@
 #include "qs_device.hpp"
 #include "qs_launch.hpp"
 
+// Timing-ablation hooks (tools/exp_run.sh): empty in the product build.  Only
+// `make exp` defines them, by force-including csrc/exp/qs_exp.hpp, whose variants give wrong
+// placements by construction (timing experiments, never the product library).
+#ifndef QS_EXP_HOOKS
+#define QS_EXP_NORM_AB(norm) (norm)
+#define QS_EXP_SLOT_KEY(act, r, q)
+#define QS_EXP_CAND_KEY(f, tot, cr, p)
+#define QS_EXP_PARK_RETURN()
+#endif
+
 namespace qs {
 
 constexpr uint32_t kFeatNorm = kFeatTaint | kFeatAffinity;
@@ -125,9 +135,12 @@ constexpr uint32_t kScanBlocksMax = 2048;
 struct ScanScratch {
     unsigned long long best;  // reduced key of the last commit (qs_score_pod reads it)
     uint32_t mt, ma;          // normalize maxima (k_scan_norm)
-    uint32_t nblk, pad;       // partials written by the last key scan
+    uint32_t lo, hi;          // node range the row scans cover (hi == 0: the whole table); a rank's
+                              // shard for the per-pod all-reduce engine (QS_ENGINE_ALLREDUCE)
     uint64_t partial[kScanBlocksMax];
 };
+static_assert(offsetof(ScanScratch, lo) == offsetof(ScanHead, lo) && offsetof(ScanScratch, mt) == offsetof(ScanHead, mt),
+              "ScanHead mirrors ScanScratch");
 
 // Block-wide max of a u64 key: wave DPP max, then one LDS exchange.
 template <int BS>
@@ -149,7 +162,8 @@ __global__ __launch_bounds__(256) void k_scan_norm(DevTable t, const PodT<F> *__
     const PodT<F> p = pods[s];
     const DPodX px = podx[s];
     uint32_t lt = 0, la = 0;
-    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < t.n; i += gridDim.x * 256) {
+    const uint32_t lo = sc->lo, hi = sc->hi ? sc->hi : t.n;
+    for (uint32_t i = lo + blockIdx.x * 256 + threadIdx.x; i < hi; i += gridDim.x * 256) {
         const RowT<F> r = load_row<F>(t, i);
         const RowX x = load_rowx<F>(t, i);
         if (feasible<F>(r, x, p, px)) {
@@ -179,7 +193,8 @@ __global__ __launch_bounds__(256) void k_scan_key(DevTable t, const PodT<F> *__r
     if (F & kFeatNorm) { px = podx[s]; mt = sc->mt; ma = sc->ma; }
     const double ymt = rcp_exact(mt), yma = rcp_exact(ma);
     uint64_t best = 0;
-    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < t.n; i += gridDim.x * 256) {
+    const uint32_t lo = sc->lo, hi = sc->hi ? sc->hi : t.n;
+    for (uint32_t i = lo + blockIdx.x * 256 + threadIdx.x; i < hi; i += gridDim.x * 256) {
         const RowT<F> r = load_row<F>(t, i);
         const RowX x = load_rowx<F>(t, i);
         const bool f = feasible<F>(r, x, p, px);
@@ -260,9 +275,9 @@ __global__ __launch_bounds__(256) void k_scan_soa(DevTable t, const PodT<F> *__r
     if (threadIdx.x == 0) sc->partial[blockIdx.x] = best;
 }
 
-// One 256-thread block: reduce the key scan's partials to the pod's winner, then (stream mode,
-// out_node != nullptr) apply Reserve to the row (and SoA) copy and emit the outputs.  Resets the
-// normalize maxima for the next pod.
+// One 256-thread block: reduce the key scan's partials to the pod's winner (nblk == 0: take sc->best,
+// e.g. after the ranks' all-reduce of it), then (stream mode, out_node != nullptr) apply Reserve to
+// the row (and SoA) copy and emit the outputs.  Resets the normalize maxima for the next pod.
 template <uint32_t F>
 __global__ __launch_bounds__(256) void k_scan_commit(DevTable t, const PodT<F> *__restrict__ pods,
                                                      uint32_t s, uint32_t nblk, ScanScratch *sc,
@@ -270,7 +285,7 @@ __global__ __launch_bounds__(256) void k_scan_commit(DevTable t, const PodT<F> *
                                                      uint64_t *stamps) {
     uint64_t v = 0;
     for (uint32_t i = threadIdx.x; i < nblk; i += 256) v = sc->partial[i] > v ? sc->partial[i] : v;
-    const uint64_t ks = block_max_u64<256>(v);
+    const uint64_t ks = nblk ? block_max_u64<256>(v) : sc->best;
     if (threadIdx.x != 0) return;
     sc->best = ks;
     sc->mt = 0;
@@ -1962,6 +1977,12 @@ __device__ __forceinline__ bool res_cross_merge(uint64_t *lbuf, uint32_t L, uint
     if (tid == 0) {
         bool ok = true;
         for (uint32_t r = 0; r < W && ok; ++r) ok = sys_poll(reinterpret_cast<const uint64_t *>(own + rsh.flags) + cell + r, tag);
+        // a flag beyond this window's tag means a peer already reused the slot (the reuse argument
+        // above broken): fail the run loudly instead of merging a newer window's keys
+        for (uint32_t r = 0; r < W && ok; ++r)
+            ok = __hip_atomic_load(reinterpret_cast<const uint64_t *>(own + rsh.flags) + cell + r, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM) == tag;
+        if (!ok) __hip_atomic_store((gu32 *)werr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         okflag = ok ? 1u : 0u;
     }
     __syncthreads();  // every wave is past its lbuf reads; the flags have been seen
@@ -1986,7 +2007,11 @@ __device__ __forceinline__ bool res_cross_merge(uint64_t *lbuf, uint32_t L, uint
 // its own mailbox and combines the W partials into the pod's global NormInfo (max, and the counts of
 // the ranks attaining it: the order does not matter).  Slot reuse as for the lists (res_cross_merge):
 // a rank writes window w after resolving w - 2, which needed every rank's lists of w - 2, produced
-// after every chunk task of those ranks had left window w - 4.  Thread 0 only; false on a timeout.
+// after every chunk task of those ranks had left window w - 4.  Both 64-bit payload words carry the
+// window (w + 1 in their high half, mt << 24 | ct and ma << 22 | ca in the low), and a reader accepts a
+// partial only when its flag equals this window's tag and both words carry this window; anything
+// newer means the slot was reused early, and the run fails (werr) instead of combining it (ADVICE
+// r4).  Thread 0 only; false on a timeout or a mismatch.
 __device__ __forceinline__ bool res_norm_exchange(const NormInfo &part, uint32_t k, uint32_t w, uint32_t g,
                                                   const ResShard &rsh, bool &hello_ok, NormInfo &out,
                                                   uint32_t *werr, uint64_t first_ticks) {
@@ -2013,7 +2038,9 @@ __device__ __forceinline__ bool res_norm_exchange(const NormInfo &part, uint32_t
         hello_ok = true;
     }
     if (g == 0) {
-        const uint64_t lo = (uint64_t)part.mt | ((uint64_t)part.ct << 32), hi = (uint64_t)part.ma | ((uint64_t)part.ca << 32);
+        // mt <= 64 (a popcount), ma <= 400 (four preferred weights <= 100), counts < 2^22 nodes
+        const uint64_t wt = (uint64_t)(w + 1) << 32;
+        const uint64_t lo = wt | (uint64_t)part.mt << 24 | part.ct, hi = wt | (uint64_t)part.ma << 22 | part.ca;
         for (uint32_t r = 0; r < W; ++r) {
             uint64_t *dst = reinterpret_cast<uint64_t *>(rsh.peers[r] + rsh.norm) + 2 * (cell + rsh.rank);
             __hip_atomic_store(dst, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -2030,7 +2057,14 @@ __device__ __forceinline__ bool res_norm_exchange(const NormInfo &part, uint32_t
         const uint64_t *src = reinterpret_cast<const uint64_t *>(own + rsh.norm) + 2 * (cell + r);
         const uint64_t lo = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         const uint64_t hi = __hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        const uint32_t qx = (uint32_t)lo, qy = (uint32_t)(lo >> 32), qz = (uint32_t)hi, qw = (uint32_t)(hi >> 32);
+        const uint64_t f = __hip_atomic_load(reinterpret_cast<const uint64_t *>(own + rsh.nflags) + cell + r,
+                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (f != tag || (uint32_t)(lo >> 32) != w + 1 || (uint32_t)(hi >> 32) != w + 1) {
+            __hip_atomic_store((gu32 *)werr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return false;
+        }
+        const uint32_t qx = (uint32_t)(lo >> 24) & 0xFFu, qy = (uint32_t)lo & 0xFFFFFFu;
+        const uint32_t qz = (uint32_t)(hi >> 22) & 0x3FFu, qw = (uint32_t)hi & 0x3FFFFFu;
         if (qx > nf.mt) { nf.mt = qx; nf.ct = 0; }
         if (qx == nf.mt) nf.ct += qy;
         if (qz > nf.ma) { nf.ma = qz; nf.ca = 0; }
@@ -2081,6 +2115,13 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
         uint64_t *clists = clists0 + (size_t)b * cwords;
         for (uint32_t task = sid; task < kw * G; task += S) {
             if (c.inject == 1u && w == 3 && task == 0) continue;  // test hook: window 3 never completes
+            if (c.inject == 2u && w >= 40 && w < 44) {  // test hook: this rank's selectors run 3 ms late
+                if (tid == 0) {
+                    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+                    while (__builtin_amdgcn_s_memrealtime() - t0 < 300000ull) __builtin_amdgcn_s_sleep(10);
+                }
+                __syncthreads();
+            }
             const uint32_t k = task / G, g = task % G;
             if (rdiag) ts0 = __builtin_amdgcn_s_memrealtime();
             const PodT<F> p = pods[s0 + k];
@@ -2122,8 +2163,8 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
                                     raw[j] = rt | (ra << 16);
                                     mt = rt > mt ? rt : mt;
                                     ma = ra > ma ? ra : ma;
-                                    tv[j] = __umul24((uint32_t)p.wfit, la_score(r, p, cv)) +
-                                            __umul24((uint32_t)p.wbal, ba_score(r, p, cv));
+                                    tv[j] = __umul24((uint32_t)p.wfit, la_score<F>(r, x, p, cv)) +
+                                            __umul24((uint32_t)p.wbal, ba_score<F>(r, x, p, cv));
                                 }
                             }
                         }
@@ -2145,8 +2186,8 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
                             raw[j] = rt | (ra << 16);
                             mt = rt > mt ? rt : mt;
                             ma = ra > ma ? ra : ma;
-                            tv[j] = __umul24((uint32_t)p.wfit, la_score(r, p, cv)) +
-                                    __umul24((uint32_t)p.wbal, ba_score(r, p, cv));
+                            tv[j] = __umul24((uint32_t)p.wfit, la_score<F>(r, x, p, cv)) +
+                                    __umul24((uint32_t)p.wbal, ba_score<F>(r, x, p, cv));
                         }
                     }
                 }
@@ -2719,20 +2760,14 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
         // NORM: st = the slot's static_raw against pod q (Tcur, or stS for a slot created this step)
         auto slot_key = [&](const RowT<F> &r, const RowX &x, const PodT<F> &q, const PodN &pn, uint32_t st) -> uint64_t {
             const bool act = (uint32_t)lane < nd;
-#ifdef QS_EXP_PLAIN_AB
-            if (false) {
-#else
-            if constexpr (NORM) {
-#endif
+            if constexpr (QS_EXP_NORM_AB(NORM)) {
                 const bool f = fits<F>(r, x, q) && (st & 1u) != 0u;
-                const uint32_t tot = norm_total<F>(r, q, cv, st, pn.nf.mt, pn.yr.x, pn.nf.ma, pn.yr.y);
+                const uint32_t tot = norm_total<F>(r, x, q, cv, st, pn.nf.mt, pn.yr.x, pn.nf.ma, pn.yr.y);
                 uint32_t fl = 0;
                 if (act && !f) fl = holder_flags<F>(st, pn.nf.mt, pn.nf.ma);
                 return ((act && f) ? ((uint64_t)(tot + 1) << 32) : 0ull) | fl;
             }
-#ifdef QS_EXP_CHEAP_AB  // timing experiment only (wrong placements): no key arithmetic in A / B
-            return act ? ((uint64_t)(((uint32_t)(r.rc + q.rc) & 511u) + 1) << 32) : 0ull;
-#endif
+            QS_EXP_SLOT_KEY(act, r, q)
             const bool f = feasible<F>(r, x, q, px);
             const uint32_t tot = node_total<F>(r, x, q, px, cv, 0, 0.0, 0, 0.0, nullptr);
             return (act && f) ? ((uint64_t)(tot + 1) << 32) : 0ull;
@@ -2985,16 +3020,12 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                 uint32_t tot, fl = 0;
                 if constexpr (NORM) {  // the candidate's static against pod i+1 came with its entry
                     f = fits<F>(cr, crx, pn1) && (c1s1 & 1u) != 0u;
-                    tot = norm_total<F>(cr, pn1, cv, c1s1, nf.mt, yr.x, nf.ma, yr.y);
+                    tot = norm_total<F>(cr, crx, pn1, cv, c1s1, nf.mt, yr.x, nf.ma, yr.y);
                     if (!f) fl = holder_flags<F>(c1s1, nf.mt, nf.ma);
                 } else {
-#ifdef QS_EXP_CHEAP_C  // timing experiment only (wrong placements): no key arithmetic in C
-                    f = true;
-                    tot = (uint32_t)(cr.rc + pn1.rc) & 511u;
-#else
                     f = feasible<F>(cr, crx, pn1, px);
                     tot = node_total<F>(cr, crx, pn1, px, cv, 0, 0.0, 0, 0.0, nullptr);
-#endif
+                    QS_EXP_CAND_KEY(f, tot, cr, pn1)
                 }
                 QS_RSTAMP_MARK(1)
                 stage[par][lane] = r1;
@@ -3113,9 +3144,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
             // new slot of pod j's winner (j = i - 1): statics against pods >= j + 3 of this window
             // (cur) and every next-window pod
             auto new_slot = [&](uint32_t j, bool cur) {
-#ifdef QS_EXP_NOPARK
-                return;
-#endif
+                QS_EXP_PARK_RETURN()
                 const ResPub pv = read_pub(&pub[j & 1]);
                 if (pv.ks == 0 || pv.slot >= 0) return;
                 const RowX sx = stagexN[j & 1][pv.src];
@@ -3129,9 +3158,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
             };
             // inherited slots x next-window pods: slots 2j (lanes 0-31) and 2j + 1 (lanes 32-63)
             auto inherited = [&](uint32_t j) {
-#ifdef QS_EXP_NOPARK
-                return;
-#endif
+                QS_EXP_PARK_RETURN()
                 const uint32_t l = 2 * j + (lane < 32 ? 0u : 1u);
                 if (l < ndi && qq < knext) {
                     const RowX sx = carryxN[l];
@@ -3637,6 +3664,20 @@ static hipError_t scan_pod_f(const DevTable &t, const void *pods_, const DPodX *
     if (part & 2)
         hipLaunchKernelGGL((k_scan_commit<F>), dim3(1), dim3(256), 0, stream, t, pods, s, blocks, sc,
                            on, ok, st);
+    // the per-pod all-reduce engine (rows over the scratch's node range, no SoA): 8 the normalize
+    // maxima, 16 the keys, 32 their reduction into sc->best, 64 the commit of sc->best
+    if (!soa) {
+        if ((part & 8) && (F & kFeatNorm))
+            hipLaunchKernelGGL((k_scan_norm<F>), dim3(blocks), dim3(256), 0, stream, t, pods, podx, s, sc);
+        if (part & 16)
+            hipLaunchKernelGGL((k_scan_key<F>), dim3(blocks), dim3(256), 0, stream, t, pods, podx, s, c, sc,
+                               nullptr, nullptr, nullptr);
+        if (part & 32)
+            hipLaunchKernelGGL((k_scan_commit<F>), dim3(1), dim3(256), 0, stream, t, pods, s, blocks, sc,
+                               nullptr, nullptr, nullptr);
+        if (part & 64)
+            hipLaunchKernelGGL((k_scan_commit<F>), dim3(1), dim3(256), 0, stream, t, pods, s, 0u, sc, on, ok, st);
+    }
     return hipGetLastError();
 }
 
@@ -3797,5 +3838,31 @@ hipError_t wide_la_stream_res(const DevTable &t, const void *pods, const DPodX *
                               uint64_t *ok, uint64_t *st, void *ctl, uint32_t sel_blocks, uint64_t *rdiag,
                               const ResShard &rsh, hipStream_t stream);
 int wide_la_stream_res_per_cu(const LaGeom &geo, uint32_t feat, uint32_t n);
+
+// Configurable-scoring-resource entry points (kFeatRes; qs_kernels_res.inc, one translation unit per
+// row layout: res_compact_* and res_wide_*).
+#define QS_DECL_RES(P)                                                                                        \
+    hipError_t P##persistent(const DevTable &t, const void *pods, const DPodX *podx, uint32_t P_,            \
+                             const DevCfg &c, int32_t *on, uint64_t *ok, uint64_t *st, hipStream_t stream);   \
+    uint32_t P##persistent_max_nodes(uint32_t feat);                                                          \
+    hipError_t P##scan_pod(const DevTable &t, const void *pods, const DPodX *podx, uint32_t s,               \
+                           const DevCfg &c, void *scratch, int32_t *on, uint64_t *ok, uint64_t *st,           \
+                           uint8_t *feas, int32_t *score, int32_t *total, int part, hipStream_t stream);      \
+    hipError_t P##score_pod1(const DevTable &t, const void *pod, const DPodX *podx, const DevCfg &c,         \
+                             uint8_t *hout, uint64_t *gs, uint64_t seq, uint32_t pidx, const HostRow &prow,   \
+                             hipStream_t stream);                                                             \
+    hipError_t P##la_window(const DevTable &t, const void *pods, const DPodX *podx, uint32_t s0, uint32_t P_, \
+                            const DevCfg &c, const LaGeom &geo, const LaBufs &bf, int32_t *on, uint64_t *ok,  \
+                            uint64_t *st, uint64_t *diag, hipStream_t stream, int part);                     \
+    hipError_t P##la_stream_res(const DevTable &t, const void *pods, const DPodX *podx, const DevCfg &c,     \
+                                uint32_t P_, const LaGeom &geo, uint64_t *lists0, uint64_t *clists0,         \
+                                uint32_t lwords, uint32_t cwords, uint4 *npart, NormInfo *norm,               \
+                                uint32_t *stat, unsigned long long *nfall, int32_t *on, uint64_t *ok,         \
+                                uint64_t *st, void *ctl, uint32_t sel_blocks, uint64_t *rdiag,                \
+                                const ResShard &rsh, hipStream_t stream);                                     \
+    int P##la_stream_res_per_cu(const LaGeom &geo, uint32_t feat, uint32_t n);
+QS_DECL_RES(res_compact_)
+QS_DECL_RES(res_wide_)
+#undef QS_DECL_RES
 
 }  // namespace qs

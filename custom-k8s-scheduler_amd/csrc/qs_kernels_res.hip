@@ -1,0 +1,3 @@
+// Compact-row instantiations for configurable scoring resources (qs_kernels_res.inc).
+#define QS_RES_WIDE 0
+#include "qs_kernels_res.inc"

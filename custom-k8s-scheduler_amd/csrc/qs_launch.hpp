@@ -63,6 +63,12 @@ size_t score_pod1_pack_bytes(uint32_t n);
 hipError_t launch_score_pod1(const DevTable &t, const void *pod, const DPodX *podx, const DevCfg &c, uint8_t *hout,
                              uint64_t *gs, uint64_t seq, uint32_t pidx, const HostRow &prow, hipStream_t stream);
 size_t scan_scratch_bytes();
+// The head of the SCAN engine's device scratch (ScanScratch, qs_kernels.hpp): the reduced key, the
+// normalize maxima and the node range of the row scans (the per-pod all-reduce engine's shard).
+struct ScanHead {
+    unsigned long long best;
+    uint32_t mt, ma, lo, hi;
+};
 
 // L = list length per pod and shard (>= K; 2K for overlapped windows).
 LaGeom la_geometry(uint32_t n, uint32_t K, uint32_t W = 1, uint32_t L = 0);

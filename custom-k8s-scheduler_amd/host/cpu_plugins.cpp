@@ -48,10 +48,57 @@ void default_normalize(NodeScoreList &scores, bool reverse) {
 
 bool hard_effect(const std::string &e) { return e == kNoSchedule || e == kNoExecute; }
 
+// NodeResourcesFitArgs.ScoringStrategy.Resources / NodeResourcesBalancedAllocationArgs.Resources as
+// (qs_resource, weight) in list order; the defaults [cpu: fit_weight_cpu, memory: fit_weight_mem] and
+// [cpu, memory] (UP apis/config/v1/defaults.go)
+using ResList = std::vector<std::pair<int32_t, int64_t>>;
+ResList fit_list(const qs_config &c) {
+    if (c.n_fit_resources == 0) return {{QS_RES_CPU, c.fit_weight_cpu}, {QS_RES_MEMORY, c.fit_weight_mem}};
+    ResList r;
+    for (int i = 0; i < c.n_fit_resources; ++i) r.push_back({c.fit_resources[i].resource, c.fit_resources[i].weight});
+    return r;
+}
+ResList balanced_list(const qs_config &c) {
+    if (c.n_balanced_resources == 0) return {{QS_RES_CPU, 1}, {QS_RES_MEMORY, 1}};
+    ResList r;
+    for (int i = 0; i < c.n_balanced_resources; ++i) r.push_back({c.balanced_resources[i], 1});
+    return r;
+}
+
+int64_t lookup(const std::map<std::string, int64_t> &m, const std::string &k) {
+    auto it = m.find(k);
+    return it == m.end() ? 0 : it->second;
+}
+
+// UP noderesources/resource_allocation.go#calculateResourceAllocatableRequest: (allocatable,
+// requested + the pod's request) of one scoring resource; cpu / memory from NonZeroRequested and the
+// pod's non-zero requests (useRequested = false, LeastAllocated) or Requested and the plain requests
+// (true, BalancedAllocation); an extended (scalar) resource the pod does not request is (0, 0), and
+// so is one the node does not have (Allocatable.ScalarResources lookup).
+std::pair<int64_t, int64_t> alloc_request(const NodeInfo &ni, const PodResources &r, int32_t res,
+                                          bool use_requested, const std::vector<std::string> &ext_names) {
+    switch (res) {
+        case QS_RES_CPU:
+            return {ni.allocatable.milli_cpu,
+                    use_requested ? ni.requested.milli_cpu + r.cpu : ni.non_zero_requested.milli_cpu + r.nz_cpu};
+        case QS_RES_MEMORY:
+            return {ni.allocatable.memory,
+                    use_requested ? ni.requested.memory + r.mem : ni.non_zero_requested.memory + r.nz_mem};
+        default: {
+            const size_t k = (size_t)(res - QS_RES_EXT0);
+            if (k >= ext_names.size()) return {0, 0};
+            const std::string &name = ext_names[k];
+            const int64_t q = lookup(r.scalar, name);
+            if (q == 0 || !ni.allocatable.scalar.count(name)) return {0, 0};
+            return {ni.allocatable.scalar.at(name), lookup(ni.requested.scalar, name) + q};
+        }
+    }
+}
+
 // ---- NodeResourcesFit ------------------------------------------------------------------------
 class NodeResourcesFit final : public PreFilterPlugin, public FilterPlugin, public ScorePlugin {
    public:
-    NodeResourcesFit(const qs_config &cfg, Handle *h) : wc_(cfg.fit_weight_cpu), wm_(cfg.fit_weight_mem), h_(h) {}
+    NodeResourcesFit(const qs_config &cfg, Handle *h) : res_(fit_list(cfg)), h_(h) {}
     std::string Name() const override { return kNodeResourcesFit; }
 
     // UP fit.go#PreFilter computes the pod's requests once per cycle (preFilterState)
@@ -85,39 +132,40 @@ class NodeResourcesFit final : public PreFilterPlugin, public FilterPlugin, publ
         return why.empty() ? Status::OK() : Status(Code::Unschedulable, why);
     }
 
-    // LeastAllocated strategy over [cpu, memory] (UP least_allocated.go#leastResourceScorer):
-    // requested = NonZeroRequested + the pod's non-zero requests; resources with allocatable 0
-    // are skipped (resource_allocation.go#score)
+    // LeastAllocated strategy over the scoring resources (UP least_allocated.go#leastResourceScorer,
+    // resource_allocation.go#score): requested = NonZeroRequested + the pod's non-zero requests for
+    // cpu / memory, Requested + the request for extended resources; resources with allocatable 0 are
+    // skipped (their weight not counted)
     std::pair<int64_t, Status> Score(CycleState &s, const Pod &pod, const std::string &node) override {
         const NodeInfo *ni = node_of(h_, node);
         if (!ni) return {0, Status::AsError("node " + node + " not found")};
         PodResources tmp;
         const PodResources &r = resources_of(s, pod, h_, &tmp);
-        const int64_t alloc[2] = {ni->allocatable.milli_cpu, ni->allocatable.memory};
-        const int64_t reqd[2] = {ni->non_zero_requested.milli_cpu + r.nz_cpu, ni->non_zero_requested.memory + r.nz_mem};
-        const int64_t w[2] = {wc_, wm_};
         int64_t score = 0, wsum = 0;
-        for (int i = 0; i < 2; ++i) {
-            if (alloc[i] == 0) continue;
-            score += least_requested_score(reqd[i], alloc[i]) * w[i];
-            wsum += w[i];
+        for (const auto &rw : res_) {
+            const auto ar = alloc_request(*ni, r, rw.first, false, h_->ExtendedResourceNames());
+            if (ar.first == 0) continue;
+            score += least_requested_score(ar.second, ar.first) * rw.second;
+            wsum += rw.second;
         }
         return {wsum == 0 ? 0 : score / wsum, Status::OK()};
     }
 
    private:
-    int64_t wc_, wm_;
+    ResList res_;
     Handle *h_;
 };
 
 // ---- NodeResourcesBalancedAllocation ---------------------------------------------------------
 class BalancedAllocation final : public ScorePlugin {
    public:
-    BalancedAllocation(const qs_config &cfg, Handle *h) : skip_be_(cfg.balanced_skip_besteffort != 0), h_(h) {}
+    BalancedAllocation(const qs_config &cfg, Handle *h)
+        : res_(balanced_list(cfg)), skip_be_(cfg.balanced_skip_besteffort != 0), h_(h) {}
     std::string Name() const override { return kNodeResourcesBalancedAllocation; }
 
-    // UP balanced_allocation.go#balancedResourceScorer over [cpu, memory], float64: fractions of
-    // Requested + the pod's requests (capped at 1), std = |f0 - f1| / 2 for two resources,
+    // UP balanced_allocation.go#balancedResourceScorer over the configured resources, float64:
+    // fractions of Requested + the pod's requests (capped at 1) in list order, std = |f0 - f1| / 2 for
+    // two, the population standard deviation (mean, sum of squared deviations, sqrt) for more,
     // int64((1 - std) * MaxNodeScore)
     std::pair<int64_t, Status> Score(CycleState &s, const Pod &pod, const std::string &node) override {
         const NodeInfo *ni = node_of(h_, node);
@@ -125,22 +173,30 @@ class BalancedAllocation final : public ScorePlugin {
         PodResources tmp;
         const PodResources &r = resources_of(s, pod, h_, &tmp);
         if (skip_be_ && r.qos == QS_QOS_BESTEFFORT) return {0, Status::OK()};
-        const int64_t alloc[2] = {ni->allocatable.milli_cpu, ni->allocatable.memory};
-        const int64_t req[2] = {ni->requested.milli_cpu + r.cpu, ni->requested.memory + r.mem};
-        double fr[2];
+        double fr[QS_MAX_SCORE_RES], total = 0.0;
         int cnt = 0;
-        for (int i = 0; i < 2; ++i) {
-            if (alloc[i] == 0) continue;
-            const double f = (double)req[i] / (double)alloc[i];
-            fr[cnt++] = f > 1 ? 1 : f;
+        for (const auto &rw : res_) {
+            const auto ar = alloc_request(*ni, r, rw.first, true, h_->ExtendedResourceNames());
+            if (ar.first == 0) continue;
+            const double f = (double)ar.second / (double)ar.first;
+            fr[cnt] = f > 1 ? 1 : f;
+            total += fr[cnt++];
         }
         double sd = 0.0;
-        if (cnt == 2) sd = std::fabs((fr[0] - fr[1]) / 2);
+        if (cnt == 2) {
+            sd = std::fabs((fr[0] - fr[1]) / 2);
+        } else if (cnt > 2) {
+            const double mean = total / (double)cnt;
+            double sum = 0.0;
+            for (int i = 0; i < cnt; ++i) sum = sum + (fr[i] - mean) * (fr[i] - mean);
+            sd = std::sqrt(sum / (double)cnt);
+        }
         const double scaled = (1 - sd) * (double)kMaxNodeScore;
         return {(int64_t)scaled, Status::OK()};
     }
 
    private:
+    ResList res_;
     bool skip_be_;
     Handle *h_;
 };

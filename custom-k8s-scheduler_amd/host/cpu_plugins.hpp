@@ -34,7 +34,8 @@ inline const char *kTaintToleration = "TaintToleration";
 inline const char *kNodeAffinity = "NodeAffinity";
 inline const char *kCPUQoSSort = "QoSSort";
 
-// cfg: LeastAllocated resource weights (fit_weight_cpu / _mem), balanced_skip_besteffort.
+// cfg: the scoring-resource lists (fit_resources / balanced_resources, or fit_weight_cpu / _mem and
+// [cpu, memory]; extended resource k = the handle's ExtendedResourceNames()[k]), balanced_skip_besteffort.
 Registry CPURegistry(const qs_config &cfg);
 // One profile per QoS class ("besteffort", "burstable", "guaranteed"): NodeResourcesFit weight
 // w_fit[q], NodeResourcesBalancedAllocation w_bal[q], TaintToleration w_taint / NodeAffinity

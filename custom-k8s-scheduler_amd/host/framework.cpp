@@ -5,6 +5,7 @@
 #include "framework.hpp"
 
 #include <algorithm>
+#include <exception>
 #include <atomic>
 #include <cmath>
 #include <condition_variable>
@@ -121,12 +122,21 @@ struct Parallelizer::Impl {
     const std::function<void(int)> *fn = nullptr;
     int n = 0, chunk = 1;
     std::atomic<int> next{0}, active{0};
+    std::exception_ptr err;  // the first exception a piece of work threw (rethrown by Until)
     void chunks() {
-        for (;;) {
-            const int b = next.fetch_add(chunk, std::memory_order_relaxed);
-            if (b >= n) return;
-            const int e = std::min(n, b + chunk);
-            for (int i = b; i < e; ++i) (*fn)(i);
+        try {
+            for (;;) {
+                const int b = next.fetch_add(chunk, std::memory_order_relaxed);
+                if (b >= n) return;
+                const int e = std::min(n, b + chunk);
+                for (int i = b; i < e; ++i) (*fn)(i);
+            }
+        } catch (...) {
+            // keep the first exception, stop handing out pieces; Until still waits for every
+            // worker to leave fn (it points at the caller's stack) before rethrowing it
+            std::lock_guard<std::mutex> g(mu);
+            if (!err) err = std::current_exception();
+            next.store(n, std::memory_order_relaxed);
         }
     }
     void worker() {
@@ -177,6 +187,7 @@ void Parallelizer::Until(int n, const std::function<void(int)> &fn) {
         m_->fn = &fn;
         m_->n = n;
         m_->chunk = chunk;
+        m_->err = nullptr;
         m_->next.store(0, std::memory_order_relaxed);
         m_->active.store(workers_ - 1, std::memory_order_relaxed);
         m_->gen.fetch_add(1, std::memory_order_release);
@@ -187,6 +198,14 @@ void Parallelizer::Until(int n, const std::function<void(int)> &fn) {
         std::unique_lock<std::mutex> lk(m_->mu);
         m_->done.wait(lk, [&] { return m_->active.load(std::memory_order_acquire) == 0; });
     }
+    std::exception_ptr e;
+    {
+        std::lock_guard<std::mutex> g(m_->mu);
+        e = m_->err;
+        m_->err = nullptr;
+        m_->fn = nullptr;
+    }
+    if (e) std::rethrow_exception(e);  // as upstream's sequential loop would have surfaced it
 }
 
 // ---- Framework (UP framework/runtime/framework.go) -----------------------------------------

@@ -18,7 +18,8 @@ import ctypes
 import numpy as np
 
 from ._abi import (ENGINES, ENGINE_NAMES, EXPORTED, LIB_PATH, POD_DTYPE, QS_ABI_VERSION,
-                   QS_MAX_EXT, QS_MAX_TERMS, QS_MODE_BATCHED, QS_MODE_EXACT, QS_OK, QschedError,
+                   QS_MAX_EXT, QS_MAX_SCORE_RES, QS_MAX_TERMS, QS_MODE_BATCHED, QS_MODE_EXACT, QS_OK,
+                   RESOURCES, QschedError,
                    QschedLibraryMissing, QsConfig, QsContainer, QsNodeRow, QsNodeSoa, QsStats,
                    load)
 
@@ -100,6 +101,21 @@ class Config(dict):
             if k in ("w_fit", "w_bal"):
                 for i in range(3):
                     getattr(c, k)[i] = int(v[i])
+            elif k == "fit_resources":  # [(name | id, weight), ...] (spec S5 "Scoring resources")
+                v = list(v or [])
+                if len(v) > QS_MAX_SCORE_RES:
+                    raise ValueError("at most 4 scoring resources")
+                c.n_fit_resources = len(v)
+                for i, (name, w) in enumerate(v):
+                    c.fit_resources[i][0] = RESOURCES[name] if isinstance(name, str) else int(name)
+                    c.fit_resources[i][1] = int(w)
+            elif k == "balanced_resources":  # [name | id, ...]
+                v = list(v or [])
+                if len(v) > QS_MAX_SCORE_RES:
+                    raise ValueError("at most 4 balanced resources")
+                c.n_balanced_resources = len(v)
+                for i, name in enumerate(v):
+                    c.balanced_resources[i] = RESOURCES[name] if isinstance(name, str) else int(name)
             else:
                 setattr(c, k, int(v))
         return c

@@ -16,19 +16,22 @@ PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # QSCHED_LIB (diagnostic builds, e.g. tools/diag_build.sh) overrides the in-tree library
 LIB_PATH = os.environ.get("QSCHED_LIB") or os.path.join(PKG_ROOT, "libqsched.so")
 
-QS_ABI_VERSION = 2
+QS_ABI_VERSION = 3
 QS_MAX_EXT = 2
 QS_MAX_TERMS = 4
 QS_MAX_APPS = 1024
 QS_MAX_ZONES = 64
 QS_AA_NONE, QS_AA_HOSTNAME, QS_AA_ZONE = 0, 1, 2
+QS_MAX_SCORE_RES = 4
+# qs_resource: scoring-resource ids ("ext0" / "ext1" = the table's extended-resource columns)
+RESOURCES = {"cpu": 1, "memory": 2, "ext0": 3, "ext1": 4}
 
 QS_OK, QS_EINVAL, QS_EDEVICE, QS_ETIMEOUT, QS_ENOMEM, QS_ESTATE = range(6)
 STATUS_NAMES = {0: "QS_OK", 1: "QS_EINVAL", 2: "QS_EDEVICE", 3: "QS_ETIMEOUT", 4: "QS_ENOMEM",
                 5: "QS_ESTATE"}
 QS_QOS_BESTEFFORT, QS_QOS_BURSTABLE, QS_QOS_GUARANTEED = 0, 1, 2
 QS_MODE_EXACT, QS_MODE_BATCHED = 0, 1
-ENGINES = {"auto": 0, "persistent": 1, "scan": 2, "lookahead": 3, "batched": 4}
+ENGINES = {"auto": 0, "persistent": 1, "scan": 2, "lookahead": 3, "batched": 4, "allreduce": 5}
 ENGINE_NAMES = {v: k for k, v in ENGINES.items()}
 LAYOUT_NAMES = {0: "compact", 1: "wide"}
 
@@ -54,6 +57,9 @@ class QsConfig(ctypes.Structure):
                 ("profile_kernels", ctypes.c_int32), ("virtual_shards", ctypes.c_int32),
                 ("lookahead_serial", ctypes.c_int32),
                 ("scan_soa_min_nodes", ctypes.c_int32), ("batch_pods", ctypes.c_int32),
+                ("n_fit_resources", ctypes.c_int32), ("fit_resources", (ctypes.c_int32 * 2) * QS_MAX_SCORE_RES),
+                ("n_balanced_resources", ctypes.c_int32),
+                ("balanced_resources", ctypes.c_int32 * QS_MAX_SCORE_RES),
                 ("reserved", ctypes.c_int32 * 3)]
 
 

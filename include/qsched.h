@@ -41,11 +41,12 @@ extern "C" {
 #define QS_API
 #endif
 
-#define QS_ABI_VERSION 2
+#define QS_ABI_VERSION 3
 #define QS_MAX_EXT 2   /* extended resources per node/pod (e.g. amd.com/gpu) */
 #define QS_MAX_TERMS 4 /* node-affinity terms per pod (required OR-terms, preferred terms) */
 #define QS_MAX_APPS 1024 /* anti-affinity groups (batched mode, spec S11) */
 #define QS_MAX_ZONES 64  /* topology zones (batched mode zone anti-affinity) */
+#define QS_MAX_SCORE_RES 4 /* entries of a scoring-resource list (cpu, memory, ext 0, ext 1) */
 
 typedef enum qs_status {
     QS_OK = 0,
@@ -65,13 +66,26 @@ typedef enum qs_mode { QS_MODE_EXACT = 0, QS_MODE_BATCHED = 1 } qs_mode;
  * UP plugins/interpodaffinity that config 5 uses): none, per node (topologyKey hostname), per zone. */
 typedef enum qs_anti_affinity { QS_AA_NONE = 0, QS_AA_HOSTNAME = 1, QS_AA_ZONE = 2 } qs_anti_affinity;
 
+/* Scoring resources (spec/semantics.md S5 "Scoring resources"): cpu, memory, or one of the table's
+ * two extended-resource columns (the caller interns e.g. "amd.com/gpu" as QS_RES_EXT0). */
+typedef enum qs_resource { QS_RES_NONE = 0, QS_RES_CPU = 1, QS_RES_MEMORY = 2, QS_RES_EXT0 = 3, QS_RES_EXT1 = 4 } qs_resource;
+/* One entry of NodeResourcesFitArgs.ScoringStrategy.Resources (UP apis/config#ResourceSpec{Name, Weight}). */
+typedef struct qs_resource_spec {
+    int32_t resource; /* qs_resource */
+    int32_t weight;   /* 1..100 (UP apis/config/validation#validateResources) */
+} qs_resource_spec;
+
 /* Which device engine runs the exact stream (all are bit-exact; AUTO picks the fastest). */
 typedef enum qs_engine {
     QS_ENGINE_AUTO = 0,
     QS_ENGINE_PERSISTENT = 1, /* one resident workgroup, node rows in registers (N <= 8192) */
     QS_ENGINE_SCAN = 2,       /* per-pod grid scan + finalize/reserve launch chain (any N) */
     QS_ENGINE_LOOKAHEAD = 3,  /* exact top-K lookahead: chip-wide stale scan + sequential resolve */
-    QS_ENGINE_BATCHED = 4     /* reported by qs_stats.engine_used for QS_MODE_BATCHED streams */
+    QS_ENGINE_BATCHED = 4,    /* reported by qs_stats.engine_used for QS_MODE_BATCHED streams */
+    QS_ENGINE_ALLREDUCE = 5   /* sharded contexts with an RCCL communicator: per pod every rank scans its
+                                 node shard and the ranks max-reduce one packed key with
+                                 ncclAllReduce(count 1, ncclUint64, ncclMax) (+ the two normalize maxima for
+                                 TaintToleration / NodeAffinity); the as-is RCCL baseline of SURVEY.md §8(e) C1 */
 } qs_engine;
 
 typedef struct qs_config {
@@ -98,6 +112,16 @@ typedef struct qs_config {
     int32_t scan_soa_min_nodes;  /* tables with at least this many nodes also keep the column-major
                                     copy the SCAN engine / qs_score_pod stream (0 = 65,536; -1 never) */
     int32_t batch_pods;          /* QS_MODE_BATCHED: pods per batch (0 = 64; at most 64) */
+    /* NodeResourcesFitArgs.ScoringStrategy.Resources of the LeastAllocated strategy, in list order
+     * (replaces UP apis/config/types_pluginargs.go#ScoringStrategy.Resources); 0 entries = the
+     * default [cpu: fit_weight_cpu, memory: fit_weight_mem].  Distinct resources, weights 1..100. */
+    int32_t n_fit_resources;
+    qs_resource_spec fit_resources[QS_MAX_SCORE_RES];
+    /* NodeResourcesBalancedAllocationArgs.Resources in list order (UP types_pluginargs.go#
+     * NodeResourcesBalancedAllocationArgs); 0 entries = the default [cpu, memory].  With three or
+     * more resources requested the score takes the mean / sqrt standard deviation (spec S5). */
+    int32_t n_balanced_resources;
+    int32_t balanced_resources[QS_MAX_SCORE_RES]; /* qs_resource */
     int32_t reserved[3];
 } qs_config;
 

@@ -40,7 +40,19 @@ POD_FIELDS_I64 = ["req_cpu", "req_mem", "nz_cpu", "nz_mem"]
 
 # spec S9 default profile weights, indexed by QoS class [BestEffort, Burstable, Guaranteed]
 DEFAULT_CONFIG = dict(wc=1, wm=1, w_fit=(1, 2, 3), w_bal=(1, 1, 1), w_tt=3, w_na=2,
-                      enable_taint=0, enable_affinity=0, balanced_skip_besteffort=0, qos_sort=1)
+                      enable_taint=0, enable_affinity=0, balanced_skip_besteffort=0, qos_sort=1,
+                      fit_resources=None, balanced_resources=None)
+
+# Scoring-resource names of the configurable lists (NodeResourcesFitArgs.ScoringStrategy.Resources =
+# fit_resources [(name, weight), ...]; NodeResourcesBalancedAllocationArgs.Resources =
+# balanced_resources [name, ...]); None = upstream's defaults [cpu:1, memory:1] / [cpu, memory].
+# "ext0" / "ext1" are the table's two extended-resource columns (e.g. amd.com/gpu).
+RES_IDS = {"cpu": 1, "memory": 2, "ext0": 3, "ext1": 4}
+MAX_SCORE_RES = 4
+
+
+def res_id(name) -> int:
+    return name if isinstance(name, int) else RES_IDS[name]
 
 
 def empty_cluster(n: int, p: int):
@@ -92,7 +104,9 @@ class _Config(ctypes.Structure):
     _fields_ = [("wc", ctypes.c_int64), ("wm", ctypes.c_int64), ("w_fit", ctypes.c_int32 * 3),
                 ("w_bal", ctypes.c_int32 * 3), ("w_tt", ctypes.c_int32), ("w_na", ctypes.c_int32),
                 ("enable_taint", ctypes.c_int32), ("enable_affinity", ctypes.c_int32),
-                ("balanced_skip_besteffort", ctypes.c_int32), ("qos_sort", ctypes.c_int32)]
+                ("balanced_skip_besteffort", ctypes.c_int32), ("qos_sort", ctypes.c_int32),
+                ("n_fit_res", ctypes.c_int32), ("fit_res", ctypes.c_int32 * 4), ("fit_w", ctypes.c_int32 * 4),
+                ("n_bal_res", ctypes.c_int32), ("bal_res", ctypes.c_int32 * 4)]
 
 
 _LIB = None
@@ -115,6 +129,10 @@ def lib():
         L.or_least_allocated.argtypes = [ctypes.c_int64] * 6
         L.or_balanced.restype = ctypes.c_int64
         L.or_balanced.argtypes = [ctypes.c_int64] * 4
+        L.or_least_allocated_v.restype = ctypes.c_int64
+        L.or_least_allocated_v.argtypes = [ctypes.c_int] + [ctypes.POINTER(ctypes.c_int64)] * 3
+        L.or_balanced_v.restype = ctypes.c_int64
+        L.or_balanced_v.argtypes = [ctypes.c_int] + [ctypes.POINTER(ctypes.c_int64)] * 2
         L.or_schedule.restype = None
         L.or_schedule.argtypes = [ctypes.c_void_p] * 6 + [ctypes.c_int]
         L.or_schedule_incremental.restype = ctypes.c_int
@@ -165,6 +183,14 @@ def _mk_cfg(cfg):
     s.w_tt, s.w_na = c["w_tt"], c["w_na"]
     s.enable_taint, s.enable_affinity = c["enable_taint"], c["enable_affinity"]
     s.balanced_skip_besteffort, s.qos_sort = c["balanced_skip_besteffort"], c["qos_sort"]
+    fr = c.get("fit_resources") or []
+    s.n_fit_res = len(fr)
+    for i, (name, w) in enumerate(fr):
+        s.fit_res[i], s.fit_w[i] = res_id(name), w
+    br = c.get("balanced_resources") or []
+    s.n_bal_res = len(br)
+    for i, name in enumerate(br):
+        s.bal_res[i] = res_id(name)
     return s
 
 
@@ -335,6 +361,25 @@ def py_normalize(raw, mx, reverse):
     return MAX_NODE_SCORE - s if reverse else s
 
 
+def py_alloc_request(nodes, pods, n, j, res, use_requested):
+    """UP noderesources/resource_allocation.go#calculateResourceAllocatableRequest: (allocatable,
+    requested + pod request) of one scoring resource; cpu / memory from NonZeroRequested and the
+    pod's non-zero request (LeastAllocated) or Requested and the plain request (Balanced); an
+    extended resource the pod does not request is (0, 0): skipped."""
+    rid = res_id(res)
+    if rid == 1:
+        k = ("req_cpu", "req_cpu") if use_requested else ("nz_cpu", "nz_cpu")
+        return int(nodes["alloc_cpu"][n]), int(nodes[k[0]][n]) + int(pods[k[1]][j])
+    if rid == 2:
+        k = ("req_mem", "req_mem") if use_requested else ("nz_mem", "nz_mem")
+        return int(nodes["alloc_mem"][n]), int(nodes[k[0]][n]) + int(pods[k[1]][j])
+    e = rid - 3
+    q = int(pods["req_ext"][j][e])
+    if q == 0:
+        return 0, 0
+    return int(nodes["alloc_ext"][n][e]), int(nodes["req_ext"][n][e]) + q
+
+
 def py_keys(nodes, pods, j, cfg):
     n_nodes = len(nodes["alloc_cpu"])
     feas = [py_feasible(nodes, pods, n, j, cfg) for n in range(n_nodes)]
@@ -348,13 +393,12 @@ def py_keys(nodes, pods, j, cfg):
         if not feas[n]:
             keys.append(0)
             continue
-        la = py_least_allocated(
-            (int(nodes["alloc_cpu"][n]), int(nodes["alloc_mem"][n])),
-            (int(nodes["nz_cpu"][n] + pods["nz_cpu"][j]), int(nodes["nz_mem"][n] + pods["nz_mem"][j])),
-            (cfg["wc"], cfg["wm"]))
-        ba = py_balanced(
-            (int(nodes["alloc_cpu"][n]), int(nodes["alloc_mem"][n])),
-            (int(nodes["req_cpu"][n] + pods["req_cpu"][j]), int(nodes["req_mem"][n] + pods["req_mem"][j])))
+        fit = cfg.get("fit_resources") or [("cpu", cfg["wc"]), ("memory", cfg["wm"])]
+        la_ar = [py_alloc_request(nodes, pods, n, j, r, False) for r, _ in fit]
+        la = py_least_allocated([a for a, _ in la_ar], [r for _, r in la_ar], [w for _, w in fit])
+        bal = cfg.get("balanced_resources") or ["cpu", "memory"]
+        ba_ar = [py_alloc_request(nodes, pods, n, j, r, True) for r in bal]
+        ba = py_balanced([a for a, _ in ba_ar], [r for _, r in ba_ar])
         if cfg["balanced_skip_besteffort"] and q == 0:
             ba = 0
         total = cfg["w_fit"][q] * la + cfg["w_bal"][q] * ba

@@ -26,14 +26,12 @@ static int64_t least_requested_score(int64_t requested, int64_t capacity) {
     return ((capacity - requested) * MAX_NODE_SCORE) / capacity;
 }
 
-/* UP noderesources/least_allocated.go#leastResourceScorer over resources [cpu, memory];
- * requested = NonZeroRequested + pod non-zero request (resource_allocation.go#score,
- * calculateResourceAllocatableRequest with useRequested=false). */
-int64_t or_least_allocated(int64_t alloc_c, int64_t reqd_c, int64_t alloc_m, int64_t reqd_m,
-                           int64_t wc, int64_t wm) {
-    int64_t alloc[2] = {alloc_c, alloc_m}, reqd[2] = {reqd_c, reqd_m}, w[2] = {wc, wm};
+/* UP noderesources/least_allocated.go#leastResourceScorer: requested[i] / allocatable[i] as
+ * resource_allocation.go#score fills them (an entry with allocatable 0 is skipped, its weight not
+ * counted). */
+int64_t or_least_allocated_v(int cnt, const int64_t *alloc, const int64_t *reqd, const int64_t *w) {
     int64_t node_score = 0, weight_sum = 0;
-    for (int i = 0; i < 2; i++) {
+    for (int i = 0; i < cnt; i++) {
         if (alloc[i] == 0) continue;
         node_score += least_requested_score(reqd[i], alloc[i]) * w[i];
         weight_sum += w[i];
@@ -42,27 +40,123 @@ int64_t or_least_allocated(int64_t alloc_c, int64_t reqd_c, int64_t alloc_m, int
     return node_score / weight_sum;
 }
 
-/* UP noderesources/balanced_allocation.go#balancedResourceScorer over [cpu, memory];
- * requested = Requested + pod request (useRequested=true). */
-int64_t or_balanced(int64_t alloc_c, int64_t req_c, int64_t alloc_m, int64_t req_m) {
-    int64_t alloc[2] = {alloc_c, alloc_m}, reqd[2] = {req_c, req_m};
-    double fr[2];
-    int cnt = 0;
-    for (int i = 0; i < 2; i++) {
+/* The default resource list [cpu, memory]: requested = NonZeroRequested + pod non-zero request
+ * (resource_allocation.go#score, calculateResourceAllocatableRequest with useRequested=false). */
+int64_t or_least_allocated(int64_t alloc_c, int64_t reqd_c, int64_t alloc_m, int64_t reqd_m,
+                           int64_t wc, int64_t wm) {
+    const int64_t alloc[2] = {alloc_c, alloc_m}, reqd[2] = {reqd_c, reqd_m}, w[2] = {wc, wm};
+    return or_least_allocated_v(2, alloc, reqd, w);
+}
+
+/* UP noderesources/balanced_allocation.go#balancedResourceScorer (float64 throughout; Go on amd64
+ * fuses nothing, so every product and sum below is rounded on its own: -ffp-contract=off, and
+ * volatile where the compiler could otherwise keep a value in extended precision). */
+int64_t or_balanced_v(int cnt, const int64_t *alloc, const int64_t *reqd) {
+    double fr[OR_MAX_SCORE_RES];
+    double total = 0;
+    int k = 0;
+    for (int i = 0; i < cnt && k < OR_MAX_SCORE_RES; i++) {
         if (alloc[i] == 0) continue;
         volatile double f = (double)reqd[i] / (double)alloc[i];
         double ff = f;
         if (ff > 1) ff = 1;
-        fr[cnt++] = ff;
+        volatile double t = total + ff; /* totalFraction += fraction */
+        total = t;
+        fr[k++] = ff;
     }
     double std = 0.0;
-    if (cnt == 2) {
+    if (k == 2) {
         volatile double d = (fr[0] - fr[1]) / 2;
         std = fabs(d);
+    } else if (k > 2) {
+        volatile double mean = total / (double)k;
+        double sum = 0;
+        for (int i = 0; i < k; i++) {
+            volatile double d = fr[i] - mean;
+            volatile double sq = d * d;
+            volatile double t = sum + sq; /* sum = sum + (fraction-mean)*(fraction-mean) */
+            sum = t;
+        }
+        volatile double var = sum / (double)k;
+        std = sqrt(var); /* Go math.Sqrt: correctly rounded (SQRTSD on amd64) */
     }
     volatile double one_minus = 1 - std;
     volatile double scaled = one_minus * (double)MAX_NODE_SCORE;
     return (int64_t)scaled;
+}
+
+/* The default resource list [cpu, memory]; requested = Requested + pod request (useRequested=true). */
+int64_t or_balanced(int64_t alloc_c, int64_t req_c, int64_t alloc_m, int64_t req_m) {
+    const int64_t alloc[2] = {alloc_c, alloc_m}, reqd[2] = {req_c, req_m};
+    return or_balanced_v(2, alloc, reqd);
+}
+
+/* UP noderesources/resource_allocation.go#calculateResourceAllocatableRequest for node n and pod j:
+ * cpu / memory from NonZeroRequested (use_requested = 0, LeastAllocated) or Requested (1,
+ * BalancedAllocation) plus the pod's request of the same kind (calculatePodResourceRequest: the
+ * non-zero defaults only when !useRequested); an extended (scalar) resource the pod does not
+ * request is (0, 0), i.e. skipped; otherwise Allocatable.ScalarResources and
+ * Requested.ScalarResources + the pod's request. */
+static void alloc_request(const or_nodes *nd, const or_pods *pd, uint32_t n, uint32_t j, int res,
+                          int use_requested, int64_t *alloc, int64_t *reqd) {
+    *alloc = 0;
+    *reqd = 0;
+    switch (res) {
+        case OR_RES_CPU:
+            *alloc = nd->alloc_cpu[n];
+            *reqd = use_requested ? nd->req_cpu[n] + pd->req_cpu[j] : nd->nz_cpu[n] + pd->nz_cpu[j];
+            break;
+        case OR_RES_MEMORY:
+            *alloc = nd->alloc_mem[n];
+            *reqd = use_requested ? nd->req_mem[n] + pd->req_mem[j] : nd->nz_mem[n] + pd->nz_mem[j];
+            break;
+        case OR_RES_EXT0:
+        case OR_RES_EXT1: {
+            const int k = res - OR_RES_EXT0;
+            const int64_t q = pd->req_ext[j * OR_MAX_EXT + k];
+            if (q == 0) break; /* podRequest == 0 && IsScalarResourceName */
+            *alloc = nd->alloc_ext[n * OR_MAX_EXT + k];
+            *reqd = nd->req_ext[n * OR_MAX_EXT + k] + q;
+            break;
+        }
+        default:
+            break;
+    }
+}
+
+/* NodeResourcesFit.Score, ScoringStrategy LeastAllocated, over the configured resources. */
+static int64_t least_allocated_node(const or_config *cfg, const or_nodes *nd, const or_pods *pd, uint32_t n,
+                                    uint32_t j) {
+    int64_t alloc[OR_MAX_SCORE_RES], reqd[OR_MAX_SCORE_RES], w[OR_MAX_SCORE_RES];
+    int cnt = 0;
+    if (cfg->n_fit_res <= 0) { /* defaults: [{cpu, wc}, {memory, wm}] */
+        alloc_request(nd, pd, n, j, OR_RES_CPU, 0, &alloc[0], &reqd[0]);
+        alloc_request(nd, pd, n, j, OR_RES_MEMORY, 0, &alloc[1], &reqd[1]);
+        w[0] = cfg->wc;
+        w[1] = cfg->wm;
+        cnt = 2;
+    } else {
+        for (; cnt < cfg->n_fit_res && cnt < OR_MAX_SCORE_RES; cnt++) {
+            alloc_request(nd, pd, n, j, cfg->fit_res[cnt], 0, &alloc[cnt], &reqd[cnt]);
+            w[cnt] = cfg->fit_w[cnt];
+        }
+    }
+    return or_least_allocated_v(cnt, alloc, reqd, w);
+}
+
+/* NodeResourcesBalancedAllocation.Score over the configured resources. */
+static int64_t balanced_node(const or_config *cfg, const or_nodes *nd, const or_pods *pd, uint32_t n, uint32_t j) {
+    int64_t alloc[OR_MAX_SCORE_RES], reqd[OR_MAX_SCORE_RES];
+    int cnt = 0;
+    if (cfg->n_bal_res <= 0) { /* defaults: [cpu, memory] */
+        alloc_request(nd, pd, n, j, OR_RES_CPU, 1, &alloc[0], &reqd[0]);
+        alloc_request(nd, pd, n, j, OR_RES_MEMORY, 1, &alloc[1], &reqd[1]);
+        cnt = 2;
+    } else {
+        for (; cnt < cfg->n_bal_res && cnt < OR_MAX_SCORE_RES; cnt++)
+            alloc_request(nd, pd, n, j, cfg->bal_res[cnt], 1, &alloc[cnt], &reqd[cnt]);
+    }
+    return or_balanced_v(cnt, alloc, reqd);
 }
 
 /* UP noderesources/fit.go#fitsRequest (+ TooManyPods check) */
@@ -132,11 +226,8 @@ static uint64_t node_key(const or_config *cfg, const or_nodes *nd, const or_pods
                          uint32_t j, int64_t mt, int64_t ma, int64_t *sc) {
     if (!feasible(cfg, nd, pd, n, j)) return 0;
     int q = pd->qos[j];
-    int64_t la = or_least_allocated(nd->alloc_cpu[n], nd->nz_cpu[n] + pd->nz_cpu[j],
-                                    nd->alloc_mem[n], nd->nz_mem[n] + pd->nz_mem[j], cfg->wc,
-                                    cfg->wm);
-    int64_t ba = or_balanced(nd->alloc_cpu[n], nd->req_cpu[n] + pd->req_cpu[j], nd->alloc_mem[n],
-                             nd->req_mem[n] + pd->req_mem[j]);
+    int64_t la = least_allocated_node(cfg, nd, pd, n, j);
+    int64_t ba = balanced_node(cfg, nd, pd, n, j);
     if (cfg->balanced_skip_besteffort && q == 0) ba = 0;
     int64_t tt = 0, na = 0;
     if (cfg->enable_taint) tt = normalize(taint_raw(nd, pd, n, j), mt, 1);

@@ -19,6 +19,10 @@
 
 #define OR_MAX_EXT 2
 #define OR_MAX_TERMS 4
+/* scoring-resource ids of the configurable resource lists (NodeResourcesFitArgs.ScoringStrategy.
+ * Resources, NodeResourcesBalancedAllocationArgs.Resources): cpu, memory, extended resource 0 / 1 */
+#define OR_MAX_SCORE_RES 4
+enum { OR_RES_NONE = 0, OR_RES_CPU = 1, OR_RES_MEMORY = 2, OR_RES_EXT0 = 3, OR_RES_EXT1 = 4 };
 
 typedef struct {
     uint32_t n;
@@ -44,6 +48,10 @@ typedef struct {
     int32_t w_fit[3], w_bal[3]; /* per QoS class: [BestEffort, Burstable, Guaranteed] */
     int32_t w_tt, w_na;
     int32_t enable_taint, enable_affinity, balanced_skip_besteffort, qos_sort;
+    /* LeastAllocated scoring resources in list order (n_fit_res = 0: [(cpu, wc), (memory, wm)]) */
+    int32_t n_fit_res, fit_res[OR_MAX_SCORE_RES], fit_w[OR_MAX_SCORE_RES];
+    /* BalancedAllocation resources in list order (n_bal_res = 0: [cpu, memory]) */
+    int32_t n_bal_res, bal_res[OR_MAX_SCORE_RES];
 } or_config;
 
 /* Per-node plugin scores for one pod against the current node table (no state change).
@@ -90,5 +98,9 @@ void or_generate(int config, uint64_t seed, or_nodes *nodes, or_pods *pods);
 int64_t or_least_allocated(int64_t alloc_c, int64_t reqd_c, int64_t alloc_m, int64_t reqd_m,
                            int64_t wc, int64_t wm);
 int64_t or_balanced(int64_t alloc_c, int64_t req_c, int64_t alloc_m, int64_t req_m);
+/* The same scorers over a resource list: (alloc[i], reqd[i]) as calculateResourceAllocatableRequest
+ * returns them ((0, 0) for an extended resource the pod does not request), w[i] the weights. */
+int64_t or_least_allocated_v(int cnt, const int64_t *alloc, const int64_t *reqd, const int64_t *w);
+int64_t or_balanced_v(int cnt, const int64_t *alloc, const int64_t *reqd);
 
 #endif

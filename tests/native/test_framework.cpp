@@ -11,14 +11,17 @@
 //   test_framework --gpu   the QoSGPU plugins on the device: filter/score tables, and the whole
 //                          ScheduleOne loop on a config-4 cluster built from k8s objects, checked
 //                          pod-by-pod against qs_schedule_stream and the CPU oracle.
+#include <atomic>
 #include <cstdio>
 #include <cstring>
 #include <functional>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
 #include "../../custom-k8s-scheduler_amd/host/cpu_plugins.hpp"
 #include "../../custom-k8s-scheduler_amd/host/qos_gpu.hpp"
+#include "../../tools/oracle_cfg.hpp"
 #include "../../tools/synth_objects.hpp"
 extern "C" {
 #include "../../oracle/qs_oracle.h"
@@ -208,6 +211,21 @@ static qs_config default_cfg(bool taint = false, bool affinity = false) {
     return c;
 }
 
+// The AMD-GPU cluster configuration: LeastAllocated {cpu:1, memory:1, amd.com/gpu:5},
+// BalancedAllocation over [cpu, memory, amd.com/gpu] (amd.com/gpu = extended resource 0).
+static qs_config gpu_scoring_cfg(bool taint, bool affinity) {
+    qs_config c = default_cfg(taint, affinity);
+    c.n_fit_resources = 3;
+    c.fit_resources[0] = {QS_RES_CPU, 1};
+    c.fit_resources[1] = {QS_RES_MEMORY, 1};
+    c.fit_resources[2] = {QS_RES_EXT0, 5};
+    c.n_balanced_resources = 3;
+    c.balanced_resources[0] = QS_RES_CPU;
+    c.balanced_resources[1] = QS_RES_MEMORY;
+    c.balanced_resources[2] = QS_RES_EXT0;
+    return c;
+}
+
 // Scores of one score plugin (weight 1) for `pod` on every node, through PreFilter + Score.
 static std::vector<int64_t> plugin_scores(const qs_config &cfg, const std::vector<Node> &nodes,
                                           const Pod &pod, const char *plugin,
@@ -352,7 +370,7 @@ static void test_gpu_schedule_one_loop_parity() {
     or_pods op{p, prc.data(), prm.data(), pre.data(), pzc.data(), pzm.data(), pq.data(), ppr.data(), pth.data(),
                pts.data(), psel.data(), pnr.data(), pnp.data(), prt.data(), ppt.data(), ppw.data(), nullptr, nullptr};
     or_generate(4, seed, &on, &op);
-    or_config oc{1, 1, {1, 2, 3}, {1, 1, 1}, 3, 2, 1, 1, 0, 1};
+    const or_config oc = oracle_cfg(cfg);
     std::vector<int32_t> oracle(p);
     or_schedule(&oc, &on, &op, oracle.data(), nullptr, nullptr, 8);
 
@@ -369,6 +387,29 @@ static void test_gpu_schedule_one_loop_parity() {
     CHECK_EQ(diff_stream, 0);
     CHECK_EQ(diff_oracle, 0);
     CHECK(unsched > 0 && unsched < (int)p);
+}
+
+// Parallelizer::Until: an exception thrown by a piece of work on any thread reaches the caller once
+// every worker has left the work function, and the pool stays usable.
+static void test_parallelizer_exceptions() {
+    Parallelizer par(8);
+    for (int rep = 0; rep < 20; ++rep) {
+        std::atomic<int> ran{0};
+        bool thrown = false;
+        try {
+            par.Until(1000, [&](int i) {
+                ran.fetch_add(1);
+                if (i == 37 + rep) throw std::runtime_error("piece failed");
+            });
+        } catch (const std::runtime_error &e) {
+            thrown = std::string(e.what()) == "piece failed";
+        }
+        CHECK(thrown);
+        CHECK(ran.load() <= 1000);
+        std::atomic<int> sum{0};
+        par.Until(1000, [&](int i) { sum.fetch_add(i); });
+        CHECK_EQ(sum.load(), 999 * 1000 / 2);
+    }
 }
 
 // ---- the CPU reference plugins (host/cpu_plugins.cpp) ------------------------------------------
@@ -399,14 +440,49 @@ static void test_cpu_plugin_scores() {
     }
 }
 
+// spec/kat.md K10 / K11 / K12 (configurable scoring resources) through the CPU plugins' Score.
+static void test_cpu_plugin_scores_resource_lists() {
+    const qs_config cfg = gpu_scoring_cfg(false, false);
+    struct Tc {
+        const char *node_cpu, *node_mem, *node_gpu, *used_cpu, *used_mem, *used_gpu, *cpu, *mem, *gpu;
+        int64_t la, ba;
+    } tcs[] = {
+        // K10 / K11: used (2000m, 8Gi, 2) + pod (2000m, 8Gi, 4) on (8000m, 32Gi, 8)
+        {"8000m", "32Gi", "8", "2000m", "8Gi", "2", "2000m", "8Gi", "4", 32, 88},
+        // K10b: the pod requests no gpu -> gpu skipped in both lists
+        {"8000m", "32Gi", "8", "2000m", "8Gi", "2", "2000m", "8Gi", nullptr, 50, 100},
+        // K12: three resources at 4/5 -> float64 std > 0 -> 99 (exact arithmetic: 100)
+        {"4000m", "10Gi", "5", nullptr, nullptr, nullptr, "3200m", "8Gi", "4", 20, 99},
+    };
+    for (const auto &tc : tcs) {
+        Scheduler sched(CPURegistry(cfg), CPUProfiles(cfg), CPUProfileOf, 1);
+        sched.AddNode(MakeNode("n0").Capacity({{kCPU, tc.node_cpu}, {kMemory, tc.node_mem}, {"amd.com/gpu", tc.node_gpu},
+                                               {kPods, "110"}}).Obj());
+        if (tc.used_cpu) {  // the node's usage: one pod scheduled (and assumed) there first
+            sched.AddPod(MakePod("used").ReqLim({{kCPU, tc.used_cpu}, {kMemory, tc.used_mem}, {"amd.com/gpu", tc.used_gpu}}, {}).Obj());
+            const auto placed = sched.Run();
+            CHECK(placed.size() == 1 && placed[0].node_index == 0);
+        }
+        ResourceList req{{kCPU, tc.cpu}, {kMemory, tc.mem}};
+        if (tc.gpu) req["amd.com/gpu"] = tc.gpu;
+        Pod pod = MakePod("p").ReqLim(req, {}).Obj();
+        auto reg = CPURegistry(cfg);
+        auto fit = std::dynamic_pointer_cast<ScorePlugin>(reg[kNodeResourcesFit](&sched));
+        auto bal = std::dynamic_pointer_cast<ScorePlugin>(reg[kNodeResourcesBalancedAllocation](&sched));
+        CycleState st;
+        CHECK_EQ(fit->Score(st, pod, "n0").first, tc.la);
+        CHECK_EQ(bal->Score(st, pod, "n0").first, tc.ba);
+    }
+}
+
 // The whole ScheduleOne loop with the CPU plugins (16-worker Parallelizer for config 2, 4 for config
 // 4) on spec/synth.md clusters built as k8s objects, pod by pod against the oracle.
-static void cpu_loop_parity(int config, uint32_t n, uint32_t p, int workers) {
+static void cpu_loop_parity(int config, uint32_t n, uint32_t p, int workers, const qs_config *over = nullptr) {
     const uint64_t seed = 0x5EED0000ull + (uint64_t)config;
     std::vector<Node> nodes;
     std::vector<Pod> pods;
     synth_objects(config, seed, n, p, &nodes, &pods);
-    const qs_config cfg = default_cfg(config == 4, config == 4);
+    const qs_config cfg = over ? *over : default_cfg(config == 4, config == 4);
     Scheduler sched(CPURegistry(cfg), CPUProfiles(cfg), CPUProfileOf, workers);
     for (const auto &x : nodes) sched.AddNode(x);
     for (const auto &x : pods) sched.AddPod(x);
@@ -425,7 +501,7 @@ static void cpu_loop_parity(int config, uint32_t n, uint32_t p, int workers) {
     or_pods op{p, prc.data(), prm.data(), pre.data(), pzc.data(), pzm.data(), pq.data(), ppr.data(), pth.data(),
                pts.data(), psel.data(), pnr.data(), pnp.data(), prt.data(), ppt.data(), ppw.data(), nullptr, nullptr};
     or_generate(config, seed, &on, &op);
-    or_config oc{1, 1, {1, 2, 3}, {1, 1, 1}, 3, 2, cfg.enable_taint, cfg.enable_affinity, 0, 1};
+    const or_config oc = oracle_cfg(cfg);
     std::vector<int32_t> oracle(p);
     or_schedule(&oc, &on, &op, oracle.data(), nullptr, nullptr, 4);
     int diff = 0, unsched = 0;
@@ -433,13 +509,18 @@ static void cpu_loop_parity(int config, uint32_t n, uint32_t p, int workers) {
         diff += loop[j] != oracle[j];
         unsched += loop[j] < 0;
     }
-    std::printf("  CPU plugins, config %d: %u pods on %u nodes (%d workers), %d unschedulable, %d differ from the oracle\n",
-                config, p, n, workers, unsched, diff);
+    std::printf("  CPU plugins, config %d%s: %u pods on %u nodes (%d workers), %d unschedulable, %d differ from the oracle\n",
+                config, cfg.n_fit_resources ? " (gpu scoring resources)" : "", p, n, workers, unsched, diff);
     CHECK_EQ(diff, 0);
     if (config == 4) CHECK(unsched > 0 && unsched < (int)p);
 }
+static void test_cpu_loop_config1() { cpu_loop_parity(1, 100, 1000, 16); }  // BASELINE configs[0] at its size
 static void test_cpu_loop_config2() { cpu_loop_parity(2, 300, 9000, 16); }
 static void test_cpu_loop_config4() { cpu_loop_parity(4, 400, 9000, 4); }
+static void test_cpu_loop_config4_gpu_scoring() {
+    const qs_config c = gpu_scoring_cfg(true, true);
+    cpu_loop_parity(4, 400, 6000, 4, &c);
+}
 
 int main(int argc, char **argv) {
     const bool gpu = argc > 1 && std::strcmp(argv[1], "--gpu") == 0;
@@ -448,8 +529,12 @@ int main(int argc, char **argv) {
         cases = {{"quantity", test_quantity}, {"tolerations", test_tolerations},
                  {"requirements", test_requirements}, {"interner", test_interner},
                  {"pod_resources", test_pod_resources}, {"qos_sort_fit_error", test_qos_sort_and_fit_error},
-                 {"cpu_plugin_scores", test_cpu_plugin_scores}, {"cpu_loop_config2", test_cpu_loop_config2},
-                 {"cpu_loop_config4", test_cpu_loop_config4}};
+                 {"parallelizer_exceptions", test_parallelizer_exceptions},
+                 {"cpu_plugin_scores", test_cpu_plugin_scores},
+                 {"cpu_plugin_scores_resource_lists", test_cpu_plugin_scores_resource_lists},
+                 {"cpu_loop_config1", test_cpu_loop_config1}, {"cpu_loop_config2", test_cpu_loop_config2},
+                 {"cpu_loop_config4", test_cpu_loop_config4},
+                 {"cpu_loop_config4_gpu_scoring", test_cpu_loop_config4_gpu_scoring}};
     } else {
         cases = {{"gpu_least_allocated", test_gpu_least_allocated}, {"gpu_balanced", test_gpu_balanced},
                  {"gpu_fit_filter", test_gpu_fit_filter}, {"gpu_taint_affinity_scores", test_gpu_taint_affinity_scores},

@@ -66,7 +66,7 @@ def test_config_default():
     lib = qsched.load()
     c = _abi.QsConfig()
     lib.qs_config_default(ctypes.byref(c))
-    assert c.abi_version == 2 and list(c.w_fit) == [1, 2, 3] and list(c.w_bal) == [1, 1, 1]
+    assert c.abi_version == 3 and list(c.w_fit) == [1, 2, 3] and list(c.w_bal) == [1, 1, 1]
     assert c.w_taint == 3 and c.w_affinity == 2 and c.qos_sort == 1
     assert c.fit_weight_cpu == 1 and c.fit_weight_mem == 1
 

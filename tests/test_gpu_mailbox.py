@@ -15,13 +15,15 @@ pytestmark = pytest.mark.gpu
 CFG4 = dict(enable_taint=1, enable_affinity=1)
 
 
-def _rank(rank, world, qin, qout, cfg, config, n, p, resident="1", delay=0.0, wide=False):
+def _rank(rank, world, qin, qout, cfg, config, n, p, resident="1", delay=0.0, wide=False, skew=False):
     import sys
     import os
     import time
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [root, os.path.join(root, "custom-k8s-scheduler_amd")]
     os.environ["QS_RESIDENT"] = resident
+    if skew and rank == 1:  # this rank's selectors of windows 40-43 run 3 ms late (mid-stream drift)
+        os.environ["QS_INJECT_FAULT"] = "resident_skew"
     import qsched
     import torch
 
@@ -58,13 +60,13 @@ def make_cluster(qsched, config, n, p, wide=False):
     return nodes, pods
 
 
-def run_world(world, cfg, config, n, p, resident="1", delay=0.0, wide=False):
+def run_world(world, cfg, config, n, p, resident="1", delay=0.0, wide=False, skew=False):
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     qout = ctx.Queue()
     qins = [ctx.Queue() for _ in range(world)]
-    procs = [ctx.Process(target=_rank, args=(r, world, qins[r], qout, cfg, config, n, p, resident, delay, wide))
+    procs = [ctx.Process(target=_rank, args=(r, world, qins[r], qout, cfg, config, n, p, resident, delay, wide, skew))
              for r in range(world)]
     for pr in procs:
         pr.start()
@@ -88,23 +90,32 @@ def run_world(world, cfg, config, n, p, resident="1", delay=0.0, wide=False):
     return results
 
 
-@pytest.mark.parametrize("cfg,config,n,p,resident,delay,wide",
-                         [({}, 2, 3000, 12000, "1", 0.0, False), ({}, 2, 3000, 12000, "0", 0.0, False),
-                          ({}, 3, 12000, 20000, "1", 0.0, False), (CFG4, 4, 2000, 6000, "1", 0.0, False),
-                          (CFG4, 4, 400, 9000, "1", 0.0, False), (CFG4, 4, 2000, 6000, "0", 0.0, False),
-                          ({}, 2, 3000, 12000, "1", 1.0, False), ({}, 2, 3000, 9000, "1", 0.0, True)],
+GPU_SCORING = dict(fit_resources=[("cpu", 1), ("memory", 1), ("ext0", 5)], balanced_resources=["cpu", "memory", "ext0"])
+
+
+@pytest.mark.parametrize("cfg,config,n,p,resident,delay,wide,skew",
+                         [({}, 2, 3000, 12000, "1", 0.0, False, False), ({}, 2, 3000, 12000, "0", 0.0, False, False),
+                          ({}, 3, 12000, 20000, "1", 0.0, False, False), (CFG4, 4, 2000, 6000, "1", 0.0, False, False),
+                          (CFG4, 4, 400, 9000, "1", 0.0, False, False), (CFG4, 4, 2000, 6000, "0", 0.0, False, False),
+                          ({}, 2, 3000, 12000, "1", 1.0, False, False), ({}, 2, 3000, 9000, "1", 0.0, True, False),
+                          (CFG4, 4, 2000, 12000, "1", 0.0, False, True), ({}, 2, 3000, 12000, "1", 0.0, False, True),
+                          (dict(CFG4, **GPU_SCORING), 4, 2000, 8000, "1", 0.0, False, False)],
                          ids=["config2-resident", "config2-per-window", "config3-resident", "config4-resident",
-                              "config4-tight-resident", "config4-per-window", "config2-late-rank", "wide-resident"])
-def test_mailbox_world2_two_processes(oracle, cfg, config, n, p, resident, delay, wide):
+                              "config4-tight-resident", "config4-per-window", "config2-late-rank", "wide-resident",
+                              "config4-skewed-rank", "config2-skewed-rank", "config4-gpu-scoring-resident"])
+def test_mailbox_world2_two_processes(oracle, cfg, config, n, p, resident, delay, wide, skew):
     """Every profile runs the SHARDED RESIDENT stream by default (each rank's
     selectors score its node range and exchange every pod's shard list — and, for TaintToleration /
     NodeAffinity, its partial maxima — through the peers' mailboxes inside the one launch);
     QS_RESIDENT=0 keeps the per-window mailbox exchange.  late-rank: rank 1 enters its run 1 s after
-    rank 0 (the first window's waits are bounded at 5 s); wide: the f64 memory layout."""
+    rank 0 (the first window's waits are bounded at 5 s); skewed-rank: rank 1's selectors
+    of windows 40-43 start 3 ms late, in the middle of the run (the slot-reuse argument and the
+    exact-tag checks of the list and partial-maxima exchanges); wide: the f64 memory
+    layout; gpu-scoring: configurable scoring resources (spec S5)."""
     from qsched import pods_from_struct
     import qsched
 
-    res = run_world(2, cfg, config, n, p, resident, delay, wide)
+    res = run_world(2, cfg, config, n, p, resident, delay, wide, skew)
     nodes, pods = make_cluster(qsched, config, n, p, wide)
     on = {k: v.copy() for k, v in nodes.items()}
     o_pl, o_keys, _ = oracle.schedule(on, pods_from_struct(pods), cfg, nthreads=16)

@@ -174,3 +174,33 @@ def test_resident_stream_second_timeout_sticks(monkeypatch):
             st.free()
             assert np.array_equal(pl, o) and np.array_equal(keys, ok)
     assert seen == ["timeout", "per-window", "timeout", "per-window", "per-window"], seen
+
+
+def test_resident_timeouts_apart_do_not_stick(monkeypatch):
+    """Only CONSECUTIVE resident timeouts keep per-window launches: timeout, per-window,
+    a resident run that succeeds, a second timeout, then per-window once and resident again."""
+    nodes, pods = synth_generate(2, 3000, 6000)
+    on = {k: v.copy() for k, v in nodes.items()}
+    o, ok, _ = O.schedule(on, pods_from_struct(pods), nthreads=16)
+    seen = []
+    with Scheduler({"engine": "lookahead"}) as s:
+        plan = ["resident_stall", None, None, "resident_stall_always", None, None]
+        for inj in plan:
+            if inj:
+                monkeypatch.setenv("QS_INJECT_FAULT", inj)
+            else:
+                monkeypatch.delenv("QS_INJECT_FAULT", raising=False)
+            s.load_nodes(nodes)
+            st = s.prepare(pods)
+            try:
+                stats = st.run()
+            except QschedError as e:
+                assert "resident lookahead stream timed out" in str(e)
+                seen.append("timeout")
+                st.free()
+                continue
+            seen.append("resident" if stats["resident"] else "per-window")
+            pl, keys = st.results()
+            st.free()
+            assert np.array_equal(pl, o) and np.array_equal(keys, ok)
+    assert seen == ["timeout", "per-window", "resident", "timeout", "per-window", "resident"], seen

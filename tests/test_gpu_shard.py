@@ -20,7 +20,7 @@ from test_gpu_parity import assert_same, run_oracle  # noqa: E402
 
 
 def run_sharded(nodes, pods, cfg, shard=None):
-    with Scheduler(dict(cfg, engine="lookahead"), shard=shard) as s:
+    with Scheduler(dict({"engine": "lookahead"}, **cfg), shard=shard) as s:
         s.load_nodes(nodes)
         st = s.prepare(pods)
         stats = st.run()
@@ -81,3 +81,32 @@ def test_config4_rccl_one_rank(oracle):
     g = run_sharded(nodes, pods, CFG4, shard=(0, 1, dist_unique_id()))
     o = run_oracle(oracle, nodes, pods, CFG4)
     assert_same(g[:2], o[:2], g[2], o[2])
+
+
+@pytest.mark.parametrize("config,n,p,prof", [(2, 3000, 3000, {}), (3, 20000, 1500, {}), (4, 2000, 2000, "norm"),
+                                             (4, 2500, 2000, "gpu-scoring")])
+def test_allreduce_engine_one_rank(oracle, config, n, p, prof):
+    """QS_ENGINE_ALLREDUCE (the as-is RCCL baseline): per pod the rank scans its
+    node shard and one ncclAllReduce(u64 max) of the packed key decides (two u32 max all-reduces of
+    the normalize maxima first for TaintToleration / NodeAffinity); at world 1 with a one-rank
+    communicator, bit-exact vs the oracle, placements, keys and the final table."""
+    from test_gpu_parity import CFG4
+    from rescfg import GPU_CFG
+    cfg = {} if not prof else (CFG4 if prof == "norm" else dict(CFG4, **GPU_CFG))
+    nodes, pods = synth_generate(config, n, p)
+    g = run_sharded(nodes, pods, dict(cfg, engine="allreduce"), shard=(0, 1, dist_unique_id()))
+    assert g[3]["engine_used"] == "allreduce"
+    o = run_oracle(oracle, nodes, pods, cfg)
+    assert_same(g[:2], o[:2], g[2], o[2])
+
+
+def test_allreduce_engine_needs_a_communicator():
+    """Without an RCCL communicator the per-pod all-reduce engine refuses to run (QS_ESTATE)."""
+    from qsched import QschedError, Scheduler
+    nodes, pods = synth_generate(2, 500, 200)
+    with Scheduler({"engine": "allreduce"}) as s:
+        s.load_nodes(nodes)
+        st = s.prepare(pods)
+        with pytest.raises(QschedError, match="RCCL communicator"):
+            st.run()
+        st.free()

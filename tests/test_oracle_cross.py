@@ -11,6 +11,7 @@ from hypothesis import HealthCheck, given, settings
 from hypothesis import strategies as st
 
 from oracle import oracle as O
+from rescfg import add_ext1, random_resource_cfg
 
 MIB, GIB = 1 << 20, 1 << 30
 
@@ -63,6 +64,24 @@ def test_c_oracle_equals_python_oracle(seed, n, p, features, qos_sort):
     assert [int(x) for x in best_c] == best_p
     for k in n1:
         assert np.array_equal(n1[k], n2[k])
+
+
+@settings(max_examples=60, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(seed=st.integers(0, 2**32 - 1), n=st.integers(1, 20), p=st.integers(0, 50), features=st.booleans())
+def test_c_oracle_equals_python_oracle_resource_lists(seed, n, p, features):
+    """Random LeastAllocated / Balanced resource lists (spec S5 "Scoring resources"), two extended
+    resource columns, both oracles bit for bit."""
+    rng = np.random.default_rng(seed)
+    nodes, pods = random_cluster(rng, n, p, True)
+    add_ext1(rng, nodes, pods)
+    nodes["req_ext"][:, 0] = np.minimum(nodes["alloc_ext"][:, 0], rng.integers(0, 3, n))
+    cfg = dict(O.DEFAULT_CONFIG, **random_resource_cfg(rng), **(CFG_FEATURES if features else {}))
+    n1, _ = O.copy_cluster(nodes, pods)
+    n2, _ = O.copy_cluster(nodes, pods)
+    pl_c, best_c, _ = O.schedule(n1, pods, cfg)
+    pl_p, best_p = O.py_schedule(n2, pods, cfg)
+    assert pl_c.tolist() == pl_p
+    assert [int(x) for x in best_c] == best_p
 
 
 def test_openmp_arm_matches_sequential():

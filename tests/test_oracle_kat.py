@@ -3,6 +3,9 @@
 The reference has no tests (parity unpinned); these hand-computed cases are what pins both oracle
 restatements (C: oracle/qs_oracle.c, Python: oracle/oracle.py py_*).
 """
+import ctypes
+import math
+
 import numpy as np
 import pytest
 
@@ -122,3 +125,92 @@ def test_qos_weights_change_the_winner():
 def test_spec_defaults_match_upstream_profile():
     assert O.DEFAULT_CONFIG["w_tt"] == 3 and O.DEFAULT_CONFIG["w_na"] == 2
     assert O.DEF_CPU == 100 and O.DEF_MEM == 209715200
+
+
+# ---- configurable scoring resources (spec/kat.md K10-K15, spec S5 "Scoring resources") ----------
+def _v(vals):
+    return (ctypes.c_int64 * len(vals))(*vals)
+
+
+def la_v(alloc, reqd, w):
+    return O.lib().or_least_allocated_v(len(alloc), _v(alloc), _v(reqd), _v(w))
+
+
+def ba_v(alloc, reqd):
+    return O.lib().or_balanced_v(len(alloc), _v(alloc), _v(reqd))
+
+
+KAT_RES = [
+    # name, alloc, reqd (after the pod), weights (None: Balanced only), LA, BA
+    ("K10", (8000, 32 * GIB, 8), (4000, 16 * GIB, 6), (1, 1, 5), 32, 88),
+    ("K10b", (8000, 32 * GIB, 0), (4000, 16 * GIB, 0), (1, 1, 5), 50, 100),
+    ("K12", (4000, 10 * GIB, 5), (3200, 8 * GIB, 4), (1, 1, 1), 20, 99),
+    ("K15", (4000, 10, 8, 4), (2000, 5, 9, 4), (1, 1, 1, 1), 25, 75),
+]
+
+
+@pytest.mark.parametrize("name,alloc,reqd,w,la,ba", KAT_RES)
+def test_kat_resource_lists(name, alloc, reqd, w, la, ba):
+    assert la_v(alloc, reqd, w) == la
+    assert O.py_least_allocated(alloc, reqd, w) == la
+    assert ba_v(alloc, reqd) == ba
+    assert O.py_balanced(alloc, reqd) == ba
+
+
+def test_three_resource_float64_sentinel():
+    # K12: three equal fractions 4/5; the float64 mean is not 0.8, so std > 0 and the score is 99
+    f = [3200 / 4000, (8 * GIB) / (10 * GIB), 4 / 5]
+    mean = (f[0] + f[1] + f[2]) / 3
+    assert mean == 0.8000000000000002
+    s = 0.0
+    for x in f:
+        s = s + (x - mean) * (x - mean)
+    assert (1 - math.sqrt(s / 3)) * 100.0 == 99.99999999999999
+    assert ba_v((4000, 10 * GIB, 5), (3200, 8 * GIB, 4)) == 99  # exact arithmetic: 100
+
+
+def _k10_cluster(gpu_req=4):
+    nodes, pods = O.empty_cluster(1, 1)
+    nodes["alloc_cpu"][0], nodes["alloc_mem"][0], nodes["alloc_ext"][0, 0] = 8000, 32 * GIB, 8
+    nodes["max_pods"][0] = 110
+    nodes["req_cpu"][0] = nodes["nz_cpu"][0] = 2000
+    nodes["req_mem"][0] = nodes["nz_mem"][0] = 8 * GIB
+    nodes["req_ext"][0, 0] = 2
+    nodes["pods"][0] = 1
+    pods["req_cpu"][0] = pods["nz_cpu"][0] = 2000
+    pods["req_mem"][0] = pods["nz_mem"][0] = 8 * GIB
+    pods["req_ext"][0, 0] = gpu_req
+    pods["qos"][0] = 2
+    return nodes, pods
+
+
+@pytest.mark.parametrize("gpu_req,la,ba", [(4, 32, 88), (0, 50, 100)])
+def test_kat_k10_k11_through_score_pod(gpu_req, la, ba):
+    """K10 / K10b / K11 through the whole per-node evaluation of both oracles."""
+    nodes, pods = _k10_cluster(gpu_req)
+    cfg = dict(fit_resources=[("cpu", 1), ("memory", 1), ("ext0", 5)],
+               balanced_resources=["cpu", "memory", "ext0"])
+    keys, scores = O.score_pod(nodes, pods, 0, cfg)
+    assert list(scores[0][:2]) == [la, ba]
+    c = dict(O.DEFAULT_CONFIG, **cfg)
+    assert O.py_keys(nodes, pods, 0, c) == [int(keys[0])]
+    assert int(keys[0]) >> 32 == 3 * la + ba + 1  # Guaranteed: w_fit 3, w_bal 1
+
+
+def test_kat_k13_k14_lists():
+    # K13: gpu in the Balanced list but not requested -> the two-resource (K7) path
+    nodes, pods = _k10_cluster(0)
+    nodes["alloc_cpu"][0], nodes["alloc_mem"][0] = 4000, 25 * GIB
+    for f in ("req_cpu", "req_mem", "nz_cpu", "nz_mem", "pods"):
+        nodes[f][0] = 0
+    pods["req_cpu"][0] = pods["nz_cpu"][0] = 2000
+    pods["req_mem"][0] = pods["nz_mem"][0] = 17 * GIB
+    _, sc = O.score_pod(nodes, pods, 0, dict(balanced_resources=["cpu", "memory", "ext0"]))
+    assert sc[0][1] == 90
+    # K14: LeastAllocated over memory only; BestEffort pod (non-zero defaults)
+    nodes["alloc_cpu"][0], nodes["alloc_mem"][0] = 4000, 10 * GIB
+    nodes["nz_mem"][0] = 5 * GIB
+    pods["req_cpu"][0] = pods["req_mem"][0] = 0
+    pods["nz_cpu"][0], pods["nz_mem"][0], pods["qos"][0] = 100, 200 * MIB, 0
+    _, sc = O.score_pod(nodes, pods, 0, dict(fit_resources=[("memory", 1)], balanced_resources=["cpu"]))
+    assert sc[0][0] == 48 and sc[0][1] == 100  # one Balanced fraction -> std 0

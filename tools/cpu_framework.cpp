@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "../custom-k8s-scheduler_amd/host/cpu_plugins.hpp"
+#include "oracle_cfg.hpp"
 #include "synth_objects.hpp"
 extern "C" {
 #include "../oracle/qs_oracle.h"
@@ -61,9 +62,8 @@ int main(int argc, char **argv) {
                pts.data(), psel.data(), pnr.data(), pnp.data(), prt.data(), ppt.data(), ppw.data(), papp.data(),
                paa.data()};
     or_generate(config, seed, &on, &op);
-    or_config oc{cfg.fit_weight_cpu, cfg.fit_weight_mem, {cfg.w_fit[0], cfg.w_fit[1], cfg.w_fit[2]},
-                 {cfg.w_bal[0], cfg.w_bal[1], cfg.w_bal[2]}, cfg.w_taint, cfg.w_affinity, cfg.enable_taint,
-                 cfg.enable_affinity, cfg.balanced_skip_besteffort, 1};
+    or_config oc = oracle_cfg(cfg);
+    oc.qos_sort = 1;
     std::vector<int32_t> ref(p);
     or_schedule(&oc, &on, &op, ref.data(), nullptr, nullptr, 16);
     int diff = 0, unsched = 0;

@@ -17,6 +17,7 @@
 extern "C" {
 #include "../oracle/qs_oracle.h"
 }
+#include "oracle_cfg.hpp"
 
 static qs_ctx *g_ctx = nullptr;
 static qs_ctx *ctx_of() { return g_ctx; }
@@ -97,7 +98,10 @@ int main(int argc, char **argv) {
                pts.data(), psel.data(), pnr.data(), pnp.data(), prt.data(), ppt.data(), ppw.data(), papp.data(),
                paa.data()};
     or_generate(2, 0x5EED0002ull, &on, &op);
-    or_config oc{1, 1, {1, 2, 3}, {1, 1, 1}, 3, 2, 0, 0, 0, 0};
+    qs_config dcfg;
+    qs_config_default(&dcfg);
+    dcfg.qos_sort = 0;
+    const or_config oc = oracle_cfg(dcfg);
     std::vector<int32_t> ref(p);
     or_schedule(&oc, &on, &op, ref.data(), nullptr, nullptr, 16);
     const bool match = std::equal(ref.begin(), ref.end(), placement.begin());
