@@ -92,6 +92,8 @@ struct qs_stream {
     std::vector<uint32_t> order;   // stream position -> arrival index
     qs_host::DevBuf d_pods, d_podx, d_node, d_key, d_stamp;
     bool ran = false;
+    int mode_ran = -1;        // qs_mode of the last run
+    uint64_t epoch_after = 0;  // the context's table epoch right after the last run (FitError replay)
     int shift = 0;
     bool wide = false;  // pod records are DPodW (the table's wide layout) when set
     // LOOKAHEAD window sequence as an instantiated HIP graph, valid while gkey matches
@@ -104,6 +106,7 @@ struct qs_stream {
 
 struct qs_ctx {
     std::mutex mu;
+    uint64_t table_epoch = 0;  // bumped by every change of the node table (load, upsert, Reserve, restore, run)
     qs_config cfg{};
     int device = 0;
     hipStream_t stream = nullptr;   // resolve chain, copies, single-kernel engines

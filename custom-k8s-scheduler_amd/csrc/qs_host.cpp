@@ -25,6 +25,9 @@
 #include <new>
 #include <string>
 #include <vector>
+#include <functional>
+#include <condition_variable>
+#include <thread>
 
 #include "qs_ctx.hpp"
 
@@ -907,6 +910,7 @@ qs_status qs_nodes_load(qs_ctx *c, const qs_node_soa *nd, uint32_t n) {
         c->dev_valid = false;
         c->saved = false;
         c->mirror_stale = false;
+        ++c->table_epoch;
         upload_table(c);
     });
 }
@@ -966,6 +970,7 @@ qs_status qs_node_upsert(qs_ctx *c, uint32_t idx, const qs_node_row *r, uint64_t
             c->saved = false;
         }
         put_row(m, idx, snap_row(one, 0));
+        ++c->table_epoch;
         // the new row's memory may need a finer unit or the wide layout (re-upload), else one row
         const int want = std::min({ctz64(r->alloc_mem), ctz64(r->req_mem), ctz64(r->nz_mem)});
         const bool was_valid = c->dev_valid;
@@ -985,6 +990,7 @@ static qs_status reserve_impl(qs_ctx *c, uint32_t node, const qs_pod *p, int sig
         sync_mirror(c);
         const RowSnap before = snap_row(c->m, node);
         mirror_reserve(c->m, node, *p, sign);
+        ++c->table_epoch;
         // any failure from here on (a column driven negative, a layout the stream's growth
         // projection rejects, a device error while pushing the row) leaves the mirror as it was:
         // the caller was told the reservation failed
@@ -1074,6 +1080,63 @@ static void unpack_base(const uint32_t *pk, uint32_t n, const uint32_t w[4], uin
                         int32_t *total) {
     unpack_body(pk, n, w, feas, score, total);
 }
+// Large tables widen in parallel: a few helper threads (spinning ~50 us for the next call, then
+// sleeping) take equal node ranges (multiples of 16) beside the calling thread (round 5: 50,000
+// nodes, every output, was ~20 us of widening on one core).
+class UnpackPool {
+   public:
+    static UnpackPool &get() {
+        // never destroyed: its detached helpers may be blocked on cv_ at process exit, and
+        // destroying a condition variable with waiters hangs the exit (glibc)
+        static UnpackPool *p = new UnpackPool;
+        return *p;
+    }
+    int parts() const { return (int)th_.size() + 1; }
+    // fn(part) for part in [0, parts()); the caller runs part 0
+    void run(const std::function<void(int)> &fn) {
+        std::lock_guard<std::mutex> one(run_mu_);  // contexts in different threads take turns
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            fn_ = &fn;
+            left_.store((int)th_.size(), std::memory_order_relaxed);
+            gen_.fetch_add(1, std::memory_order_release);
+        }
+        cv_.notify_all();
+        fn(0);
+        while (left_.load(std::memory_order_acquire) != 0) std::this_thread::yield();
+    }
+
+   private:
+    UnpackPool() {
+        const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+        const int helpers = (int)std::min(3u, hw > 1 ? hw - 1 : 0u);
+        for (int k = 0; k < helpers; ++k) th_.emplace_back([this, k] { loop(k + 1); });
+        for (auto &t : th_) t.detach();  // process lifetime (no join at static destruction)
+    }
+    void loop(int part) {
+        uint64_t seen = 0;
+        for (;;) {
+            const auto t0 = std::chrono::steady_clock::now();
+            while (gen_.load(std::memory_order_acquire) == seen &&
+                   std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(50))
+                std::this_thread::yield();
+            if (gen_.load(std::memory_order_acquire) == seen) {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return gen_.load(std::memory_order_acquire) != seen; });
+            }
+            seen = gen_.load(std::memory_order_acquire);
+            (*fn_)(part);
+            left_.fetch_sub(1, std::memory_order_acq_rel);
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_, run_mu_;
+    std::condition_variable cv_;
+    std::atomic<uint64_t> gen_{0};
+    std::atomic<int> left_{0};
+    const std::function<void(int)> *fn_ = nullptr;
+};
+
 static void unpack_scores(const uint32_t *pk, uint32_t n, const uint32_t w[4], uint8_t *feas, int32_t *score,
                           int32_t *total) {
     using Fn = void (*)(const uint32_t *, uint32_t, const uint32_t *, uint8_t *, int32_t *, int32_t *);
@@ -1086,7 +1149,23 @@ static void unpack_scores(const uint32_t *pk, uint32_t n, const uint32_t w[4], u
 #endif
         return (Fn)unpack_base;
     }();
-    fn(pk, n, w, feas, score, total);
+    static const uint32_t par_min = [] {
+        const char *e = getenv("QS_UNPACK_PAR_MIN");  // nodes from which the widening runs in parallel
+        return e ? (uint32_t)std::max(0, atoi(e)) : 16384u;
+    }();
+    if (n < par_min || (!score && !total) || UnpackPool::get().parts() < 2) {
+        fn(pk, n, w, feas, score, total);
+        return;
+    }
+    UnpackPool &pool = UnpackPool::get();
+    const uint32_t parts = (uint32_t)pool.parts();
+    const uint32_t per = ((n + parts - 1) / parts + 15) & ~15u;
+    pool.run([&](int part) {
+        const uint32_t b = std::min(n, (uint32_t)part * per), e = std::min(n, b + per);
+        if (b < e)
+            fn(pk + b, e - b, w, feas ? feas + b : nullptr, score ? score + 4 * (size_t)b : nullptr,
+               total ? total + b : nullptr);
+    });
 }
 
 // The one-launch score of one pod into the context's pinned buffer: pod by value,
@@ -1705,6 +1784,8 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
         // the timed region): a later device fault rebuilds the table from it
         sync_mirror(c);
         s->ran = true;
+        s->mode_ran = (int)mode;
+        s->epoch_after = ++c->table_epoch;
         if (stats) {
             std::memset(stats, 0, sizeof(*stats));
             for (int k = 0; k < 4; k++) {
@@ -1775,6 +1856,7 @@ qs_status qs_table_restore(qs_ctx *c) {
         HIPCHK(hipMemcpyAsync(c->tbl.p, c->tbl_saved.p, c->tbl.bytes, hipMemcpyDeviceToDevice, c->stream));
         c->m = c->m_saved;        // the mirror of the snapshot
         c->mirror_stale = false;
+        ++c->table_epoch;
         c->soa_valid = false;     // the SoA copy is rebuilt from the restored rows on demand
     });
 }
@@ -1820,6 +1902,71 @@ size_t qs_struct_size(int which) {
         case 5: return sizeof(qs_stats);
         default: return 0;
     }
+}
+
+// FitError diagnosis (UP framework/types.go#FitError): the table at each requested pod's turn is the
+// run's initial table (the final mirror minus every placed pod's delta) plus the deltas of the pods
+// placed before it in stream order; each node's reasons follow spec S4/S5's filters in upstream's
+// default order, NodeResourcesFit listing every insufficient resource (UP fit.go#fitsRequest).
+qs_status qs_stream_fit_errors(qs_ctx *c, qs_stream *s, const uint32_t *pods, uint32_t mreq, uint32_t *counts) {
+    return guarded(c, [&] {
+        if (!s || !s->ran) fail(QS_ESTATE, "stream has not run");
+        if (s->mode_ran != QS_MODE_EXACT) fail(QS_EINVAL, "FitError diagnosis covers exact streams");
+        if (s->epoch_after != c->table_epoch) fail(QS_ESTATE, "the node table changed after the stream's run");
+        if (mreq && (!pods || !counts)) fail(QS_EINVAL, "null pods / counts");
+        const uint32_t P = s->p;
+        for (uint32_t q = 0; q < mreq; q++)
+            if (pods[q] >= P) fail(QS_EINVAL, "pod index out of range");
+        std::memset(counts, 0, sizeof(uint32_t) * QS_FIT_REASONS * (size_t)mreq);
+        if (!mreq) return;
+        HIPCHK(hipSetDevice(c->device));
+        sync_mirror(c);
+        std::vector<int32_t> node(P);
+        if (P) HIPCHK(hipMemcpy(node.data(), s->d_node.p, 4 * (size_t)P, hipMemcpyDeviceToHost));
+        // stream position -> requested slots (a pod may be requested twice)
+        std::vector<std::vector<uint32_t>> want(P);
+        std::vector<uint32_t> pos_of(P);
+        for (uint32_t k = 0; k < P; k++) pos_of[s->order[k]] = k;
+        for (uint32_t q = 0; q < mreq; q++) want[pos_of[pods[q]]].push_back(q);
+        Mirror m = c->m;
+        for (uint32_t k = 0; k < P; k++)
+            if (node[k] >= 0) mirror_reserve(m, (uint32_t)node[k], s->pods[s->order[k]], -1);
+        const bool taint = c->cfg.enable_taint != 0, aff = c->cfg.enable_affinity != 0;
+        auto subset = [](const uint64_t *mask, const uint64_t *bits) {
+            return (mask[0] & ~bits[0]) == 0 && (mask[1] & ~bits[1]) == 0;
+        };
+        for (uint32_t k = 0; k < P; k++) {
+            const qs_pod &p = s->pods[s->order[k]];
+            if (node[k] < 0 && !want[k].empty()) {
+                uint32_t cnt[QS_FIT_REASONS] = {0};
+                const bool any_req = p.req_cpu || p.req_mem || p.req_ext[0] || p.req_ext[1];
+                for (uint32_t i = 0; i < m.n; i++) {
+                    if (taint && (m.th[i] & ~p.tol_hard) != 0) { ++cnt[QS_FIT_TAINT]; continue; }
+                    if (aff) {
+                        const uint64_t *lb = &m.lb[2 * (size_t)i];
+                        bool ok = subset(p.sel, lb);
+                        if (ok && p.n_req_terms > 0) {
+                            bool one = false;
+                            for (int t = 0; t < p.n_req_terms; t++) one = one || subset(p.req_terms[t], lb);
+                            ok = one;
+                        }
+                        if (!ok) { ++cnt[QS_FIT_AFFINITY]; continue; }
+                    }
+                    if (m.np[i] + 1 > m.mp[i]) ++cnt[QS_FIT_TOO_MANY_PODS];
+                    if (!any_req) continue;
+                    if (p.req_cpu > 0 && p.req_cpu > m.ac[i] - m.rc[i]) ++cnt[QS_FIT_CPU];
+                    if (p.req_mem > 0 && p.req_mem > m.am[i] - m.rm[i]) ++cnt[QS_FIT_MEMORY];
+                    for (int e = 0; e < QS_MAX_EXT; e++) {
+                        const int64_t q = p.req_ext[e];
+                        if (q != 0 && q > m.ae[(size_t)i * QS_MAX_EXT + e] - m.re[(size_t)i * QS_MAX_EXT + e])
+                            ++cnt[QS_FIT_EXT0 + e];
+                    }
+                }
+                for (uint32_t q : want[k]) std::memcpy(counts + (size_t)q * QS_FIT_REASONS, cnt, sizeof cnt);
+            }
+            if (node[k] >= 0) mirror_reserve(m, (uint32_t)node[k], p, +1);
+        }
+    });
 }
 
 qs_status qs_stream_stamps(qs_ctx *c, qs_stream *s, uint64_t *stamps) {

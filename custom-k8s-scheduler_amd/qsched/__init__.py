@@ -19,11 +19,11 @@ import numpy as np
 
 from ._abi import (ENGINES, ENGINE_NAMES, EXPORTED, LIB_PATH, POD_DTYPE, QS_ABI_VERSION,
                    QS_MAX_EXT, QS_MAX_SCORE_RES, QS_MAX_TERMS, QS_MODE_BATCHED, QS_MODE_EXACT, QS_OK,
-                   RESOURCES, QschedError,
+                   RESOURCES, FIT_REASONS, QschedError,
                    QschedLibraryMissing, QsConfig, QsContainer, QsNodeRow, QsNodeSoa, QsStats,
                    load)
 
-__all__ = ["Scheduler", "Config", "POD_DTYPE", "pods_to_struct", "pods_from_struct",
+__all__ = ["Scheduler", "Config", "POD_DTYPE", "pods_to_struct", "pods_from_struct", "fit_error_message",
            "synth_generate", "dist_unique_id", "empty_nodes", "pod_from_containers", "compute_qos", "load",
            "QschedError", "QschedLibraryMissing", "ENGINES", "EXPORTED", "LIB_PATH"]
 
@@ -294,6 +294,18 @@ class Stream:
         self.s._chk(self.s.lib.qs_stream_stamps(self.s.ctx, self.h, _ptr(out)))
         return out
 
+    def fit_errors(self, pods=None):
+        """qs_stream_fit_errors: per requested pod (arrival indices; default: every unschedulable
+        pod) the count of nodes per FitError reason column (FIT_REASONS), against the table at that
+        pod's turn.  Returns (indices, counts[m, 7])."""
+        if pods is None:
+            pl, _ = self.results()
+            pods = np.nonzero(pl < 0)[0]
+        idx = np.ascontiguousarray(pods, dtype=np.uint32)
+        counts = np.zeros((len(idx), len(FIT_REASONS)), np.uint32)
+        self.s._chk(self.s.lib.qs_stream_fit_errors(self.s.ctx, self.h, _ptr(idx), len(idx), _ptr(counts)))
+        return idx, counts
+
     def free(self):
         if self.h:
             self.s._chk(self.s.lib.qs_stream_free(self.s.ctx, self.h))
@@ -336,6 +348,15 @@ def _containers(containers):
                 setattr(arr[i], k, int(v))
                 setattr(arr[i], "has_" + k, 1)
     return arr
+
+
+def fit_error_message(counts, n_nodes, ext_names=("ext0", "ext1")):
+    """UP framework/types.go#FitError.Error() from one pod's reason counts: "0/N nodes are available:
+    <count> <reason>, ..." with the "count reason" strings sorted as Go's sort.Strings does."""
+    names = [r.format(ext0=ext_names[0], ext1=ext_names[1]) for r in FIT_REASONS]
+    parts = sorted(f"{int(c)} {names[k]}" for k, c in enumerate(counts) if c)
+    msg = f"0/{n_nodes} nodes are available:"
+    return msg + (f" {', '.join(parts)}." if parts else "")
 
 
 def pod_from_containers(containers, overhead=None):

@@ -267,6 +267,26 @@ QS_API qs_status qs_stream_results(qs_ctx *ctx, qs_stream *s, int32_t *placement
 QS_API qs_status qs_stream_free(qs_ctx *ctx, qs_stream *s);
 /* Per-pod device timestamps (100 MHz s_memrealtime ticks, stream order; record_timestamps = 1). */
 QS_API qs_status qs_stream_stamps(qs_ctx *ctx, qs_stream *s, uint64_t *stamps_p);
+/* FitError diagnosis of an exact stream's unschedulable pods (replaces UP framework/types.go#FitError,
+ * Diagnosis.NodeToStatusMap; the "0/N nodes are available: ..." message).  For each requested pod
+ * (arrival index) the number of nodes that rejected it for each reason, against the table as it
+ * stood when that pod was scheduled: the stream's device placements replayed over the host mirror.
+ * A node counts under the first failing filter in upstream's default order (TaintToleration,
+ * NodeAffinity, NodeResourcesFit) and, for NodeResourcesFit, under every insufficient resource
+ * (UP noderesources/fit.go#fitsRequest).  counts = m x QS_FIT_REASONS; a placed pod gets zeros.
+ * Call after qs_stream_run of an exact stream and before any other change to the table
+ * (QS_ESTATE otherwise). */
+typedef enum qs_fit_reason {
+    QS_FIT_TOO_MANY_PODS = 0, /* "Too many pods" */
+    QS_FIT_CPU = 1,           /* "Insufficient cpu" */
+    QS_FIT_MEMORY = 2,        /* "Insufficient memory" */
+    QS_FIT_EXT0 = 3,          /* "Insufficient <extended resource 0>" */
+    QS_FIT_EXT1 = 4,          /* "Insufficient <extended resource 1>" */
+    QS_FIT_TAINT = 5,         /* "node(s) had untolerated taint" */
+    QS_FIT_AFFINITY = 6,      /* "node(s) didn't match Pod's node affinity/selector" */
+    QS_FIT_REASONS = 7
+} qs_fit_reason;
+QS_API qs_status qs_stream_fit_errors(qs_ctx *ctx, qs_stream *s, const uint32_t *pods, uint32_t m, uint32_t *counts);
 
 /* ---- host helpers (spec S2/S3, spec/synth.md) ---- */
 QS_API qs_status qs_pod_from_containers(const qs_container *c, uint32_t nc, const int64_t *overhead_cpu_mem,
