@@ -115,6 +115,9 @@ struct DevCfg {
     // producers may be a peer rank still in host-side prepare (sharded: 5 s, as the per-window
     // mailbox wait, qs_dist.cpp); 0 = the 0.5 s bound of every later wait.
     uint64_t first_ticks;
+    // QS_RES_DIAG=1: the resident selectors time their phases too (extra barriers); =2: the
+    // resolver's counters only, selectors untouched
+    uint32_t sel_diag;
 };
 
 // Resolver prologue: thread 0 spins (s_sleep) until window s0/K's lists are published, then every

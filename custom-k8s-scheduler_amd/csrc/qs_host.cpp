@@ -1109,7 +1109,9 @@ class UnpackPool {
    private:
     UnpackPool() {
         const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-        const int helpers = (int)std::min(3u, hw > 1 ? hw - 1 : 0u);
+        const char *e = getenv("QS_UNPACK_THREADS");  // helper threads (default 7)
+        const unsigned want = e ? (unsigned)std::max(0, atoi(e)) : 7u;
+        const int helpers = (int)std::min(want, hw > 1 ? hw - 1 : 0u);
         for (int k = 0; k < helpers; ++k) th_.emplace_back([this, k] { loop(k + 1); });
         for (auto &t : th_) t.detach();  // process lifetime (no join at static destruction)
     }
@@ -1643,7 +1645,9 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                     // sharded: window 0's waits cover a peer still in host-side prepare (5 s)
                     dcr.first_ticks = c->world > 1 ? 500000000ull : 0ull;
                     // QS_RES_DIAG=1: the resolver's time split (list waits / window bodies / between)
-                    static const bool rdiag_on = getenv("QS_RES_DIAG") && getenv("QS_RES_DIAG")[0] == '1';
+                    static const bool rdiag_on = getenv("QS_RES_DIAG") && (getenv("QS_RES_DIAG")[0] == '1' ||
+                                                                             getenv("QS_RES_DIAG")[0] == '2');
+                    dcr.sel_diag = getenv("QS_RES_DIAG") && getenv("QS_RES_DIAG")[0] == '1' ? 1u : 0u;
                     uint64_t *rdiag = nullptr;
                     if (rdiag_on) {
                         c->diag.ensure(256);
@@ -1664,6 +1668,18 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                         const double nw = h[3] ? (double)h[3] : 1.0;
                         fprintf(stderr, "QS_RES_DIAG resolver %.3f us per window; windows whose lists were not prefetched %llu of %llu (selectors %u)\n",
                                 h[1] * 0.01 / nw, (unsigned long long)h[4], (unsigned long long)h[3], sel);
+                        if (h[2])
+                            fprintf(stderr, "QS_RES_DIAG selector 0: done seen %.2f us, its task finished %.2f us after "
+                                            "the resolver's start of the window it overlaps (%llu windows)\n",
+                                    h[13] * 0.01 / (double)h[2], h[14] * 0.01 / (double)h[2], (unsigned long long)h[2]);
+                        if (h[6])
+                            fprintf(stderr, "QS_RES_DIAG prefetch check: %llu windows short of lists, %.2f lists missing "
+                                            "on average\n", (unsigned long long)h[6], (double)h[5] / (double)h[6]);
+                        if (h[27] + h[28] + h[29] + h[30] + h[31])
+                            fprintf(stderr, "QS_RES_DIAG window boundary (ns per window, wave D): bookkeeping %.0f "
+                                            "-> B2 %.0f -> B3 %.0f -> B1 %.0f -> pod 0 decided %.0f\n",
+                                    h[27] * 10.0 / nw, h[28] * 10.0 / nw, h[29] * 10.0 / nw, h[30] * 10.0 / nw,
+                                    h[31] * 10.0 / nw);
                         if (h[19])
                             fprintf(stderr, "QS_RES_DIAG selector task (us): scoring %.2f chunk top-L %.2f publish/merge %.2f (tasks %llu, merges %llu)\n",
                                     h[16] * 0.01 / (double)h[19], h[17] * 0.01 / (double)h[19], h[18] * 0.01 / (double)h[19],

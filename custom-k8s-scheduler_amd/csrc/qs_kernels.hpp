@@ -1862,13 +1862,17 @@ __device__ __forceinline__ bool res_wait_ge(const uint32_t *p, uint32_t want, ui
                                             uint64_t ticks = kResWaitTicks) {
     if (load_coh_u32(p) >= want) return true;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    for (;;) {
+    // one sc1 load per round on the polled word (a round trip to the Infinity Cache): the error word
+    // and the clock only every 16th round, so a waiter sees its signal one round trip after it lands
+    for (uint32_t it = 1;; ++it) {
         __builtin_amdgcn_s_sleep(1);
         if (load_coh_u32(p) >= want) return true;
-        if (load_coh_u32(werr) != 0u) return false;
-        if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
-            __hip_atomic_store((gu32 *)werr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return false;
+        if ((it & 15u) == 0u) {
+            if (load_coh_u32(werr) != 0u) return false;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
+                __hip_atomic_store((gu32 *)werr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                return false;
+            }
         }
     }
 }
@@ -2095,6 +2099,8 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
     // rdiag (QS_RES_DIAG=1): summed s_memrealtime ticks of the selectors' phases, [16] scoring,
     // [17] chunk top-L, [18] publish / merge, [19] tasks, [20] merges
     uint64_t ts0 = 0, ts1 = 0, ts2 = 0, dsc = 0, dtl = 0, dpm = 0, ntask = 0, nmerge = 0;
+    // QS_RES_DIAG: selector 0 — `done` seen / its task finished, after the resolver's window start
+    uint64_t tdone_ = 0, wstart_ = 0, seen_ = 0, fin_ = 0, nwt_ = 0;
     __shared__ uint64_t lbuf[64];
     __shared__ uint32_t okflag_[4];  // (16 B: keeps the dynamic-LDS base 16-byte aligned)
     __shared__ uint32_t nred[4][8];  // NORM: per-wave partial maxima and counts
@@ -2108,6 +2114,10 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
         if (sid >= kw * G) continue;  // no task of this window (uniform per block)
         if (w >= 2) {  // the table after window w-2, and this parity's buffers free again
             if (tid == 0) okflag = res_wait_ge(&ctl->done, w - 1, c.werr) ? 1u : 0u;
+            if (rdiag && sid == 0 && tid == 0) {  // (the resolver posts each window's start time)
+                tdone_ = __builtin_amdgcn_s_memrealtime();
+                wstart_ = load_coh_u64(&rdiag[15]);
+            }
             __syncthreads();
             if (!okflag) return;
         }
@@ -2123,7 +2133,7 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
                 __syncthreads();
             }
             const uint32_t k = task / G, g = task % G;
-            if (rdiag) ts0 = __builtin_amdgcn_s_memrealtime();
+            if (rdiag && c.sel_diag) ts0 = __builtin_amdgcn_s_memrealtime();
             const PodT<F> p = pods[s0 + k];
             const uint32_t start = lo + g * chunk, end = min(hi, start + chunk);
             const uint32_t base = start + (uint32_t)w8 * E * kWave + lane;
@@ -2298,10 +2308,10 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
                     }
                 }
             }
-            if (rdiag) { __syncthreads(); ts1 = __builtin_amdgcn_s_memrealtime(); }
+            if (rdiag && c.sel_diag) { __syncthreads(); ts1 = __builtin_amdgcn_s_memrealtime(); }
             block_topl<kResBS, E>(tv, L, lbuf, [&](int j) { return pack_key(tv[j], base + j * kWave); });
             __syncthreads();  // lbuf complete
-            if (rdiag) ts2 = __builtin_amdgcn_s_memrealtime();
+            if (rdiag && c.sel_diag) ts2 = __builtin_amdgcn_s_memrealtime();
             uint64_t *out = lists + (size_t)k * 64;
             // NORM: the pod's NormInfo goes out with its list (written before the list's signal)
             auto put_norm = [&]() {
@@ -2353,13 +2363,20 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
                 }
             }
             __syncthreads();  // lbuf / okflag reused by the next task
-            if (rdiag) {
+            if (rdiag && c.sel_diag) {
                 const uint64_t t3 = __builtin_amdgcn_s_memrealtime();
                 dsc += ts1 - ts0; dtl += ts2 - ts1; dpm += t3 - ts2; ++ntask;
             }
         }
+        if (rdiag && sid == 0 && tid == 0 && w >= 2) {  // QS_RES_DIAG: selector 0's window timeline
+            const uint64_t tp = __builtin_amdgcn_s_memrealtime();
+            seen_ += tdone_ - wstart_;
+            fin_ += tp - wstart_;
+            ++nwt_;
+        }
     }
-    if (rdiag && tid == 0) {
+    if (rdiag && sid == 0 && tid == 0) { rdiag[13] = seen_; rdiag[14] = fin_; rdiag[2] = nwt_; }
+    if (rdiag && c.sel_diag && tid == 0) {
         atomicAdd((unsigned long long *)&rdiag[16], (unsigned long long)dsc);
         atomicAdd((unsigned long long *)&rdiag[17], (unsigned long long)dtl);
         atomicAdd((unsigned long long *)&rdiag[18], (unsigned long long)dpm);
@@ -2562,6 +2579,16 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
     DevCfg cv = c;
     asm volatile("" : "+v"(cv.yd_both), "+v"(cv.yd_c), "+v"(cv.yd_m), "+v"(cv.wc), "+v"(cv.wm));
     uint64_t ts_ = 0, busy_ = 0, steps_ = 0, sub_[3] = {0, 0, 0};
+    // QS_RES_DIAG: wave D's window-boundary segments (s_memrealtime ticks summed over the windows):
+    // [0] last step's barrier -> bookkeeping done, [1] -> B2, [2] -> B3, [3] -> B1, [4] -> pod 0 decided
+    uint64_t bseg_[5] = {0, 0, 0, 0, 0}, bt_ = 0;
+    auto bmark = [&](int k) {
+        if (rdiag) {
+            const uint64_t t_ = __builtin_amdgcn_s_memrealtime();
+            if (k >= 0 && bt_) bseg_[k] += t_ - bt_;
+            bt_ = t_;
+        }
+    };
     // the pipeline waves (0-3) win VALU issue arbitration against the parked waves sharing their
     // SIMDs (MI355X_MICROARCH.md, two waves per SIMD: priority, then age)
     if (wv < 4) __builtin_amdgcn_s_setprio(3);
@@ -2601,6 +2628,8 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
             bool stopped = false;  // NORM: a rescan ran in this window
             if (NORM) __syncthreads();  // B0
             __syncthreads();  // B1
+            if (w > 0) bmark(3);
+            if (rdiag && lane == 0) store_coh_u64(&rdiag[15], __builtin_amdgcn_s_memrealtime());
             for (uint32_t i = 0; i < kend; ++i) {
                 QS_RSTAMP_BEGIN()
                 const int par = i & 1, pp = par ^ 1;
@@ -2672,6 +2701,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                         res_key = ks;
                         if (stamps) res_stamp = __builtin_amdgcn_s_memrealtime();
                     }
+                    if (i == 0 && w > 0) bmark(4);
                 }
                 QS_RSTAMP_MARK(0)
                 QS_RSTAMP_END()
@@ -2711,6 +2741,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                 }
             }
             steps_ += kend;
+            bmark(-1);
             if (NORM && stopped && lane == 0 && nfall) atomicAdd(nfall + 1, 1ull);  // windows with a rescan
             if ((uint32_t)lane < kend) {
                 out_node[s0 + lane] = res_key ? (int32_t)key_node(res_key) : -1;
@@ -2738,8 +2769,11 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
 #pragma unroll
                 for (int q = 0; q < PQ; ++q) dq[q] = npq[q];
             }
+            bmark(0);
             __syncthreads();  // B2
+            bmark(1);
             __syncthreads();  // B3 (wave A stored and staged the won rows)
+            bmark(2);
             nd = (uint32_t)__popcll(wm);
             didx = (uint32_t)lane < nd ? dnode[lane] : 0xFFFFFFFFu;
             won = false;
@@ -2901,6 +2935,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
         uint64_t pe0 = 0, pe1 = 0, pe2 = 0;
         uint64_t pn0 = 0, pn1w = 0;  // NORM: the next window's NormInfo of this lane's pod (prefetched)
         uint32_t rdyv = 0, nfallback = 0;
+        uint64_t cdef_ = 0, cmiss_ = 0;  // QS_RES_DIAG: lists missing at the prefetch check (sum, windows)
         auto dirty_bit = [&](uint64_t e) -> bool {
             const uint32_t nidx = e ? key_node(e) : 0u;
             return (dirty[nidx >> 5] >> (nidx & 31)) & 1u;
@@ -3060,6 +3095,10 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                     if (i == kend - 5) rdyv = load_coh_u32(&ctl->rdy[(w + 1) & 1][0]);
                     if (i == kend - 3) {
                         pref = __builtin_amdgcn_readfirstlane(rdyv) >= tnext;
+                        if (rdiag && !pref) {  // QS_RES_DIAG: how many of the next window's lists were missing
+                            cdef_ += tnext - (uint32_t)__builtin_amdgcn_readfirstlane(rdyv);
+                            cmiss_ += 1;
+                        }
                         if (pref) {
                             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                             pe0 = ent(listsn, 0, knext);
@@ -3103,7 +3142,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
             __syncthreads();  // B2
             __syncthreads();  // B3 (D cleared the dropped slots' dirty bits before B2)
         }
-        if (rdiag && lane == 0) rdiag[4] = nfallback;
+        if (rdiag && lane == 0) { rdiag[4] = nfallback; rdiag[5] = cdef_; rdiag[6] = cmiss_; }
     } else if constexpr (NORM) {
         // ---- waves 4-7: slot statics, the rescans' extra hands, the next window's pod records ------
         // Per step (work(i), before the step's barrier; a STOP's rescan of pod i-1 already done):
@@ -3245,6 +3284,8 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
         if (wv == 0) rdiag[26] = sub_[0];
         if (wv == 0) rdiag[12] = steps_;
     }
+    if (rdiag && lane == 0 && wv == 0)
+        for (int k = 0; k < 5; ++k) rdiag[27 + k] = bseg_[k];
 }
 #undef QS_RSTAMP_BEGIN
 #undef QS_RSTAMP_END
