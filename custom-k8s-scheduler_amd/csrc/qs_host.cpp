@@ -1650,9 +1650,9 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                     dcr.sel_diag = getenv("QS_RES_DIAG") && getenv("QS_RES_DIAG")[0] == '1' ? 1u : 0u;
                     uint64_t *rdiag = nullptr;
                     if (rdiag_on) {
-                        c->diag.ensure(256);
+                        c->diag.ensure(1024);
                         rdiag = c->diag.as<uint64_t>();
-                        HIPCHK(hipMemsetAsync(rdiag, 0, 256, c->stream));
+                        HIPCHK(hipMemsetAsync(rdiag, 0, 1024, c->stream));
                     }
                     kt.begin(3, c->stream);  // the one launch, under "resolve"
                     HIPCHK(launch_la_stream_res(c->dt, dp, dx, dcr, P, rgeo, L0, c->clists.as<uint64_t>(),
@@ -1662,8 +1662,8 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                                                 st, c->resctl.p, sel, rdiag, rsh, c->stream));
                     kt.end(3, c->stream);
                     if (rdiag) {
-                        uint64_t h[32] = {0};
-                        HIPCHK(hipMemcpyAsync(h, rdiag, 256, hipMemcpyDeviceToHost, c->stream));
+                        uint64_t h[128] = {0};
+                        HIPCHK(hipMemcpyAsync(h, rdiag, 1024, hipMemcpyDeviceToHost, c->stream));
                         HIPCHK(hipStreamSynchronize(c->stream));
                         const double nw = h[3] ? (double)h[3] : 1.0;
                         fprintf(stderr, "QS_RES_DIAG resolver %.3f us per window; windows whose lists were not prefetched %llu of %llu (selectors %u)\n",
@@ -1672,6 +1672,25 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
                             fprintf(stderr, "QS_RES_DIAG selector 0: done seen %.2f us, its task finished %.2f us after "
                                             "the resolver's start of the window it overlaps (%llu windows)\n",
                                     h[13] * 0.01 / (double)h[2], h[14] * 0.01 / (double)h[2], (unsigned long long)h[2]);
+                        {
+                            std::vector<double> fin;
+                            for (uint32_t k = 0; k < std::min(sel, 64u); ++k)
+                                if (h[64 + k]) fin.push_back(h[64 + k] * 0.01);
+                            std::sort(fin.begin(), fin.end());
+                            if (!fin.empty()) {
+                                fprintf(stderr, "QS_RES_DIAG selectors' mean finish (us after window start), sorted:");
+                                for (double v : fin) fprintf(stderr, " %.1f", v);
+                                fprintf(stderr, "\n");
+                            }
+                        }
+                        if (h[36] + h[37] + h[38])
+                            fprintf(stderr, "QS_RES_DIAG B3 -> B1 busy (ns per window, without the B1 wait): D %.0f, A %.0f, "
+                                            "C %.0f\n", h[38] * 10.0 / nw, h[37] * 10.0 / nw, h[36] * 10.0 / nw);
+                        if (h[33])
+                            fprintf(stderr, "QS_RES_DIAG last list of a window published %.2f us after the start of "
+                                            "the window before it (%llu windows; after 13 us %llu, after 15 us %llu)\n",
+                                    h[32] * 0.01 / (double)h[33], (unsigned long long)h[33],
+                                    (unsigned long long)h[34], (unsigned long long)h[35]);
                         if (h[6])
                             fprintf(stderr, "QS_RES_DIAG prefetch check: %llu windows short of lists, %.2f lists missing "
                                             "on average\n", (unsigned long long)h[6], (double)h[5] / (double)h[6]);

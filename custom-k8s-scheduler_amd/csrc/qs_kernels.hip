@@ -176,7 +176,13 @@ LaGeom la_stream_res_plan(const LaGeom &geo, uint32_t feat, uint32_t n, uint32_t
     const uint32_t gmax = std::min(two ? 16u : 8u, ((two ? 2u : 1u) * cus - 1) / geo.K);
     if (gmax == 0) return r;
     constexpr uint32_t bs = kResBS;  // threads of a selector workgroup
-    const uint32_t G0 = std::min(gmax, (n + 5 * bs - 1) / (5 * bs));
+    // chunks of up to 5 * 512 nodes, or, where one selector per CU still covers every task, of
+    // 3 * 512: shorter tasks put a window's last list out earlier (config 2: 13.3 -> 12.2 us after
+    // the previous window's start, so the resolver's prefetch check at its pod K-3 stops missing
+    // it, and the boundary p99 drops 1.52 -> 1.20 us); QS_RES_G: at least that many (experiments)
+    static const uint32_t gwant = getenv("QS_RES_G") ? (uint32_t)std::max(0, atoi(getenv("QS_RES_G"))) : 0u;
+    const uint32_t gsmall = std::min((cus - 1) / geo.K, (n + 3 * bs - 1) / (3 * bs));
+    const uint32_t G0 = std::min(gmax, std::max({gwant, gsmall, (n + 5 * bs - 1) / (5 * bs)}));
     const uint32_t e_need = ((n + G0 - 1) / G0 + bs - 1) / bs;
     uint32_t E = 0;
     for (uint32_t e : {3u, 5u, 8u, 16u})

@@ -1881,7 +1881,7 @@ __device__ __forceinline__ uint32_t res_add(uint32_t *p) {
 }
 // Wave 0 sorts a pod's list (LDS, L <= 64 entries) best-first into its final slot; then the block
 // signals the resolver (every storing wave drained, barrier, one lane adds).
-__device__ __forceinline__ void res_publish_list(const uint64_t *lbuf, uint32_t L, uint64_t *out, uint32_t *rdy) {
+__device__ __forceinline__ uint32_t res_publish_list(const uint64_t *lbuf, uint32_t L, uint64_t *out, uint32_t *rdy) {
     if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
         uint64_t v = (uint32_t)lane < L ? lbuf[lane] : 0ull;
@@ -1890,14 +1890,14 @@ __device__ __forceinline__ void res_publish_list(const uint64_t *lbuf, uint32_t 
         drain_stores();
     }
     __syncthreads();
-    if (threadIdx.x == 0) res_add(rdy);
+    return threadIdx.x == 0 ? res_add(rdy) : 0u;  // (thread 0: the count before this list)
 }
 // Normalizing profiles: the same, plus the static parts (static_raw) of the pod's sorted entries
 // against the next two stream pods, sout[0][lane] vs pod s + 1 and sout[1][lane] vs pod s + 2 (the
 // resolver's wave C scores a candidate entry for the next pod, waves A/B a new slot taken from it
 // for the pod after that).  Waves 0 and 1, one pod each; published before the list's signal.
 template <class PodRec>
-__device__ __forceinline__ void res_publish_list_norm(uint64_t *lbuf, uint32_t L, uint64_t *out, uint32_t *rdy,
+__device__ __forceinline__ uint32_t res_publish_list_norm(uint64_t *lbuf, uint32_t L, uint64_t *out, uint32_t *rdy,
                                                       const DevTable &t, const PodRec *__restrict__ pods,
                                                       const DPodX *__restrict__ podx, uint32_t s, uint32_t P,
                                                       uint32_t *sout) {
@@ -1919,7 +1919,7 @@ __device__ __forceinline__ void res_publish_list_norm(uint64_t *lbuf, uint32_t L
     }
     drain_stores();
     __syncthreads();
-    if (threadIdx.x == 0) res_add(rdy);
+    return threadIdx.x == 0 ? res_add(rdy) : 0u;
 }
 
 // Sharded resident stream: the block holding rank `rank`'s shard list of window
@@ -2100,7 +2100,7 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
     // [17] chunk top-L, [18] publish / merge, [19] tasks, [20] merges
     uint64_t ts0 = 0, ts1 = 0, ts2 = 0, dsc = 0, dtl = 0, dpm = 0, ntask = 0, nmerge = 0;
     // QS_RES_DIAG: selector 0 — `done` seen / its task finished, after the resolver's window start
-    uint64_t tdone_ = 0, wstart_ = 0, seen_ = 0, fin_ = 0, nwt_ = 0;
+    uint64_t tdone_ = 0, wstart_ = 0, seen_ = 0, fin_ = 0, nwt_ = 0, lastp_ = 0, nlast_ = 0, late13_ = 0, late15_ = 0;
     __shared__ uint64_t lbuf[64];
     __shared__ uint32_t okflag_[4];  // (16 B: keeps the dynamic-LDS base 16-byte aligned)
     __shared__ uint32_t nred[4][8];  // NORM: per-wave partial maxima and counts
@@ -2114,7 +2114,7 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
         if (sid >= kw * G) continue;  // no task of this window (uniform per block)
         if (w >= 2) {  // the table after window w-2, and this parity's buffers free again
             if (tid == 0) okflag = res_wait_ge(&ctl->done, w - 1, c.werr) ? 1u : 0u;
-            if (rdiag && sid == 0 && tid == 0) {  // (the resolver posts each window's start time)
+            if (rdiag && tid == 0) {  // (the resolver posts each window's start time)
                 tdone_ = __builtin_amdgcn_s_memrealtime();
                 wstart_ = load_coh_u64(&rdiag[15]);
             }
@@ -2327,11 +2327,19 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
                 if (rsh.W > 1) {
                     if (!res_cross_merge(lbuf, L, k, w, rsh, hello_ok, okflag, c.werr, c.first_ticks)) return false;
                 }
+                uint32_t r0;
                 if constexpr (NORM)
-                    res_publish_list_norm(lbuf, L, out, &ctl->rdy[b][0], t, pods, podx, s0 + k, P,
-                                          stat0 + ((size_t)b * K + k) * 128);
+                    r0 = res_publish_list_norm(lbuf, L, out, &ctl->rdy[b][0], t, pods, podx, s0 + k, P,
+                                               stat0 + ((size_t)b * K + k) * 128);
                 else
-                    res_publish_list(lbuf, L, out, &ctl->rdy[b][0]);
+                    r0 = res_publish_list(lbuf, L, out, &ctl->rdy[b][0]);
+                if (rdiag && tid == 0 && w >= 2 && r0 + 1 == (w >> 1) * K + kw) {  // QS_RES_DIAG: the window's last list
+                    const uint64_t dt_ = __builtin_amdgcn_s_memrealtime() - wstart_;
+                    lastp_ += dt_;
+                    ++nlast_;
+                    late13_ += dt_ > 1300u;
+                    late15_ += dt_ > 1500u;
+                }
                 return true;
             };
             if (G == 1) {
@@ -2368,7 +2376,7 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
                 dsc += ts1 - ts0; dtl += ts2 - ts1; dpm += t3 - ts2; ++ntask;
             }
         }
-        if (rdiag && sid == 0 && tid == 0 && w >= 2) {  // QS_RES_DIAG: selector 0's window timeline
+        if (rdiag && tid == 0 && w >= 2) {  // QS_RES_DIAG: this selector's window timeline
             const uint64_t tp = __builtin_amdgcn_s_memrealtime();
             seen_ += tdone_ - wstart_;
             fin_ += tp - wstart_;
@@ -2376,6 +2384,13 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
         }
     }
     if (rdiag && sid == 0 && tid == 0) { rdiag[13] = seen_; rdiag[14] = fin_; rdiag[2] = nwt_; }
+    if (rdiag && tid == 0 && sid < 64) rdiag[64 + sid] = nwt_ ? fin_ / nwt_ : 0ull;  // mean finish, per selector
+    if (rdiag && tid == 0 && nlast_) {  // when each window's last list went out
+        atomicAdd((unsigned long long *)&rdiag[32], (unsigned long long)lastp_);
+        atomicAdd((unsigned long long *)&rdiag[33], (unsigned long long)nlast_);
+        atomicAdd((unsigned long long *)&rdiag[34], (unsigned long long)late13_);
+        atomicAdd((unsigned long long *)&rdiag[35], (unsigned long long)late15_);
+    }
     if (rdiag && c.sel_diag && tid == 0) {
         atomicAdd((unsigned long long *)&rdiag[16], (unsigned long long)dsc);
         atomicAdd((unsigned long long *)&rdiag[17], (unsigned long long)dtl);
@@ -2581,7 +2596,8 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
     uint64_t ts_ = 0, busy_ = 0, steps_ = 0, sub_[3] = {0, 0, 0};
     // QS_RES_DIAG: wave D's window-boundary segments (s_memrealtime ticks summed over the windows):
     // [0] last step's barrier -> bookkeeping done, [1] -> B2, [2] -> B3, [3] -> B1, [4] -> pod 0 decided
-    uint64_t bseg_[5] = {0, 0, 0, 0, 0}, bt_ = 0;
+    // [5] B3 -> B1 without the B1 wait (waves A and C: their [0])
+    uint64_t bseg_[6] = {0, 0, 0, 0, 0, 0}, bt_ = 0;
     auto bmark = [&](int k) {
         if (rdiag) {
             const uint64_t t_ = __builtin_amdgcn_s_memrealtime();
@@ -2618,15 +2634,19 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
             const uint32_t knext = w + 1 < nwin ? min(K, P - s0 - K) : 0u;
             // next window's pod records (to LDS at the end; loaded unconditionally, clamped, so the
             // loads stay in flight through the window instead of being waited for at a branch join)
+            // (three named registers, not an int4[PQ] array: the array stayed a private-memory
+            // alloca, so the loads were waited for right away and spilled to scratch before B1,
+            // ≈ 0.6 µs of every window boundary)
             constexpr int PQ = (int)(sizeof(PodT<F>) / 16);  // 16-byte quads per pod record (2, wide 3)
+            static_assert(PQ == 2 || PQ == 3, "pod record of two or three 16-byte quads");
             const int4 *pq = reinterpret_cast<const int4 *>(pods + min(s0 + K + (uint32_t)lane, P - 1));
-            int4 npq[PQ];
-#pragma unroll
-            for (int q = 0; q < PQ; ++q) npq[q] = pq[q];
+            const int4 npq0 = pq[0], npq1 = pq[1];
+            const int4 npq2 = PQ > 2 ? pq[PQ - 1] : make_int4(0, 0, 0, 0);
             uint64_t res_key = 0, res_stamp = 0;
             ResPub pv = none;
             bool stopped = false;  // NORM: a rescan ran in this window
             if (NORM) __syncthreads();  // B0
+            if (w > 0) bmark(5);
             __syncthreads();  // B1
             if (w > 0) bmark(3);
             if (rdiag && lane == 0) store_coh_u64(&rdiag[15], __builtin_amdgcn_s_memrealtime());
@@ -2766,8 +2786,9 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
             if ((uint32_t)lane < knext) {
                 int4 *dq = reinterpret_cast<int4 *>(&wpods2[(w + 1) & 1][lane]);
-#pragma unroll
-                for (int q = 0; q < PQ; ++q) dq[q] = npq[q];
+                dq[0] = npq0;
+                dq[1] = npq1;
+                if (PQ > 2) dq[PQ - 1] = npq2;
             }
             bmark(0);
             __syncthreads();  // B2
@@ -2848,6 +2869,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
             if (NORM) __syncthreads();  // B0 (the window's NormInfo is in LDS)
             if (wv == 1 && nd > 0)  // pod 0, inherited slots
                 keyA[1][lane] = slot_key(S, SX, wp[0], podn(0), NORM ? Tcur[lane] : 0u);
+            if (w > 0) bmark(0);
             __syncthreads();  // B1
             const uint32_t isig = min(2u, kend - 1);
             PodT<F> pprev = wp[0], pcur = wp[0];  // pods i-1 and i (pod i+1's record is read each step)
@@ -2917,6 +2939,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                 S = empty_row<F>();
                 SX = RowX{};
             }
+            bmark(-1);
         }
         if (wv == 1 && pend) {
             drain_stores();
@@ -3004,6 +3027,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
             }  // else r1 / x1 hold e0's row (loaded at the previous window's last pod)
             pref = false;
             if (NORM) __syncthreads();  // B0
+            if (w > 0) bmark(0);
             __syncthreads();  // B1
             const bool pfw = hasnext && kend >= 6;  // prefetch the next window during this one
             PodT<F> pcur = wp[0];  // pod i's record (pod i+1's is read each step)
@@ -3141,6 +3165,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
             if (NORM && pref && (uint32_t)lane < knext) put_norm((w + 1) & 1, pn0, pn1w);
             __syncthreads();  // B2
             __syncthreads();  // B3 (D cleared the dropped slots' dirty bits before B2)
+            bmark(-1);
         }
         if (rdiag && lane == 0) { rdiag[4] = nfallback; rdiag[5] = cdef_; rdiag[6] = cmiss_; }
     } else if constexpr (NORM) {
@@ -3286,6 +3311,8 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
     }
     if (rdiag && lane == 0 && wv == 0)
         for (int k = 0; k < 5; ++k) rdiag[27 + k] = bseg_[k];
+    if (rdiag && lane == 0 && wv == 0) rdiag[38] = bseg_[5];
+    if (rdiag && lane == 0 && (wv == 1 || wv == 3)) rdiag[wv == 1 ? 37 : 36] = bseg_[0];
 }
 #undef QS_RSTAMP_BEGIN
 #undef QS_RSTAMP_END
