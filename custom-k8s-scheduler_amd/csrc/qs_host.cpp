@@ -734,10 +734,12 @@ uint64_t run_batched(qs_ctx *c, qs_stream *s, const void *dp, const DPodX *dx, i
     const size_t cwords = std::max<size_t>(1, (size_t)geo.K * geo.G * geo.L);
     c->lists.ensure(8 * lwords);
     c->clists.ensure(8 * cwords);
-    c->bctrl.ensure(4 * 128);
-    uint32_t *ctrl = c->bctrl.as<uint32_t>(), *bidx = ctrl + 64;
+    c->bctrl.ensure(4 * 192);
+    uint32_t *ctrl = c->bctrl.as<uint32_t>(), *bidx = ctrl + 64, *tickets = ctrl + 128;
     LaBufs bf{c->lists.as<uint64_t>(), c->clists.as<uint64_t>(), nullptr, nullptr, nullptr, nullptr,
               nullptr, bidx, ctrl};
+    static const char *fm = getenv("QS_BATCH_FUSED_MERGE");  // 0: the separate k_la_merge launch (A/B)
+    if (!(fm && fm[0] == '0')) bf.tickets = tickets;
     auto batch = [&]() {
         kt.begin(2, c->stream);
         HIPCHK(launch_la_window(c->dt, dp, dx, 0, P, c->dc, geo, bf, on, ok, nullptr, nullptr, c->stream, 1));
@@ -749,6 +751,7 @@ uint64_t run_batched(qs_ctx *c, qs_stream *s, const void *dp, const DPodX *dx, i
     const uint32_t nb0 = (P + B - 1) / B;
     auto enqueue = [&]() {
         HIPCHK(hipMemsetAsync(bf.lists, 0, 8 * lwords, c->stream));
+        HIPCHK(hipMemsetAsync(tickets, 0, 4 * 64, c->stream));
         HIPCHK(launch_batch_init(ctrl, bidx, P, B, c->stream));
         static const char *se = getenv("QS_SYNC_EVERY");  // profiling aid (see the lookahead run)
         const uint32_t every = se ? (uint32_t)atoi(se) : 0u;

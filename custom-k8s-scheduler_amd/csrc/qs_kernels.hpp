@@ -765,7 +765,7 @@ __device__ __forceinline__ void la_select_block(uint32_t bid, const DevTable &t,
                                                 const uint4 *__restrict__ npart, uint32_t K,
                                                 NormInfo *__restrict__ norm_out,
                                                 const uint32_t *__restrict__ pidx,
-                                                const uint32_t *__restrict__ pcount) {
+                                                const uint32_t *__restrict__ pcount, uint32_t *tickets) {
     const SelBlock b = sel_block(t, sh, G, chunk, bid);
     uint32_t s;
     if (pidx) {  // batched mode: the batch's stream positions and size live on the device
@@ -828,6 +828,39 @@ __device__ __forceinline__ void la_select_block(uint32_t bid, const DevTable &t,
     }
     uint64_t *out = G == 1 ? lists + (size_t)b.v * sh.RS + (size_t)b.k * GLp
                            : clists + (((size_t)b.vs * sh.kw + b.k) * G + b.g) * L;
+    if (G > 1 && tickets) {
+        // batched mode: the chunk list goes out write-through, and the pod's last-arriving chunk
+        // block merges the G lists (k_la_merge's routine inside this launch: one launch and its
+        // gap less per batch); the merger resets the pod's ticket for the next batch's launch
+        __shared__ uint64_t cl_[64];
+        __shared__ uint32_t last_;
+        block_topl<BS, E>(tv, L, cl_, [&](int j) { return pack_key(tv[j], base + j * kWave); });
+        __syncthreads();
+        if ((uint32_t)tid < L) store_coh_u64(out + tid, cl_[tid]);
+        drain_stores();
+        __syncthreads();
+        uint32_t *tk = tickets + (size_t)b.vs * sh.kw + b.k;
+        if (tid == 0)
+            last_ = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u == G ? 1u : 0u;
+        __syncthreads();
+        if (!last_) return;
+        if (tid == 0) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        constexpr int E2 = 2;  // G * L <= 2 * BS (the launcher checks)
+        const uint32_t M = G * L;
+        const uint64_t *in = clists + ((size_t)b.vs * sh.kw + b.k) * M;
+        uint64_t e[E2];
+        uint32_t t2[E2];
+#pragma unroll
+        for (int j = 0; j < E2; ++j) {
+            const uint32_t pos = (uint32_t)w * E2 * kWave + (uint32_t)j * kWave + lane;
+            e[j] = pos < M ? load_coh_u64(in + pos) : 0ull;
+            t2[j] = (uint32_t)(e[j] >> 32);
+        }
+        uint64_t *fin = lists + (size_t)(sh.v0 + b.vs) * sh.RS + (size_t)b.k * GLp;
+        block_topl<BS, E2>(t2, L, fin, [&](int j) { return e[j]; });
+        sort_list_desc(fin, L);
+        return;
+    }
     block_topl<BS, E>(tv, L, out, [&](int j) { return pack_key(tv[j], base + j * kWave); });
     if (G == 1) sort_list_desc(out, L);  // a final list (else k_la_merge sorts)
 }
@@ -842,9 +875,9 @@ __global__ __launch_bounds__(BS) void k_la_select(DevTable t, const PodT<F> *__r
                                                   const uint4 *__restrict__ npart, uint32_t K,
                                                   NormInfo *__restrict__ norm_out,
                                                   const uint32_t *__restrict__ pidx,
-                                                  const uint32_t *__restrict__ pcount) {
+                                                  const uint32_t *__restrict__ pcount, uint32_t *tickets) {
     la_select_block<BS, E, F>(blockIdx.x, t, pods, podx, c, s0, P, sh, G, L, chunk, GLp, lists, clists,
-                              npart, K, norm_out, pidx, pcount);
+                              npart, K, norm_out, pidx, pcount, tickets);
 }
 
 // Grid: shards × pods.  Reduces a pod's G chunk lists (M = G*L keys, chunk-major: equal totals
@@ -3790,14 +3823,16 @@ static hipError_t la_window_f(const DevTable &t, const void *pods_, const DPodX 
         QS_RET(hipGetLastError());
     }
     if (part & 1) {
+        // batched mode: the merge inside the select launch (its G * L keys: two per thread)
+        uint32_t *tickets = (bf.tickets && G > 1 && G * L <= 512) ? bf.tickets : nullptr;
         switch (geo.E) {
-#define QS_SEL(EE) case EE: hipLaunchKernelGGL((k_la_select<256, EE, F>), grid, dim3(256), 0, stream, t, pods, podx, c, s0, P, sh, G, L, geo.chunk, GLp, bf.lists, bf.clists, bf.npart, K, bf.norm, bf.pidx, bf.pcount); break;
+#define QS_SEL(EE) case EE: hipLaunchKernelGGL((k_la_select<256, EE, F>), grid, dim3(256), 0, stream, t, pods, podx, c, s0, P, sh, G, L, geo.chunk, GLp, bf.lists, bf.clists, bf.npart, K, bf.norm, bf.pidx, bf.pcount, tickets); break;
             QS_SEL(1) QS_SEL(2) QS_SEL(3) QS_SEL(4) QS_SEL(5) QS_SEL(6) QS_SEL(8) QS_SEL(10) QS_SEL(12) QS_SEL(16)
 #undef QS_SEL
             default: return hipErrorInvalidValue;
         }
         QS_RET(hipGetLastError());
-        if (G > 1) {
+        if (G > 1 && !tickets) {
             const uint32_t M = G * L, e2 = (M + 255) / 256;
             const dim3 mgrid(geo.nv * kw);
             switch (e2) {

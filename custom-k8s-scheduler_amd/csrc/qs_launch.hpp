@@ -89,6 +89,9 @@ struct LaBufs {
     const uint32_t *pidx = nullptr, *pcount = nullptr;
     // normalizing profiles, four-wave resolver: the stop record it hands to the resume kernel
     uint32_t *rec = nullptr;
+    // batched mode: per pod chunk-arrival tickets (zeroed at the stream's start); with them the
+    // select launch merges each pod's chunk lists itself (no k_la_merge launch)
+    uint32_t *tickets = nullptr;
 };
 // In-kernel window hand-off (DevCfg::ready): publish a window's lists (value = run << 32 | w + 1).
 hipError_t launch_ready_set(uint64_t *ready, uint64_t value, hipStream_t stream);
