@@ -8,13 +8,15 @@ TAG=${1:-r01}
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 rm -rf $OUT; mkdir -p $OUT profiles
-ARGS="--steps 2 --warmup 1 --no-cpu --no-config3"
+ARGS="--steps 2 --warmup 1 --no-cpu"  # config 3 included: its k_la_stream_res row
 PMC_ARGS="--steps 1 --warmup 1 --no-cpu --no-config3 --no-extra"  # the scan leg too: k_scan_soa traffic
 # heartbeat for the GPU pool's silence watchdog (counter passes print nothing for minutes)
 ( while sleep 45; do date >> $OUT/heartbeat; done ) &
 HB=$!
 trap "kill $HB 2>/dev/null" EXIT
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py $ARGS > $OUT/trace.log 2>&1
+# (QS_GRAPH=0: rocprofv3 7.2's kernel trace crashed (SIGSEGV in the HIP runtime) on the batched
+# leg's graph launch in round 5; the resident streams are single launches either way)
+QS_GRAPH=0 QS_SYNC_EVERY=64 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py $ARGS > $OUT/trace.log 2>&1
 echo "trace done"
 # counter passes: cross-stream events (QS_HANDOFF=0: counter collection serialises dispatches, so a
 # resolver waiting in-kernel for the other stream's lists would time out), individual launches
