@@ -16,7 +16,7 @@ for g in ${GS:-0 4}; do
 done
 for leg in ${LEGS:-config4 wide config3}; do
   timeout -k 10 300 python -u bench.py --leg $leg --no-cpu > gpurun_out/leg_${leg}_r5f.json 2>gpurun_out/leg_${leg}_r5f.err || exit 9
-  python -c "import json;d=json.load(open('gpurun_out/leg_${leg}_r5f.json'));print('$leg', d['value'], d.get('ms_per_step'), d['check'].get('placements_match'))"
+  python -c "import json;d=json.load(open('gpurun_out/leg_${leg}_r5f.json'));print('$leg', d['value'], d.get('ms_per_step'), d.get('check', d).get('placements_match'))"
 done
 QS_RES_G=4 timeout -k 10 300 python -u bench.py --leg config4 --no-cpu > gpurun_out/leg_config4g4_r5f.json 2>gpurun_out/leg_config4g4_r5f.err || exit 9
 python -c "import json;d=json.load(open('gpurun_out/leg_config4g4_r5f.json'));print('config4 G=4', d['value'], d.get('ms_per_step'), d['check'].get('placements_match'))"
