@@ -738,7 +738,7 @@ uint64_t run_batched(qs_ctx *c, qs_stream *s, const void *dp, const DPodX *dx, i
     uint32_t *ctrl = c->bctrl.as<uint32_t>(), *bidx = ctrl + 64, *tickets = ctrl + 128;
     LaBufs bf{c->lists.as<uint64_t>(), c->clists.as<uint64_t>(), nullptr, nullptr, nullptr, nullptr,
               nullptr, bidx, ctrl};
-    static const char *fm = getenv("QS_BATCH_FUSED_MERGE");  // 0: the separate k_la_merge launch (A/B)
+    const char *fm = getenv("QS_BATCH_FUSED_MERGE");  // 0: the separate k_la_merge launch (read per run)
     if (!(fm && fm[0] == '0')) bf.tickets = tickets;
     auto batch = [&]() {
         kt.begin(2, c->stream);

@@ -39,6 +39,22 @@ def test_batched_parity(oracle, config, n, p, batch):
     assert stats["batches"] == o_nb
 
 
+@pytest.mark.parametrize("n,fused", [(3000, "0"), (20000, "1")])
+def test_batched_merge_forms(oracle, monkeypatch, n, fused):
+    """The two merge forms of a batch's chunk lists give the same lists: the merge inside the select
+    launch (per-pod tickets, the default when G * L <= 512) switched off with
+    QS_BATCH_FUSED_MERGE=0, and a 20,000-node table whose G * L > 512 takes the separate k_la_merge
+    launch whatever the switch says."""
+    monkeypatch.setenv("QS_BATCH_FUSED_MERGE", fused)
+    nodes, pods = synth_generate(5, n, 4000)
+    g_pl, g_keys, g_final, stats = run_gpu_batched(nodes, pods)
+    on = {k: v.copy() for k, v in nodes.items()}
+    o_pl, o_keys, o_nb = oracle.schedule_batched(on, pods_from_struct(pods), batch=64, nthreads=16)
+    assert np.array_equal(g_pl, o_pl)
+    assert np.array_equal(g_keys, o_keys)
+    assert stats["batches"] == o_nb
+
+
 def test_batched_full_config5_invariants():
     """BASELINE.json configs[4]: 10,000 nodes; 200,000 pods with 1,000 anti-affinity apps."""
     nodes, pods = synth_generate(5, 10000, 200000)
