@@ -213,6 +213,14 @@ __global__ __launch_bounds__(256) void k_scan_key(DevTable t, const PodT<F> *__r
     if (threadIdx.x == 0) sc->partial[blockIdx.x] = best;
 }
 
+// One 16-byte quad of a SoA column, read non-temporally: every byte of the scan is read once per
+// pod, and the streaming hint took k_scan_soa from 5.2 to 5.9-6.0 TB/s on the 2^24-node table
+// (65 -> 74 % of the 8 TB/s peak, tools/scan_probe.py; four quads in flight per lane instead of two
+// was slower, 4.7-5.5 TB/s with or without the hint).
+__device__ __forceinline__ int4 soa_quad(const int32_t *col, uint32_t q) {
+    return __builtin_bit_cast(int4, __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(col) + q));
+}
+
 // Keys over the SoA copy (HBM-resident tables; F = 0 or kFeatExt): lane q covers nodes
 // 4q..4q+3 with one 16-byte load per column; RN(1/alloc) is recomputed in registers (rcp_int:
 // the same value the host stores in the row copy, so keys are bit-identical to k_scan_key).
@@ -233,10 +241,10 @@ __global__ __launch_bounds__(256) void k_scan_soa(DevTable t, const PodT<F> *__r
         for (int h = 0; h < 2; ++h) {
             const uint32_t qh = min(q0 + h * stride, nq - 1);
 #pragma unroll
-            for (int k = 0; k < 8; ++k) cols[h][k] = reinterpret_cast<const int4 *>(t.soa.c[k])[qh];
+            for (int k = 0; k < 8; ++k) cols[h][k] = soa_quad(t.soa.c[k], qh);
             if (F & kFeatExt) {
 #pragma unroll
-                for (int k = 8; k < kSCols; ++k) cols[h][k] = reinterpret_cast<const int4 *>(t.soa.c[k])[qh];
+                for (int k = 8; k < kSCols; ++k) cols[h][k] = soa_quad(t.soa.c[k], qh);
             }
         }
 #pragma unroll
