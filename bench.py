@@ -233,8 +233,14 @@ def diag_runs(cx, nodes, pods, cfg, sharded):
             st2.run()
             d = np.diff(st2.stamps().astype(np.int64)) * 0.01  # 100 MHz s_memrealtime ticks -> us
             st2.free()
-            return float(np.percentile(d, 50)), float(np.percentile(d, 99))
-        p50, p99 = run_phase(cx, stamps)
+            # split by window position: the interval ending at a window's first pod
+            # (the window boundary, 1 in K) against the ones inside a window
+            K = int(cfg.get("lookahead") or 32)
+            bnd = (np.arange(1, len(d) + 1) % K) == 0
+            split = {"window_boundary": float(np.percentile(d[bnd], 99)) if bnd.any() else None,
+                     "within_window": float(np.percentile(d[~bnd], 99)) if (~bnd).any() else None}
+            return float(np.percentile(d, 50)), float(np.percentile(d, 99)), split
+        p50, p99, split = run_phase(cx, stamps)
     finally:
         s2.close()
     s3 = open_sched(cx, dict(cfg, profile_kernels=1), sharded)
@@ -252,7 +258,7 @@ def diag_runs(cx, nodes, pods, cfg, sharded):
         kp = run_phase(cx, prof)
     finally:
         s3.close()
-    return p50, p99, kp
+    return p50, p99, kp, split
 
 
 def roofline(kp, n_nodes, n_pods, fallback_s):
@@ -462,7 +468,7 @@ def measure(cx, a, workload, steps, warmup, with_diag=True):
            "n_pods": n_pods, "desc": desc, "sharded": sharded, "nodes": nodes, "pods": pods,
            "replicas": ranks_work}
     if with_diag:
-        out["p50"], out["p99"], out["kp"] = diag_runs(cx, nodes, pods, cfg, sharded)
+        out["p50"], out["p99"], out["kp"], out["p99_split"] = diag_runs(cx, nodes, pods, cfg, sharded)
         out["wall_fallback"] = last["wall_s"]
     return out
 
@@ -853,6 +859,8 @@ def main():
                        "lookahead": a.lookahead or 32, "parallelism": par},
             "evals_per_s": round(m["value"] * m["n_nodes"], 1),
             "p50_pod_latency_us": round(m["p50"], 4), "p99_pod_latency_us": round(m["p99"], 4),
+            "p99_pod_latency_split_us": {k: (round(v, 4) if v is not None else None)
+                                         for k, v in (m.get("p99_split") or {}).items()},
             "unschedulable_frac": round(m["unschedulable_frac"], 5),
             "roofline": rl,
             "kernels_us_per_step": {k: round(v["s"] * 1e6, 1) for k, v in m["kp"].items()},
