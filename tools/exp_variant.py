@@ -1,5 +1,5 @@
 """Build a timing variant of the compact kernels (libqsched_<name>.so) from text substitutions of
-csrc/qs_kernels.hpp, without touching the product sources (DESIGN.md §4.1e method: measure a
+csrc/qs_kernels.hpp (or qs_device.hpp), without touching the product sources (DESIGN.md §4.1e method: measure a
 variant against the product in the same gpurun call, keep it only if it wins).
 
 Usage: python tools/exp_variant.py NAME 'old1' 'new1' ['old2' 'new2' ...]
@@ -22,12 +22,15 @@ def main():
     if os.path.exists(dst):
         shutil.rmtree(dst)
     shutil.copytree(src, dst)
-    p = os.path.join(dst, "qs_kernels.hpp")
-    s = open(p).read()
+    # each substitution applies to the first of these headers that holds its `old` text
+    files = [os.path.join(dst, f) for f in ("qs_kernels.hpp", "qs_device.hpp")]
+    text = {f: open(f).read() for f in files}
     for old, new in zip(subs[0::2], subs[1::2]):
-        assert old in s, f"not found: {old[:80]!r}"
-        s = s.replace(old, new)
-    open(p, "w").write(s)
+        f = next((f for f in files if old in text[f]), None)
+        assert f is not None, f"not found: {old[:80]!r}"
+        text[f] = text[f].replace(old, new)
+    for f in files:
+        open(f, "w").write(text[f])
     flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-ffp-contract=off",
              "-Wno-unused-function", "-mllvm", "-amdgpu-atomic-optimizer-strategy=None",
              f"-I{os.path.join(ROOT, 'include')}"]
