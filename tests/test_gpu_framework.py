@@ -46,12 +46,14 @@ def test_score_pod_parity(layout, config, n):
             np.testing.assert_array_equal(got["scores"][feas], sc[feas])
 
 
-@pytest.mark.parametrize("n", [1, 255, 257, 4096, 16384, 16385, 50000, 70001])
+@pytest.mark.parametrize("n", [1, 255, 257, 1023, 1024, 1025, 4096, 16383, 16384, 16385, 50000,
+                               70001])
 def test_score_pod_grid_edges_reused_buffers(n):
-    """The multi-workgroup score launch (one node per thread, ceil(n/256) workgroups, the last
-    arrival publishing best + done) at workgroup-count edges and beyond round 3's 16,384-node
-    one-launch limit (50,000 = config 3's table; 70,001 keeps a SoA copy too), with the packed outputs
-    unpacked 16 nodes at a time (tails 1, 15, 1, 0, 0, 1, 0, 1) into caller buffers reused across
+    """The multi-workgroup score launch (one node per thread, ceil(n/1024) workgroups of
+    kScorePodGT = 1024 threads, the last arrival publishing best + done) at workgroup-count edges
+    (1023/1024/1025, 16383/16384/16385) and beyond round 3's 16,384-node one-launch limit
+    (50,000 = config 3's table; 70,001 keeps a SoA copy too), with the packed outputs unpacked 16
+    nodes at a time (tails 1, 15, 1, 15, 0, 1, 0, 15, 0, 1, 0, 1) into caller buffers reused across
     calls and Reserves; every call diffed against the oracle and against a fresh-buffer call."""
     from oracle import oracle as O
     nodes, pods = synth_generate(2, n, 12)
