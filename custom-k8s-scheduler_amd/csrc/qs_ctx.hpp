@@ -42,6 +42,14 @@ struct QsError {
 
 [[noreturn]] inline void fail(qs_status st, const std::string &m) { throw QsError{st, m}; }
 
+// Why the calling thread's last qs_open / qs_open_shard failed (there is no context to hold the
+// message): qs_last_error(NULL) returns it.
+inline thread_local std::string g_open_err;
+inline qs_status open_failed(qs_status st, const std::string &m) {
+    g_open_err = m;
+    return st;
+}
+
 struct DevBuf {
     void *p = nullptr;
     size_t bytes = 0;
@@ -130,6 +138,7 @@ struct qs_ctx {
     uint64_t device_faults = 0; // QS_EDEVICE results so far (each one drops the device table)
     qs_host::DevBuf diag;
     qs_host::DevBuf scratch, lists, clists, dio, npart, normi, nstat, nfall, nrec, bctrl, one_pod, one_podx;
+    qs_host::DevBuf vshard;  // the all-reduce engine's virtual-world node ranges ([V][lo, hi])
     void *pin = nullptr;   // qs_score_pod's packed outputs, written by the kernel (pinned host memory)
     size_t pin_bytes = 0;
     uint64_t score_seq = 0;  // the kernel's done word for the call in flight

@@ -124,7 +124,8 @@ qs_status qs_dist_unique_id(uint8_t out[128]) {
 
 qs_status qs_open_shard(const qs_config *cfg, int device, int rank, int world,
                         const uint8_t nccl_id[128], qs_ctx **out) {
-    if (!cfg || !out || world < 1 || world > 16 || rank < 0 || rank >= world) return QS_EINVAL;
+    if (!cfg || !out || world < 1 || world > 16 || rank < 0 || rank >= world)
+        return open_failed(QS_EINVAL, "qs_open_shard: need 0 <= rank < world <= 16 and a config");
     qs_status st = qs_open(cfg, device, out);
     if (st != QS_OK) return st;
     qs_ctx *c = *out;
@@ -138,9 +139,12 @@ qs_status qs_open_shard(const qs_config *cfg, int device, int rank, int world,
     ncclComm_t comm = nullptr;
     const ncclResult_t r = ncclCommInitRank(&comm, world, id, rank);
     if (r != ncclSuccess) {
+        const char *last = ncclGetLastError(nullptr);
         qs_close(c);
         *out = nullptr;
-        return QS_EDEVICE;
+        return open_failed(QS_EDEVICE, std::string("ncclCommInitRank(world ") + std::to_string(world) + ", rank " +
+                                           std::to_string(rank) + ", device " + std::to_string(device) +
+                                           "): " + nccl_msg(r) + (last && *last ? std::string(" — ") + last : ""));
     }
     c->comm = comm;
     return QS_OK;

@@ -771,6 +771,7 @@ uint64_t run_batched(qs_ctx *c, qs_stream *s, const void *dp, const DPodX *dx, i
         put(&geo, sizeof geo);
         const int tag = 2;  // batched
         put(&tag, sizeof tag);
+        put(&bf.tickets, sizeof bf.tickets);  // the merge form is read per run
         if (!s->gexec || s->gkey != key) {
             if (s->gexec) (void)hipGraphExecDestroy(s->gexec);
             s->gexec = nullptr;
@@ -830,7 +831,8 @@ void qs_config_default(qs_config *cfg) {
 }
 
 qs_status qs_open(const qs_config *cfg, int device, qs_ctx **out) {
-    if (!cfg || !out) return QS_EINVAL;
+    g_open_err.clear();
+    if (!cfg || !out) return open_failed(QS_EINVAL, "qs_open: null config or output pointer");
     *out = nullptr;
     qs_ctx *c = new (std::nothrow) qs_ctx();
     if (!c) return QS_ENOMEM;
@@ -849,10 +851,10 @@ qs_status qs_open(const qs_config *cfg, int device, qs_ctx **out) {
         HIPCHK(hipMemset(c->scratch.p, 0, scan_scratch_bytes()));
     } catch (const QsError &e) {
         delete c;
-        return e.st;
+        return open_failed(e.st, e.msg);
     } catch (...) {
         delete c;
-        return QS_EDEVICE;
+        return open_failed(QS_EDEVICE, "qs_open: unexpected failure");
     }
     *out = c;
     return QS_OK;
@@ -878,7 +880,11 @@ qs_status qs_close(qs_ctx *c) {
     return QS_OK;
 }
 
-const char *qs_last_error(const qs_ctx *c) { return c ? c->err.c_str() : "null context"; }
+// (no context: why the calling thread's last qs_open / qs_open_shard failed, or "null context")
+const char *qs_last_error(const qs_ctx *c) {
+    if (c) return c->err.c_str();
+    return g_open_err.empty() ? "null context" : g_open_err.c_str();
+}
 
 qs_status qs_nodes_load(qs_ctx *c, const qs_node_soa *nd, uint32_t n) {
     return guarded(c, [&] {
@@ -1313,6 +1319,12 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
         if (mode != QS_MODE_EXACT && mode != QS_MODE_BATCHED) fail(QS_EINVAL, "unknown qs_mode");
         if (s->shift != c->shift || s->wide != c->wide) fail(QS_ESTATE, "node table re-laid out after prepare");
         HIPCHK(hipSetDevice(c->device));
+        // from here on the device table (and d_node) may change even if this run fails part way
+        // (e.g. a resident timeout): invalidate the stream's results and every other stream's FitError
+        // replay now; only a successful run sets them again below
+        s->ran = false;
+        s->mode_ran = -1;
+        ++c->table_epoch;
         if (!c->dev_valid) upload_table(c);  // recovery after a device fault: rebuild from the mirror
         const uint32_t n = c->m.n, P = s->p;
         c->dc.feat = s->feat;
@@ -1355,27 +1367,48 @@ qs_status qs_stream_run(qs_ctx *c, qs_stream *s, qs_mode mode, qs_stats *stats) 
             } else if (eng == QS_ENGINE_ALLREDUCE) {
                 // SURVEY.md §8(e) C1 as-is: per pod every rank scans its contiguous node shard over the
                 // rows, one ncclAllReduce(u64 max) of the packed key (C2: the two normalize maxima
-                // first), and every rank applies the same Reserve to its replicated table
+                // first), and every rank applies the same Reserve to its replicated table.
+                // virtual_shards = V > 1 on a one-rank communicator: this context scans all V node
+                // ranges of a V-rank world in turn into the same scratch (the maxima with atomicMax,
+                // the keys max-into-best), so the shard partition and the max over shards run
+                // exactly as V ranks would compute them (the test form of the multi-rank engine)
                 if (!c->comm)
                     fail(QS_ESTATE, "the all-reduce engine needs an RCCL communicator (qs_open_shard with an id)");
+                const uint32_t V = c->world == 1 && c->cfg.virtual_shards > 1 ? (uint32_t)c->cfg.virtual_shards : 1u;
+                const uint32_t R = V > 1 ? V : (uint32_t)c->world;
                 DevTable dt = c->dt;
                 std::memset(&dt.soa, 0, sizeof dt.soa);  // rows only (the SoA copy is marked stale below)
-                const uint32_t sh[2] = {(uint32_t)((uint64_t)n * c->rank / c->world),
-                                        (uint32_t)((uint64_t)n * (c->rank + 1) / c->world)};
+                std::vector<uint32_t> sh(2 * (size_t)R);
+                for (uint32_t r = 0; r < R; ++r) {
+                    sh[2 * r] = (uint32_t)((uint64_t)n * r / R);
+                    sh[2 * r + 1] = (uint32_t)((uint64_t)n * (r + 1) / R);
+                }
+                const uint32_t r0 = V > 1 ? 0u : (uint32_t)c->rank;  // this rank's range (V = 1)
+                c->vshard.ensure(8 * (size_t)R);
+                HIPCHK(hipMemcpy(c->vshard.p, sh.data(), 8 * (size_t)R, hipMemcpyHostToDevice));
                 HIPCHK(hipMemsetAsync(c->scratch.p, 0, scan_scratch_bytes(), c->stream));
-                HIPCHK(hipMemcpyAsync(static_cast<char *>(c->scratch.p) + offsetof(ScanHead, lo), sh, 8,
-                                      hipMemcpyHostToDevice, c->stream));
+                char *lohi = static_cast<char *>(c->scratch.p) + offsetof(ScanHead, lo);
+                auto range = [&](uint32_t r) {
+                    return hipMemcpyAsync(lohi, c->vshard.as<uint32_t>() + 2 * r, 8, hipMemcpyDeviceToDevice, c->stream);
+                };
+                if (V == 1) HIPCHK(range(r0));
                 ScanHead *sc = c->scratch.as<ScanHead>();
                 const bool norm = (c->dc.feat & (kFeatTaint | kFeatAffinity)) != 0;
                 for (uint32_t k = 0; k < P; k++) {
                     kt.begin(1, c->stream);
                     if (norm) {
-                        HIPCHK(launch_scan_pod(dt, dp, dx, k, c->dc, c->scratch.p, on, ok, st, nullptr, nullptr,
-                                               nullptr, 8, c->stream));
+                        for (uint32_t v = 0; v < V; ++v) {
+                            if (V > 1) HIPCHK(range(v));
+                            HIPCHK(launch_scan_pod(dt, dp, dx, k, c->dc, c->scratch.p, on, ok, st, nullptr, nullptr,
+                                                   nullptr, 8, c->stream));
+                        }
                         allreduce_max_u32(c, &sc->mt, 2, c->stream);
                     }
-                    HIPCHK(launch_scan_pod(dt, dp, dx, k, c->dc, c->scratch.p, on, ok, st, nullptr, nullptr,
-                                           nullptr, 16 | 32, c->stream));
+                    for (uint32_t v = 0; v < V; ++v) {
+                        if (V > 1) HIPCHK(range(v));
+                        HIPCHK(launch_scan_pod(dt, dp, dx, k, c->dc, c->scratch.p, on, ok, st, nullptr, nullptr,
+                                               nullptr, 16 | 32, c->stream));
+                    }
                     allreduce_max_u64(c, reinterpret_cast<uint64_t *>(&sc->best), 1, c->stream);
                     HIPCHK(launch_scan_pod(dt, dp, dx, k, c->dc, c->scratch.p, on, ok, st, nullptr, nullptr,
                                            nullptr, 64, c->stream));
@@ -1946,7 +1979,10 @@ size_t qs_struct_size(int which) {
 // run's initial table (the final mirror minus every placed pod's delta) plus the deltas of the pods
 // placed before it in stream order; each node's reasons follow spec S4/S5's filters in upstream's
 // default order, NodeResourcesFit listing every insufficient resource (UP fit.go#fitsRequest).
-qs_status qs_stream_fit_errors(qs_ctx *c, qs_stream *s, const uint32_t *pods, uint32_t mreq, uint32_t *counts) {
+// counts: m x QS_FIT_REASONS; tcounts (nullable): m x 64, the QS_FIT_TAINT nodes split by the first
+// untolerated taint bit (the lowest set bit of taint_hard & ~tol_hard)
+static qs_status fit_errors(qs_ctx *c, qs_stream *s, const uint32_t *pods, uint32_t mreq, uint32_t *counts,
+                            uint32_t *tcounts) {
     return guarded(c, [&] {
         if (!s || !s->ran) fail(QS_ESTATE, "stream has not run");
         if (s->mode_ran != QS_MODE_EXACT) fail(QS_EINVAL, "FitError diagnosis covers exact streams");
@@ -1956,6 +1992,7 @@ qs_status qs_stream_fit_errors(qs_ctx *c, qs_stream *s, const uint32_t *pods, ui
         for (uint32_t q = 0; q < mreq; q++)
             if (pods[q] >= P) fail(QS_EINVAL, "pod index out of range");
         std::memset(counts, 0, sizeof(uint32_t) * QS_FIT_REASONS * (size_t)mreq);
+        if (tcounts) std::memset(tcounts, 0, sizeof(uint32_t) * 64 * (size_t)mreq);
         if (!mreq) return;
         HIPCHK(hipSetDevice(c->device));
         sync_mirror(c);
@@ -1977,9 +2014,14 @@ qs_status qs_stream_fit_errors(qs_ctx *c, qs_stream *s, const uint32_t *pods, ui
             const qs_pod &p = s->pods[s->order[k]];
             if (node[k] < 0 && !want[k].empty()) {
                 uint32_t cnt[QS_FIT_REASONS] = {0};
+                uint32_t tcnt[64] = {0};
                 const bool any_req = p.req_cpu || p.req_mem || p.req_ext[0] || p.req_ext[1];
                 for (uint32_t i = 0; i < m.n; i++) {
-                    if (taint && (m.th[i] & ~p.tol_hard) != 0) { ++cnt[QS_FIT_TAINT]; continue; }
+                    if (taint && (m.th[i] & ~p.tol_hard) != 0) {
+                        ++cnt[QS_FIT_TAINT];
+                        ++tcnt[__builtin_ctzll(m.th[i] & ~p.tol_hard)];
+                        continue;
+                    }
                     if (aff) {
                         const uint64_t *lb = &m.lb[2 * (size_t)i];
                         bool ok = subset(p.sel, lb);
@@ -2000,11 +2042,24 @@ qs_status qs_stream_fit_errors(qs_ctx *c, qs_stream *s, const uint32_t *pods, ui
                             ++cnt[QS_FIT_EXT0 + e];
                     }
                 }
-                for (uint32_t q : want[k]) std::memcpy(counts + (size_t)q * QS_FIT_REASONS, cnt, sizeof cnt);
+                for (uint32_t q : want[k]) {
+                    std::memcpy(counts + (size_t)q * QS_FIT_REASONS, cnt, sizeof cnt);
+                    if (tcounts) std::memcpy(tcounts + (size_t)q * 64, tcnt, sizeof tcnt);
+                }
             }
             if (node[k] >= 0) mirror_reserve(m, (uint32_t)node[k], p, +1);
         }
     });
+}
+
+qs_status qs_stream_fit_errors(qs_ctx *c, qs_stream *s, const uint32_t *pods, uint32_t mreq, uint32_t *counts) {
+    return fit_errors(c, s, pods, mreq, counts, nullptr);
+}
+
+qs_status qs_stream_fit_taints(qs_ctx *c, qs_stream *s, const uint32_t *pods, uint32_t mreq, uint32_t *counts,
+                               uint32_t *taint_counts) {
+    if (!taint_counts && mreq) return QS_EINVAL;
+    return fit_errors(c, s, pods, mreq, counts, taint_counts);
 }
 
 qs_status qs_stream_stamps(qs_ctx *c, qs_stream *s, uint64_t *stamps) {

@@ -295,7 +295,14 @@ __global__ __launch_bounds__(256) void k_scan_commit(DevTable t, const PodT<F> *
     for (uint32_t i = threadIdx.x; i < nblk; i += 256) v = sc->partial[i] > v ? sc->partial[i] : v;
     const uint64_t ks = nblk ? block_max_u64<256>(v) : sc->best;
     if (threadIdx.x != 0) return;
-    sc->best = ks;
+    if (nblk && !out_node) {
+        // the all-reduce engine's shard reduction (part 32): max INTO best, so the shards of a
+        // virtual world (one context scanning every node range in turn) combine as the all-reduce
+        // does; the commit (part 64) consumes best and clears it for the next pod
+        sc->best = ks > sc->best ? ks : sc->best;
+        return;
+    }
+    sc->best = nblk ? ks : 0ull;
     sc->mt = 0;
     sc->ma = 0;
     if (!out_node) return;

@@ -19,7 +19,7 @@ import numpy as np
 
 from ._abi import (ENGINES, ENGINE_NAMES, EXPORTED, LIB_PATH, POD_DTYPE, QS_ABI_VERSION,
                    QS_MAX_EXT, QS_MAX_SCORE_RES, QS_MAX_TERMS, QS_MODE_BATCHED, QS_MODE_EXACT, QS_OK,
-                   RESOURCES, FIT_REASONS, QschedError,
+                   RESOURCES, FIT_REASONS, QS_FIT_TAINT, QschedError,
                    QschedLibraryMissing, QsConfig, QsContainer, QsNodeRow, QsNodeSoa, QsStats,
                    load)
 
@@ -139,7 +139,8 @@ class Scheduler:
             st = self.lib.qs_open_shard(ctypes.byref(self.cfg), device, rank, world, buf,
                                         ctypes.byref(ctx))
         if st != QS_OK:
-            raise QschedError(st, "qs_open failed (no HIP device?)")
+            why = self.lib.qs_last_error(None)
+            raise QschedError(st, "qs_open failed: " + (why.decode() if why else "no HIP device?"))
         self.ctx = ctx
         self.n = 0
 
@@ -294,17 +295,24 @@ class Stream:
         self.s._chk(self.s.lib.qs_stream_stamps(self.s.ctx, self.h, _ptr(out)))
         return out
 
-    def fit_errors(self, pods=None):
+    def fit_errors(self, pods=None, by_taint=False):
         """qs_stream_fit_errors: per requested pod (arrival indices; default: every unschedulable
         pod) the count of nodes per FitError reason column (FIT_REASONS), against the table at that
-        pod's turn.  Returns (indices, counts[m, 7])."""
+        pod's turn.  Returns (indices, counts[m, 7]); with by_taint (qs_stream_fit_taints) also
+        taint_counts[m, 64], the untolerated-taint column split by the node's first untolerated taint
+        bit (upstream names that taint in the reason string)."""
         if pods is None:
             pl, _ = self.results()
             pods = np.nonzero(pl < 0)[0]
         idx = np.ascontiguousarray(pods, dtype=np.uint32)
         counts = np.zeros((len(idx), len(FIT_REASONS)), np.uint32)
-        self.s._chk(self.s.lib.qs_stream_fit_errors(self.s.ctx, self.h, _ptr(idx), len(idx), _ptr(counts)))
-        return idx, counts
+        if not by_taint:
+            self.s._chk(self.s.lib.qs_stream_fit_errors(self.s.ctx, self.h, _ptr(idx), len(idx), _ptr(counts)))
+            return idx, counts
+        tcounts = np.zeros((len(idx), 64), np.uint32)
+        self.s._chk(self.s.lib.qs_stream_fit_taints(self.s.ctx, self.h, _ptr(idx), len(idx), _ptr(counts),
+                                                     _ptr(tcounts)))
+        return idx, counts, tcounts
 
     def free(self):
         if self.h:
@@ -350,11 +358,32 @@ def _containers(containers):
     return arr
 
 
-def fit_error_message(counts, n_nodes, ext_names=("ext0", "ext1")):
+def fit_error_message(counts, n_nodes, ext_names=("ext0", "ext1"), taint_counts=None, taint_names=None):
     """UP framework/types.go#FitError.Error() from one pod's reason counts: "0/N nodes are available:
-    <count> <reason>, ..." with the "count reason" strings sorted as Go's sort.Strings does."""
-    names = [r.format(ext0=ext_names[0], ext1=ext_names[1]) for r in FIT_REASONS]
-    parts = sorted(f"{int(c)} {names[k]}" for k, c in enumerate(counts) if c)
+    <count> <reason>, ..." with the "count reason" strings sorted as Go's sort.Strings does.
+
+    Upstream's TaintToleration reason names the node's first untolerated taint ("node(s) had
+    untolerated taint {key: value}", taint_toleration.go#Filter), so each distinct taint is its own
+    reason.  Pass taint_counts (this pod's row of ``fit_errors(by_taint=True)``) and taint_names
+    (interned bit -> "key: value", e.g. from qsched.workload's taint dictionary) to get that text;
+    without them the untolerated-taint nodes are one reason and a bit without a name renders as
+    "taint-<bit>"."""
+    names = [r.format(ext0=ext_names[0], ext1=ext_names[1], taint="{taint}") for r in FIT_REASONS]
+    parts = []
+    for k, c in enumerate(counts):
+        if not c:
+            continue
+        if k == QS_FIT_TAINT and taint_counts is not None:
+            tc = np.asarray(taint_counts)
+            assert int(tc.sum()) == int(c), "taint_counts must split this pod's untolerated-taint count"
+            for b in np.nonzero(tc)[0]:
+                nm = (taint_names or {}).get(int(b), f"taint-{int(b)}")
+                parts.append(f"{int(tc[b])} " + names[k].replace("{taint}", nm))
+        elif k == QS_FIT_TAINT:
+            parts.append(f"{int(c)} node(s) had untolerated taint")
+        else:
+            parts.append(f"{int(c)} {names[k]}")
+    parts.sort()
     msg = f"0/{n_nodes} nodes are available:"
     return msg + (f" {', '.join(parts)}." if parts else "")
 

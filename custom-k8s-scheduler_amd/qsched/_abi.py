@@ -25,7 +25,9 @@ QS_AA_NONE, QS_AA_HOSTNAME, QS_AA_ZONE = 0, 1, 2
 QS_MAX_SCORE_RES = 4
 # qs_fit_reason: FitError reason columns of qs_stream_fit_errors, with upstream's reason strings
 FIT_REASONS = ["Too many pods", "Insufficient cpu", "Insufficient memory", "Insufficient {ext0}",
-               "Insufficient {ext1}", "node(s) had untolerated taint", "node(s) didn't match Pod's node affinity/selector"]
+               "Insufficient {ext1}", "node(s) had untolerated taint {{{taint}}}",
+               "node(s) didn't match Pod's node affinity/selector"]
+QS_FIT_TAINT = 5
 # qs_resource: scoring-resource ids ("ext0" / "ext1" = the table's extended-resource columns)
 RESOURCES = {"cpu": 1, "memory": 2, "ext0": 3, "ext1": 4}
 
@@ -153,6 +155,7 @@ _SIGS = {
     "qs_stream_results": (ctypes.c_int, [_P, _P, _P, _P]),
     "qs_stream_stamps": (ctypes.c_int, [_P, _P, _P]),
     "qs_stream_fit_errors": (ctypes.c_int, [_P, _P, _P, ctypes.c_uint32, _P]),
+    "qs_stream_fit_taints": (ctypes.c_int, [_P, _P, _P, ctypes.c_uint32, _P, _P]),
     "qs_stream_free": (ctypes.c_int, [_P, _P]),
     "qs_pod_from_containers": (ctypes.c_int, [_P, ctypes.c_uint32, _P, _P]),
     "qs_compute_qos": (ctypes.c_int32, [_P, ctypes.c_uint32]),

@@ -170,12 +170,14 @@ def _count(op, params):
     return int(params[p])
 
 
-def load(path_or_text, workload=None, testcase=None):
+def load(path_or_text, workload=None, testcase=None, names=False):
     """Parse a workload file; returns (nodes, pods, profile) for the chosen test case/workload.
 
     nodes: canonical node columns (qsched.empty_nodes layout); pods: POD_DTYPE array in creation
     order; profile: {"enable_taint", "enable_affinity"} switched on when the file uses taints,
-    tolerations, node selectors or node affinity."""
+    tolerations, node selectors or node affinity.  names=True adds a fourth item, {"taints":
+    {bit: "key: value"}}, the interned taint dictionary FitError texts name taints with
+    (qsched.fit_error_message's taint_names)."""
     text = path_or_text
     if "\n" not in str(path_or_text):
         with open(path_or_text) as f:
@@ -244,7 +246,10 @@ def load(path_or_text, workload=None, testcase=None):
         pods[j] = rec
     for i, (_, labels) in enumerate(node_specs):
         nodes["label_bits"][i] = it.label_bits(labels)
-    return nodes, pods, {"enable_taint": int(uses_taint), "enable_affinity": int(uses_aff)}
+    prof = {"enable_taint": int(uses_taint), "enable_affinity": int(uses_aff)}
+    if names:
+        return nodes, pods, prof, {"taints": {b: f"{t['key']}: {t['value']}" for b, t in enumerate(it.taints)}}
+    return nodes, pods, prof
 
 
 def _containers(spec, it):

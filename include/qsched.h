@@ -282,11 +282,21 @@ typedef enum qs_fit_reason {
     QS_FIT_MEMORY = 2,        /* "Insufficient memory" */
     QS_FIT_EXT0 = 3,          /* "Insufficient <extended resource 0>" */
     QS_FIT_EXT1 = 4,          /* "Insufficient <extended resource 1>" */
-    QS_FIT_TAINT = 5,         /* "node(s) had untolerated taint" */
+    QS_FIT_TAINT = 5,         /* "node(s) had untolerated taint {key: value}" (split per taint:
+                               * qs_stream_fit_taints) */
     QS_FIT_AFFINITY = 6,      /* "node(s) didn't match Pod's node affinity/selector" */
     QS_FIT_REASONS = 7
 } qs_fit_reason;
 QS_API qs_status qs_stream_fit_errors(qs_ctx *ctx, qs_stream *s, const uint32_t *pods, uint32_t m, uint32_t *counts);
+/* The same counts, plus the QS_FIT_TAINT nodes split by taint (UP plugins/tainttoleration/
+ * taint_toleration.go#Filter: "node(s) had untolerated taint {%s: %s}" names the FIRST untolerated
+ * NoSchedule / NoExecute taint of the node, one reason string per distinct taint, which FitError.Error()
+ * counts separately).  taint_counts = m x 64: per pod, per interned taint bit b, the nodes whose first
+ * untolerated hard taint is bit b (the lowest set bit of taint_hard & ~tol_hard; the interning order
+ * stands for the node's taint order, exact when every node lists its taints in interning order, as
+ * the workload loader's and the synthetic generator's nodes do).  Row sums equal counts[QS_FIT_TAINT]. */
+QS_API qs_status qs_stream_fit_taints(qs_ctx *ctx, qs_stream *s, const uint32_t *pods, uint32_t m, uint32_t *counts,
+                                      uint32_t *taint_counts);
 
 /* ---- host helpers (spec S2/S3, spec/synth.md) ---- */
 QS_API qs_status qs_pod_from_containers(const qs_container *c, uint32_t nc, const int64_t *overhead_cpu_mem,

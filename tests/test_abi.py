@@ -87,7 +87,8 @@ def test_open_without_device_returns_status():
     bad.abi_version = 7
     assert lib.qs_open(ctypes.byref(bad), 0, ctypes.byref(ctx)) == _abi.QS_EINVAL
     assert lib.qs_close(None) == _abi.QS_EINVAL
-    assert lib.qs_last_error(None) == b"null context"
+    # no context: qs_last_error(NULL) says why this thread's last qs_open failed
+    assert b"abi_version" in lib.qs_last_error(None) or b"version" in lib.qs_last_error(None)
 
 
 # ---- spec S2 / S3 (UP component-helpers/resource#PodRequests, qos.go#ComputePodQOS) ----------

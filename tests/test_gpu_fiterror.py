@@ -101,3 +101,64 @@ def test_fit_errors_refuse_after_table_change():
         with pytest.raises(QschedError, match="changed after"):
             st.fit_errors()
         st.free()
+
+
+@pytest.mark.parametrize("cfg,config,n,p", [(CFG4, 4, 400, 9000), (dict(CFG4, **GPU_CFG), 4, 400, 6000)],
+                         ids=["config4-tight", "config4-gpu-scoring"])
+def test_fit_errors_split_by_taint(oracle, cfg, config, n, p):
+    """upstream's TaintToleration reason names the node's first untolerated taint, so
+    FitError.Error() counts each taint separately.  qs_stream_fit_taints splits the untolerated-taint
+    column per taint bit (the lowest untolerated hard bit); the split must sum to the column and match
+    a numpy replay of the same rule at every unschedulable pod's turn."""
+    nodes, pods = synth_generate(config, n, p)
+    with Scheduler(dict(cfg, engine="lookahead")) as s:
+        s.load_nodes(nodes)
+        st = s.prepare(pods)
+        st.run()
+        idx, counts, tcounts = st.fit_errors(by_taint=True)
+        idx2, counts2 = st.fit_errors()
+        st.free()
+    assert np.array_equal(idx, idx2) and np.array_equal(counts, counts2)
+    assert np.array_equal(tcounts.sum(axis=1), counts[:, 5])
+    if "w_fit" not in str(cfg) and "fit_resources" not in cfg:
+        assert counts[:, 5].any()  # (the tight config-4 stream has taint rejections to split)
+    op = pods_from_struct(pods)
+    th = nodes["taint_hard"].astype(np.uint64)  # static during the stream
+    for q, j in enumerate(idx):
+        un = th & ~np.uint64(op["tol_hard"][int(j)])
+        first = np.array([int(u & (~u + np.uint64(1))).bit_length() - 1 for u in un[un != 0]], np.int64)
+        ref = np.bincount(first, minlength=64) if first.size else np.zeros(64, np.int64)
+        assert np.array_equal(tcounts[q].astype(np.int64), ref), int(j)
+    names = {b: f"key{b}: v{b}" for b in range(64)}
+    if not counts[:, 5].any():
+        return
+    q = int(np.nonzero(counts[:, 5])[0][0])
+    msg = fit_error_message(counts[q], n, ("amd.com/gpu", "ext1"), tcounts[q], names)
+    for b in np.nonzero(tcounts[q])[0]:
+        assert f"{int(tcounts[q][b])} node(s) had untolerated taint {{key{b}: v{b}}}" in msg
+    parts = msg.split(": ", 1)[1].rstrip(".").split(", ")
+    assert parts == sorted(parts)  # Go's sort.Strings over the "count reason" strings
+
+
+def test_fit_errors_named_taints_from_a_workload():
+    """The golden workload's GPU nodes carry {amd.com/gpu: present} (NoSchedule): a pod without the
+    toleration that fits nowhere else reports that taint by name, as upstream's FitError text does."""
+    import os
+    from qsched import workload
+    path = os.path.join(os.path.dirname(__file__), "golden", "workloads", "qos_mix.yaml")
+    nodes, pods, prof, names = workload.load(path, names=True)
+    assert "amd.com/gpu: present" in names["taints"].values()
+    # one pod asking for more cpu than any untainted node has: every node rejects it
+    big = pods[:1].copy()
+    big["req_cpu"] = big["nz_cpu"] = 48_000
+    big["tol_hard"] = 0
+    with Scheduler(dict(prof, engine="lookahead")) as s:
+        s.load_nodes(nodes)
+        st = s.prepare(big)
+        st.run()
+        idx, counts, tcounts = st.fit_errors(by_taint=True)
+        st.free()
+    assert list(idx) == [0]
+    msg = fit_error_message(counts[0], len(nodes["alloc_cpu"]), taint_names=names["taints"], taint_counts=tcounts[0])
+    assert "node(s) had untolerated taint {amd.com/gpu: present}" in msg, msg
+    assert "Insufficient cpu" in msg, msg

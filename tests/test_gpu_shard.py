@@ -100,6 +100,26 @@ def test_allreduce_engine_one_rank(oracle, config, n, p, prof):
     assert_same(g[:2], o[:2], g[2], o[2])
 
 
+@pytest.mark.parametrize("V", [2, 3, 8])
+@pytest.mark.parametrize("config,n,p,prof", [(2, 3000, 2000, {}), (4, 2000, 1500, "norm"), (4, 2500, 1500, "gpu-scoring")])
+def test_allreduce_engine_virtual_world(oracle, V, config, n, p, prof):
+    """The per-pod all-reduce engine of a V-rank world in one process: the one-rank
+    context scans each rank's node range [r*n/V, (r+1)*n/V) in turn into the same scratch — partial
+    normalize maxima by atomicMax, partial keys max-into-best, as ncclAllReduce(max) combines the
+    ranks' values — then commits the one Reserve every rank would apply.  The shard partition, the
+    max over shards (ties across a shard edge resolve to the lower node index through the packed
+    key) and the replicated commit are checked bit-exact against the oracle, placements, keys and the
+    final table.  (A real two-rank communicator needs two devices: test_gpu_rccl_world2.py.)"""
+    from test_gpu_parity import CFG4
+    from rescfg import GPU_CFG
+    cfg = {} if not prof else (CFG4 if prof == "norm" else dict(CFG4, **GPU_CFG))
+    nodes, pods = synth_generate(config, n, p)
+    g = run_sharded(nodes, pods, dict(cfg, engine="allreduce", virtual_shards=V), shard=(0, 1, dist_unique_id()))
+    assert g[3]["engine_used"] == "allreduce"
+    o = run_oracle(oracle, nodes, pods, cfg)
+    assert_same(g[:2], o[:2], g[2], o[2])
+
+
 def test_allreduce_engine_needs_a_communicator():
     """Without an RCCL communicator the per-pod all-reduce engine refuses to run (QS_ESTATE)."""
     from qsched import QschedError, Scheduler
