@@ -42,12 +42,25 @@ WORKLOADS = {
                                    "node table sharded across ranks (list exchange per window)"),
     "config4": (4, 5000, 150000, "config4: 5,000 nodes x 150,000 pods, exact sequential, Fit + "
                                  "Balanced + TaintToleration + NodeAffinity + amd.com/gpu"),
+    "config4_gpu_scoring": (4, 5000, 150000, "config4 with the AMD-GPU scoring resources: 5,000 nodes x "
+                                             "150,000 pods, LeastAllocated {cpu:1, memory:1, amd.com/gpu:5}, "
+                                             "BalancedAllocation over [cpu, memory, amd.com/gpu], TaintToleration "
+                                             "+ NodeAffinity"),
     "config5": (5, 10000, 200000, "config5: 10,000 nodes x 200,000 pods, BATCHED mode (spec S11: "
                                   "64-pod batches, one pod per node per batch, hostname/zone "
                                   "anti-affinity over 1,000 apps) - approximate, reported separately"),
 }
 MODE = {"config5": "batched"}
-PROFILE = {"config4": {"enable_taint": 1, "enable_affinity": 1}}  # plugin switches per workload
+PROFILE = {"config4": {"enable_taint": 1, "enable_affinity": 1},  # plugin switches per workload
+           # NodeResourcesFitArgs.ScoringStrategy.Resources / BalancedAllocationArgs.Resources of an
+           # AMD-GPU cluster (BASELINE.json configs[3]; spec S5): the kFeatRes kernels
+           "config4_gpu_scoring": {"enable_taint": 1, "enable_affinity": 1,
+                                   "fit_resources": [("cpu", 1), ("memory", 1), ("ext0", 5)],
+                                   "balanced_resources": ["cpu", "memory", "ext0"]}}
+# algorithmic bytes per pod x node evaluation of the normalizing profiles: the 8 state columns (32 B),
+# the two extended-resource columns (8 B) and the taint / label mask row (32 B)
+B_NODE_NORM = 72
+C4G_INST = "<23u,"  # k_la_stream_res<kFeatRes | kFeatExt | kFeatTaint | kFeatAffinity, ...> (qs_kernels_res.inc)
 B_NODE = 32  # algorithmic bytes per pod×node evaluation (8 int32 columns)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md:36 (spec); 6,290 GB/s measured
 KERNEL_NAMES = {"resolve": "k_la_resolve4", "select": "k_la_select", "persistent": "k_persistent",
@@ -71,7 +84,8 @@ def parse(argv=None):
                     help="skip the end-to-end, framework-path and wide-layout legs")
     ap.add_argument("--transport", default="mailbox", choices=["mailbox", "rccl"],
                     help="sharded exchange (N > 1): peer-memory mailbox over xGMI, or RCCL all-gather")
-    ap.add_argument("--leg", default=None, choices=["config2", "wide", "config3", "config4", "config5", "framework"],
+    ap.add_argument("--leg", default=None, choices=["config2", "wide", "config3", "config4", "config4_gpu_scoring",
+                                                    "config5", "framework"],
                     help="run only this sub-leg on one GPU and print its JSON object (iteration probe, "
                          "not the bench line)")
     ap.add_argument("--rccl-sample", type=int, default=20000,
@@ -261,35 +275,39 @@ def diag_runs(cx, nodes, pods, cfg, sharded):
     return p50, p99, kp, split
 
 
-def roofline(kp, n_nodes, n_pods, fallback_s):
+def roofline(kp, n_nodes, n_pods, fallback_s, b_node=B_NODE, inst=None):
     """Dominant kernel (most device time in the profiled run): algorithmic bytes per launch =
     (pod x node evaluations it completes per launch) x B_node / mean launch time."""
     dom = max(kp, key=lambda k: kp[k]["s"]) if kp else None
     avg_s = kp[dom]["s"] / kp[dom]["launches"] if dom else fallback_s
     units = n_pods * n_nodes / (kp[dom]["launches"] if dom else 1)
-    achieved = units * B_NODE / avg_s / 1e9
+    achieved = units * b_node / avg_s / 1e9
     kname = KERNEL_NAMES.get(dom, dom)
-    traffic = pmc_traffic(kname) if dom else None
+    traffic, tk = pmc_traffic(kname, inst) if dom else (None, None)
     return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5),
             "traffic": None if traffic is None else round(traffic),
             "kernel": kname, "avg_launch_us": round(avg_s * 1e6, 3),
-            "bytes_per_launch": round(units * B_NODE)}
+            "bytes_per_launch": round(units * b_node), "bytes_per_eval": b_node, "traffic_kernel": tk}
 
 
-def pmc_traffic(kernel_prefix):
-    """HBM bytes per launch of `kernel_prefix` from the committed rocprofv3 PMC summary
+def pmc_traffic(kernel_prefix, inst=None):
+    """HBM bytes per launch of `kernel_prefix` (and, if given, the template-argument prefix `inst`,
+    e.g. "<23u," for one feature class) from the committed rocprofv3 PMC summary
     (profiles/*_pmc_summary.csv, tools/summarize_pmc.py: separate FETCH_SIZE and WRITE_SIZE
-    passes, 2 x FETCH_SIZE + WRITE_SIZE per MI355X_MICROARCH.md:298).  None if not collected."""
+    passes, 2 x FETCH_SIZE + WRITE_SIZE per MI355X_MICROARCH.md:298), with the matched row's
+    kernel name.  (None, None) if not collected."""
     import csv
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.csv")))
     if not files:
-        return None
+        return None, None
     for row in csv.DictReader(open(files[-1])):
-        if row["kernel"].split("<")[0].endswith(kernel_prefix):
-            return float(row["hbm_bytes_per_launch"])
-    return None
+        name = row["kernel"]
+        base, _, targs = name.partition("<")
+        if base.endswith(kernel_prefix) and (inst is None or ("<" + targs).startswith(inst)):
+            return float(row["hbm_bytes_per_launch"]), name
+    return None, None
 
 
 _T0 = time.time()
@@ -573,7 +591,8 @@ def check_stream(m):
     from qsched.checks import stream_invariants
 
     norm = bool(m["cfg"].get("enable_taint") or m["cfg"].get("enable_affinity"))
-    ocfg = {k: m["cfg"][k] for k in ("enable_taint", "enable_affinity") if k in m["cfg"]}
+    ocfg = {k: m["cfg"][k] for k in ("enable_taint", "enable_affinity", "fit_resources", "balanced_resources")
+            if k in m["cfg"]}
     on = {k: v.copy() for k, v in m["nodes"].items()}
     sub = qsched.pods_from_struct(m["pods"])
     t0 = time.perf_counter()
@@ -654,7 +673,7 @@ def scan_roofline(cx, a, n_nodes=1 << 24, n_pods=32):
             "oracle_16t_s": round(oracle_s, 2),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": pmc_traffic("k_scan_soa"), "kernel": "k_scan_soa",
+                         "traffic": pmc_traffic("k_scan_soa")[0], "kernel": "k_scan_soa",
                          "avg_launch_us": round(avg * 1e6, 2),
                          "bytes_per_launch": n_nodes * B_NODE}}
 
@@ -781,10 +800,14 @@ def run_leg(cx, a, leg):
     if leg == "framework":
         return framework_leg(cx)
     steps = 1 if leg == "config3" else 3
-    m = measure(cx, a, leg, steps, 1, with_diag=False)
+    gs = leg == "config4_gpu_scoring"
+    m = measure(cx, a, leg, steps, 1, with_diag=gs)
     out = {"workload": m["desc"], "value": round(m["value"], 1), "unit": "pods/s",
            "ms_per_step": round(m["ms_per_step"], 3), "engine": m["engine"], "launch": m["launch"],
            "unschedulable_frac": round(m["unschedulable_frac"], 5)}
+    if gs:
+        out["roofline"] = roofline(m["kp"], m["n_nodes"], m["n_pods"], m["wall_fallback"], b_node=B_NODE_NORM,
+                                   inst=C4G_INST)
     out["check"] = check_batched(m) if leg == "config5" else check_stream(m)
     return out
 
@@ -819,12 +842,14 @@ def main():
                 rccl = measure_rccl_per_pod(cx, a)
             except Exception as e:  # reported, not fatal (every rank fails it at the same point)
                 rccl = {"error": repr(e)[:300]}
-    c3 = c4 = c5 = scan = None
+    c3 = c4 = c4g = c5 = scan = None
     if cx.world == 1 and workload == "config2" and not a.no_config3:
         progress("config3 leg")
         c3 = measure(cx, a, "config3", 1, 1, with_diag=False)
         progress("config4 leg")
         c4 = measure(cx, a, "config4", 3, 1, with_diag=False)
+        progress("config4 leg with the AMD-GPU scoring resources")
+        c4g = measure(cx, a, "config4_gpu_scoring", 3, 1, with_diag=True)
         progress("config5 leg")
         c5 = measure(cx, a, "config5", 3, 1, with_diag=False)
     if cx.world == 1 and not a.no_scan:
@@ -837,7 +862,8 @@ def main():
         fw = framework_leg(cx)
         wide = wide_leg(cx, a)
     if cx.rank == 0:
-        rl = roofline(m["kp"], m["n_nodes"], m["n_pods"], m["wall_fallback"])
+        rl = roofline(m["kp"], m["n_nodes"], m["n_pods"], m["wall_fallback"],
+                      inst="<0u," if not m["sharded"] and workload == "config2" else None)
         if m["sharded"]:
             how = ("RCCL all-gather per window" if TRANSPORT["name"] == "rccl" else
                    "peer-memory mailbox, shard lists exchanged in-launch" if m["launch"] == "resident" else
@@ -892,6 +918,16 @@ def main():
                               "engine": c4["engine"], "launch": c4["launch"],
                               "unschedulable_frac": round(c4["unschedulable_frac"], 5),
                               "check": check_stream(c4)}
+        if c4g is not None:
+            out["config4_gpu_scoring"] = {
+                "workload": c4g["desc"], "value": round(c4g["value"], 1), "unit": "pods/s",
+                "evals_per_s": round(c4g["value"] * c4g["n_nodes"], 1),
+                "ms_per_step": round(c4g["ms_per_step"], 3), "steps": 3, "engine": c4g["engine"],
+                "launch": c4g["launch"], "unschedulable_frac": round(c4g["unschedulable_frac"], 5),
+                "vs_config4": round(c4g["value"] / c4["value"], 4),
+                "roofline": roofline(c4g["kp"], c4g["n_nodes"], c4g["n_pods"], c4g["wall_fallback"],
+                                     b_node=B_NODE_NORM, inst=C4G_INST),
+                "check": check_stream(c4g)}
         if c5 is not None:
             out["config5_batched"] = {"workload": c5["desc"], "value": round(c5["value"], 1),
                                       "unit": "pods/s", "evals_per_s": round(c5["value"] * c5["n_nodes"], 1),

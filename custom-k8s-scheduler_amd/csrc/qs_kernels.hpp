@@ -2195,9 +2195,12 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
                     // compact rows: a lane issues the loads of kSelB nodes (rows and masks) before it
                     // decodes any (one round trip per group instead of one per node), then scores them
                     // one after another
+                    // (configurable scoring resources at 16 nodes per lane: two nodes per group, so the
+                    // kernel stays within 256 VGPRs without spills — tests/test_kernel_resources.py)
+                    constexpr int SB = ((F & kFeatRes) != 0 && E >= 16) ? 2 : kSelB;
 #pragma unroll
-                    for (int j0 = 0; j0 < E; j0 += kSelB) {
-                        constexpr int B = E < kSelB ? E : kSelB;
+                    for (int j0 = 0; j0 < E; j0 += SB) {
+                        constexpr int B = E < SB ? E : SB;
                         RowQ q[B];
                         DMask mk[B];
 #pragma unroll
@@ -2481,7 +2484,7 @@ constexpr size_t res_stream_lds_bytes(uint32_t n) {
     if ((F & kFeatNorm) != 0)
         b += 2 * kResNormK * (sizeof(DPodX) + sizeof(NormInfo) + sizeof(double2)) + 2 * 64 * sizeof(RowX) +
              64 * sizeof(RowX) + 64 * (sizeof(RowT<F>) + sizeof(RowX)) + 2 * 64 * 4 + 64 * 4 + 16 * 4 + 8 * 8 + 16 +
-             2 * kResNormK * kResTStride * 4 + 2 * 64 * 4 + 2 * kResNormK * 4;
+             2 * kResNormK * kResTStride * 4 + 2 * 64 * 4 + 2 * kResNormK * 4 + 64 * sizeof(DMask);
     return b;
 }
 // QS_RES_DIAG_BLOCK build (experiments): per-role busy shader cycles per pod step, barrier exit
@@ -2505,13 +2508,13 @@ constexpr bool kResDiag = false;
 template <uint32_t F>
 __device__ __forceinline__ uint64_t res_rescan_pass(const DevTable &t, const PodT<F> &p, const DPodX &pxi,
                                                     const uint32_t *dirty, const uint32_t *sidx, const RowT<F> *srow,
-                                                    const RowX *sxr, uint32_t *red_m, uint64_t *red_k,
-                                                    const uint32_t *snd, const DevCfg &cv) {
+                                                    const RowX *sxr, const DMask *smask, uint32_t *red_m,
+                                                    uint64_t *red_k, const uint32_t *snd, const DevCfg &cv) {
     __syncthreads();  // R1: slots staged
     const int lane = threadIdx.x & 63;
     const uint32_t wid = (threadIdx.x >> 6) - 4;
     const uint32_t n = t.n, nds = *snd;
-    constexpr uint32_t U = 4;
+    constexpr uint32_t U = 2;  // (rows per lane in flight: 4 put the normalizing kernels over 256 VGPRs)
     auto rows_at = [&](uint32_t b0, RowT<F>(&r)[U], RowX(&x)[U]) {
 #pragma unroll
         for (uint32_t u = 0; u < U; ++u) {
@@ -2527,6 +2530,8 @@ __device__ __forceinline__ uint64_t res_rescan_pass(const DevTable &t, const Pod
                 while (j + 1 < nds && sidx[j] != idx) ++j;  // dirty <=> held by a slot
                 r[u] = srow[j];
                 x[u] = sxr[j];
+                const DMask m = smask[j];
+                x[u].th = m.th; x[u].ts = m.ts; x[u].lb0 = m.lb0; x[u].lb1 = m.lb1;
             }
         }
     };
@@ -2633,7 +2638,11 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
     uint32_t *Tcur = (uint32_t *)base; base += kResNormK * kResTStride * 4;
     uint32_t *Tnext = (uint32_t *)base; base += kResNormK * kResTStride * 4;
     uint32_t(*stS)[64] = (uint32_t(*)[64])base; base += 2 * 64 * 4;
-    uint32_t(*nflag2)[kResNormK] = (uint32_t(*)[kResNormK])base;
+    uint32_t(*nflag2)[kResNormK] = (uint32_t(*)[kResNormK])base; base += 2 * kResNormK * 4;
+    // NORM: the taint / label masks of the current slots by slot lane (waves A / B carry only a
+    // slot's extended resources: the masks are written by wave 6 when a slot is created, by wave A
+    // at a window boundary for the inherited ones, and read by rescans and the boundary)
+    DMask *smask = (DMask *)base;
     const ResPub none{0, 0xFFFFFFFFu, -1, -1, 0, {0, 0}};
     const DPodX px{};
     // the LeastAllocated weights and weight-sum reciprocals held in VGPRs: the score's per-lane
@@ -2670,7 +2679,8 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
     // NORM: exact rescan of window pod i by the parked waves (res_rescan_pass); the pipeline waves
     // keep the barrier count (res_rescan_wait) and read its key
     auto rescan_pass = [&](uint32_t i, uint32_t wb) -> uint64_t {
-        return res_rescan_pass<F>(t, wpods2[wb][i], wpodx2[wb][i], dirty, sidx, srow, sxr, red_m, red_k, snd, cv);
+        return res_rescan_pass<F>(t, wpods2[wb][i], wpodx2[wb][i], dirty, sidx, srow, sxr, smask, red_m, red_k, snd,
+                                  cv);
     };
 
     if (wv == 0) {
@@ -2885,8 +2895,9 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
             } else {
                 if ((uint32_t)lane == pv.nd_old) {
                     S = stage[pp][pv.src];
-                    if constexpr (NORM) {
-                        SX = stagexN[pp][pv.src];
+                    if constexpr (NORM) {  // (the extended resources only: masks in smask)
+                        const int4 e = *reinterpret_cast<const int4 *>(&stagexN[pp][pv.src]);
+                        SX.ae0 = e.x; SX.re0 = e.y; SX.ae1 = e.z; SX.re1 = e.w;
                         snew = stS[pp][pv.src];
                     } else if (F & kFeatExt) {
                         const int4 e = stagex[pp][pv.src];
@@ -2899,7 +2910,10 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
         };
         // NORM: D stopped at window pod j: stage the slot rows (wave A), rescan with every wave
         auto rescan_ab = [&](uint32_t j, uint32_t wb) {
-            if (wv == 1 && (uint32_t)lane < nd) { srow[lane] = S; sxr[lane] = SX; }
+            if (wv == 1 && (uint32_t)lane < nd) {  // (the rescan takes the slot masks from smask)
+                srow[lane] = S;
+                *reinterpret_cast<int4 *>(&sxr[lane]) = make_int4(SX.ae0, SX.re0, SX.ae1, SX.re1);
+            }
             (void)res_rescan_wait(red_k);
             (void)j;
             (void)wb;
@@ -2969,8 +2983,12 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
             if (wv == 1 && keep) {
                 store_row_coh<F>(t, rs, xnode[lane], S, SX);
                 carry[rk] = S;
-                if constexpr (NORM) carryxN[rk] = SX;
-                else carryx[rk] = make_int4(SX.ae0, SX.re0, SX.ae1, SX.re1);
+                if constexpr (NORM) {
+                    const DMask m = smask[lane];
+                    carryxN[rk] = RowX{SX.ae0, SX.re0, SX.ae1, SX.re1, m.th, m.ts, m.lb0, m.lb1};
+                } else {
+                    carryx[rk] = make_int4(SX.ae0, SX.re0, SX.ae1, SX.re1);
+                }
             }
             if (wv == 1) pend = w + 1;
             __syncthreads();  // B3
@@ -2978,7 +2996,10 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
             if ((uint32_t)lane < nd) {
                 S = carry[lane];
                 if constexpr (NORM) {
-                    SX = carryxN[lane];
+                    const RowX o = carryxN[lane];
+                    SX = RowX{};
+                    SX.ae0 = o.ae0; SX.re0 = o.re0; SX.ae1 = o.ae1; SX.re1 = o.re1;
+                    if (wv == 1) smask[lane] = DMask{o.th, o.ts, o.lb0, o.lb1};
                 } else {
                     const int4 e = carryx[lane];
                     SX.ae0 = e.x; SX.re0 = e.y; SX.ae1 = e.z; SX.re1 = e.w;
@@ -3261,6 +3282,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                 if (pv.ks == 0 || pv.slot >= 0) return;
                 const RowX sx = stagexN[j & 1][pv.src];
                 const uint32_t l = pv.nd_old;
+                if (lane == 0) smask[l] = DMask{sx.th, sx.ts, sx.lb0, sx.lb1};
                 const uint32_t st = static_raw(sx.th, sx.ts, sx.lb0, sx.lb1, myf, myx);
                 if (lane < 32) {
                     if (cur && qq >= j + 3 && qq < kend) Tcur[qq * kResTStride + l] = st;
