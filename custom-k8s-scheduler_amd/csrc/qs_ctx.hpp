@@ -171,7 +171,18 @@ struct qs_ctx {
     bool mbox_fine = false;  // the mailbox is fine-grained device memory (hipDeviceMallocFinegrained)
     bool mbox_broken = false;  // a mailbox wait timed out: the ranks are out of step until every
                                // rank calls qs_dist_mailbox_connect again
+    // QS_MBOX_HOST=1 at qs_dist_mailbox_export: every rank's mailbox is POSIX shared host memory
+    // registered with HIP (mapped, the GPU reads and writes it over the host link), so no GPU L2 is
+    // shared by the ranks' mailboxes even with every rank on one GPU (the test form of the
+    // cross-device protocol).  mbox.p is then the device alias of the own mapping.
+    bool mbox_host = false;
+    void *mbox_hptr = nullptr;                        // own mapping (host address)
+    std::string mbox_shm;                             // own segment name (unlinked at close)
+    std::vector<void *> mbox_hmaps;                   // peers' mappings (host addresses)
 };
+namespace qs_host {
+void mbox_host_release(qs_ctx *c);  // qs_dist.cpp: unregister / unmap the host-memory mailboxes
+}
 
 namespace qs_host {
 // Node shards of the LOOKAHEAD select for this context: W shards in total, this process scores

@@ -560,6 +560,19 @@ __device__ __forceinline__ uint32_t div_small(uint32_t num, uint32_t den) {
     q = r >= (int32_t)den ? q + 1 : q;
     return den ? (uint32_t)q : 0u;
 }
+// RN(x / c) for the resource count c in {3, 4} of BalancedAllocation's >= 3-resource path (x >= 0,
+// normal or zero: a sum of fractions or of squared deviations): c = 4 an exact scaling; c = 3
+// Markstein's correction of q0 = RN(x RN(1/3)) (the remainder fma(-q0, 3, x) is exact and one fma with
+// the correctly rounded reciprocal rounds the quotient correctly), in place of the IEEE division's
+// scale / rcp / Newton / fixup sequence on the key chain.  Checked against IEEE division on 80 M
+// cases (tests/native/exact_arith.c mode 5) and by every configurable-resource parity test.
+__device__ __forceinline__ double div_count(double x, uint32_t c) {
+    const double y3 = 0x1.5555555555555p-2;  // RN(1/3)
+    const double q0 = x * y3;
+    const double r = __builtin_fma(-q0, 3.0, x);
+    const double q3 = __builtin_fma(r, y3, q0);
+    return c == 4u ? x * 0.25 : q3;
+}
 // Correctly rounded f64 square root (Go math.Sqrt, SQRTSD): LLVM's gfx950 expansion of llvm.sqrt.f64
 // (scaling, v_rsq_f64, two Newton steps, the fma residual correction), checked bit for bit against
 // the host's sqrt on 33 M inputs by tests/native/sqrt_sweep.hip (tests/test_gpu_sqrt.py).
@@ -645,8 +658,7 @@ __device__ __forceinline__ uint32_t ba_score(const R &r, const RowX &x, const P 
         if (cnt == 2u) {
             sd = __builtin_fabs((fa - fb) / 2);
         } else if (cnt > 2u) {
-            const double dn = (double)cnt;
-            const double mean = tot / dn;  // IEEE division (-ffp-contract=off, no fast-math)
+            const double mean = div_count(tot, cnt);  // = RN(tot / cnt), the IEEE quotient
             double s = 0.0;
 #pragma unroll
             for (int j = 0; j < QS_BAL_MAX; ++j) {
@@ -654,7 +666,7 @@ __device__ __forceinline__ uint32_t ba_score(const R &r, const RowX &x, const P 
                 const double sq = d * d;
                 s = s + (ij[j] ? sq : 0.0);
             }
-            sd = sqrt_rn(s / dn);
+            sd = sqrt_rn(div_count(s, cnt));
         }
     } else {
         (void)x;

@@ -6,6 +6,13 @@
 // replaces K latency-bound 8-byte all-reduces (SURVEY.md §7 H4 option 3).  Every rank then runs the
 // same resolver over the same gathered lists and its replicated table, so placements and table
 // updates are identical on all ranks without a second exchange.
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -150,11 +157,78 @@ qs_status qs_open_shard(const qs_config *cfg, int device, int rank, int world,
     return QS_OK;
 }
 
+}  // extern "C"
+
+namespace qs_host {
+
+// A kMbBytes POSIX shared-memory segment, mapped and registered with HIP; returns the host address.
+static void *mbox_host_map(const char *name, bool create) {
+    const int fd = shm_open(name, create ? (O_CREAT | O_EXCL | O_RDWR) : O_RDWR, 0600);
+    if (fd < 0) fail(QS_EDEVICE, std::string("shm_open ") + name + ": " + std::strerror(errno));
+    if (create && ftruncate(fd, (off_t)kMbBytes) != 0) {
+        ::close(fd);
+        fail(QS_EDEVICE, std::string("ftruncate ") + name);
+    }
+    void *h = mmap(nullptr, kMbBytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    ::close(fd);
+    if (h == MAP_FAILED) fail(QS_EDEVICE, std::string("mmap ") + name);
+    if (hipHostRegister(h, kMbBytes, hipHostRegisterMapped) != hipSuccess) {
+        (void)hipGetLastError();
+        munmap(h, kMbBytes);
+        fail(QS_EDEVICE, std::string("hipHostRegister ") + name);
+    }
+    return h;
+}
+static char *mbox_host_dev(void *h) {
+    void *d = nullptr;
+    HIPCHK(hipHostGetDevicePointer(&d, h, 0));
+    return static_cast<char *>(d);
+}
+void mbox_host_release(qs_ctx *c) {
+    if (!c->mbox_host) return;
+    for (void *h : c->mbox_hmaps) {
+        (void)hipHostUnregister(h);
+        munmap(h, kMbBytes);
+    }
+    c->mbox_hmaps.clear();
+    if (c->mbox_hptr) {
+        (void)hipHostUnregister(c->mbox_hptr);
+        munmap(c->mbox_hptr, kMbBytes);
+        shm_unlink(c->mbox_shm.c_str());
+    }
+    c->mbox_hptr = nullptr;
+    c->mbox.p = nullptr;  // (the device alias of a host mapping: nothing for DevBuf to free)
+    c->mbox.bytes = 0;
+    c->mbox_host = false;
+}
+
+}  // namespace qs_host
+
+extern "C" {
+
 qs_status qs_dist_mailbox_export(qs_ctx *c, uint8_t handle[64]) {
     if (!c || !handle) return QS_EINVAL;
     std::lock_guard<std::mutex> lk(c->mu);
     try {
         HIPCHK(hipSetDevice(c->device));
+        const char *hm = getenv("QS_MBOX_HOST");
+        if (!c->mbox.p && hm && hm[0] == '1') {
+            // host-memory mailbox: the handle is 'H' + the segment's name
+            static int seq = 0;
+            c->mbox_shm = "/qsched_mb_" + std::to_string((long)getpid()) + "_" + std::to_string(seq++);
+            c->mbox_hptr = mbox_host_map(c->mbox_shm.c_str(), true);
+            c->mbox_host = true;
+            c->mbox.p = mbox_host_dev(c->mbox_hptr);
+            c->mbox.bytes = kMbBytes;
+            std::memset(c->mbox_hptr, 0, kMbBytes);
+            __sync_synchronize();
+        }
+        if (c->mbox_host) {
+            std::memset(handle, 0, 64);
+            handle[0] = 'H';
+            std::memcpy(handle + 1, c->mbox_shm.c_str(), std::min<size_t>(62, c->mbox_shm.size()));
+            return QS_OK;
+        }
         if (!c->mbox.p) {
             // Fine-grained device memory: peers write it over xGMI while this GPU polls
             // its flags and reads its slots, so it must stay coherent with remote writers without
@@ -200,8 +274,18 @@ qs_status qs_dist_mailbox_connect(qs_ctx *c, const uint8_t *handles) {
         // this call on every rank, and each rank restarts from an empty mailbox and sequence 0
         for (void *p : c->mbox_opened) (void)hipIpcCloseMemHandle(p);
         c->mbox_opened.clear();
+        for (void *h : c->mbox_hmaps) {
+            (void)hipHostUnregister(h);
+            munmap(h, kMbBytes);
+        }
+        c->mbox_hmaps.clear();
         c->mbox_on = false;
-        HIPCHK(hipMemset(c->mbox.p, 0, kMbBytes));
+        if (c->mbox_host) {
+            std::memset(c->mbox_hptr, 0, kMbBytes);
+            __sync_synchronize();
+        } else {
+            HIPCHK(hipMemset(c->mbox.p, 0, kMbBytes));
+        }
         HIPCHK(hipDeviceSynchronize());
         c->run_seq = 0;
         c->mbox_broken = false;
@@ -214,8 +298,18 @@ qs_status qs_dist_mailbox_connect(qs_ctx *c, const uint8_t *handles) {
                 bases[(size_t)r] = static_cast<char *>(c->mbox.p);
                 continue;
             }
+            const uint8_t *hr = handles + 64 * (size_t)r;
+            if ((hr[0] == 'H') != c->mbox_host) fail(QS_EINVAL, "mailbox handles of mixed kinds (QS_MBOX_HOST on some ranks only)");
+            if (c->mbox_host) {
+                char name[64] = {0};
+                std::memcpy(name, hr + 1, 62);
+                void *h = mbox_host_map(name, false);
+                c->mbox_hmaps.push_back(h);
+                bases[(size_t)r] = mbox_host_dev(h);
+                continue;
+            }
             hipIpcMemHandle_t h;
-            std::memcpy(&h, handles + 64 * (size_t)r, sizeof h);
+            std::memcpy(&h, hr, sizeof h);
             void *p = nullptr;
             HIPCHK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
             c->mbox_opened.push_back(p);

@@ -870,6 +870,7 @@ qs_status qs_close(qs_ctx *c) {
         c->comm = nullptr;
         for (void *p : c->mbox_opened) (void)hipIpcCloseMemHandle(p);
         c->mbox_opened.clear();
+        mbox_host_release(c);
     }
     hipStream_t s = c->stream, s2 = c->stream2;
     if (s2) (void)hipStreamSynchronize(s2);

@@ -2474,6 +2474,9 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
 // barrier (B0: the window's NormInfo in LDS before wave A's first keys), four per rescan.  The four
 // extra waves also stage the next window's pod extension records (176 B each) in LDS.
 constexpr uint32_t kResNormK = 32;  // window pods whose NORM records are staged per parity (K <= 32)
+// Fit + Balanced (+ext) profiles: stream pods whose list entries / candidate rows sit in the LDS
+// rings of waves 4 (entries) and 5 (rows), indexed by stream pod modulo kResRing
+constexpr uint32_t kResRing = 4;
 constexpr uint32_t kResTStride = 65;
 constexpr size_t kResLdsMax = 96 * 1024;
 constexpr uint32_t kResSgprMax = 112;  // bound on the resident kernels' sgpr_count (checked: tools/kres.sh)  // dynamic LDS of the resident launch (gfx950: up to 160 KiB per workgroup)  // slot statics [pod][lane] rows, padded: both access patterns conflict-free
@@ -2481,6 +2484,8 @@ template <uint32_t F>
 constexpr size_t res_stream_lds_bytes(uint32_t n) {
     size_t b = ((((size_t)n + 31) / 32 + 3) & ~(size_t)3) * 4 + 4 * 2 * 64 * 8 + 2 * 64 * (sizeof(RowT<F>) + sizeof(int4)) +
                2 * sizeof(ResPub) + 3 * 64 * 4 + 64 * (sizeof(RowT<F>) + sizeof(int4)) + 2 * 64 * sizeof(PodT<F>);
+    if ((F & kFeatNorm) == 0)  // the entry / candidate-row rings (kResRing pods) and the late flag
+        b += kResRing * 64 * (8 + sizeof(RowT<F>) + sizeof(int4)) + 16;
     if ((F & kFeatNorm) != 0)
         b += 2 * kResNormK * (sizeof(DPodX) + sizeof(NormInfo) + sizeof(double2)) + 2 * 64 * sizeof(RowX) +
              64 * sizeof(RowX) + 64 * (sizeof(RowT<F>) + sizeof(RowX)) + 2 * 64 * 4 + 64 * 4 + 16 * 4 + 8 * 8 + 16 +
@@ -2643,6 +2648,15 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
     // slot's extended resources: the masks are written by wave 6 when a slot is created, by wave A
     // at a window boundary for the inherited ones, and read by rescans and the boundary)
     DMask *smask = (DMask *)base;
+    // RING (Fit + Balanced (+ext); the NORM arrays above are not allocated then, so the rings start
+    // right after nflag2's slot): stream pod g's list entry per lane (ringE[g % kResRing]), the rows
+    // of those entries (ringR / ringX: extended resources), and wave 4's "next window's lists were
+    // not there in time" flag for C's boundary fallback
+    char *rbase = (char *)(wpodx2);
+    uint64_t(*ringE)[64] = (uint64_t(*)[64])rbase; rbase += kResRing * 64 * 8;
+    RowT<F>(*ringR)[64] = (RowT<F>(*)[64])rbase; rbase += kResRing * 64 * sizeof(RowT<F>);
+    int4(*ringX)[64] = (int4(*)[64])rbase; rbase += kResRing * 64 * sizeof(int4);
+    uint32_t *late = (uint32_t *)rbase;
     const ResPub none{0, 0xFFFFFFFFu, -1, -1, 0, {0, 0}};
     const DPodX px{};
     // the LeastAllocated weights and weight-sum reciprocals held in VGPRs: the score's per-lane
@@ -2669,6 +2683,10 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
     for (uint32_t i = threadIdx.x; i < nwords; i += 256) dirty[i] = 0;
     if (threadIdx.x < min(K, P)) wpods2[0][threadIdx.x] = pods[threadIdx.x];
     if (threadIdx.x == 0) pub[1] = none;
+    if constexpr (!NORM) {  // RING: no entry yet (wave 5 may read a slot before its first write)
+        for (uint32_t j = threadIdx.x; j < kResRing * 64; j += 256) (&ringE[0][0])[j] = 0ull;
+        if (threadIdx.x == 0) *late = 1u;  // window 0: C fetches its first entries and row
+    }
     if constexpr (NORM) {  // window 0's pod extension records
         constexpr uint32_t q = sizeof(DPodX) / 16;
         for (uint32_t j = threadIdx.x; j < min(K, P) * q; j += kResBS)
@@ -2888,20 +2906,26 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
         uint32_t snew = 0;  // NORM: the static of a slot created by the applied winner
         // (the new slot's row is read from LDS at pv.src: a per-lane readlane of the own-lane staged
         // rows instead was measured slower, A / B +90 busy cycles a step)
-        auto apply = [&](const ResPub &pv, int pp, const PodT<F> &pprev) {
+        // gi: the stream pod whose winner pv is (RING: its candidates' rows are ringR[gi % kResRing])
+        auto apply = [&](const ResPub &pv, int pp, const PodT<F> &pprev, uint32_t gi) {
             if (pv.ks == 0) return;
             if (pv.slot >= 0) {
                 if (lane == pv.slot) reserve(S, SX, pprev, +1);
             } else {
                 if ((uint32_t)lane == pv.nd_old) {
-                    S = stage[pp][pv.src];
+                    if constexpr (!NORM) {
+                        S = ringR[gi % kResRing][pv.src];
+                        if (F & kFeatExt) {
+                            const int4 e = ringX[gi % kResRing][pv.src];
+                            SX.ae0 = e.x; SX.re0 = e.y; SX.ae1 = e.z; SX.re1 = e.w;
+                        }
+                    } else {
+                        S = stage[pp][pv.src];
+                    }
                     if constexpr (NORM) {  // (the extended resources only: masks in smask)
                         const int4 e = *reinterpret_cast<const int4 *>(&stagexN[pp][pv.src]);
                         SX.ae0 = e.x; SX.re0 = e.y; SX.ae1 = e.z; SX.re1 = e.w;
                         snew = stS[pp][pv.src];
-                    } else if (F & kFeatExt) {
-                        const int4 e = stagex[pp][pv.src];
-                        SX.ae0 = e.x; SX.re0 = e.y; SX.ae1 = e.z; SX.re1 = e.w;
                     }
                     reserve(S, SX, pprev, +1);
                 }
@@ -2951,7 +2975,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                 }
                 const uint32_t nd0 = nd;
                 QS_RSTAMP_MARK(0)
-                if (i > 0) apply(pv, pp, pprev);
+                if (i > 0) apply(pv, pp, pprev, s0 + i - 1);
                 QS_RSTAMP_MARK(1)
                 if (wv == 1 && pend && i == isig) {
                     // the previous window's rows went out write-through a window boundary ago
@@ -2970,13 +2994,14 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                     const uint32_t st = (nd != nd0 && (uint32_t)lane == nd0) ? snew : tst;
                     (wv == 1 ? keyA : keyB)[par][lane] = slot_key(s2, x2s, pn1, pnc, st);
                 }
+
                 pprev = pcur;
                 pcur = pn1;
                 QS_RSTAMP_END()
                 __syncthreads();
             }
             if (NORM && read_pub(&pub[(kend - 1) & 1]).slot == -2) rescan_ab(kend - 1, w & 1);
-            apply(read_pub(&pub[(kend - 1) & 1]), (kend - 1) & 1, pprev);
+            apply(read_pub(&pub[(kend - 1) & 1]), (kend - 1) & 1, pprev, s0 + kend - 1);
             __syncthreads();  // B2 (D's slot ranks and nodes)
             const uint32_t rk = xrank[lane];
             const bool keep = (uint32_t)lane < nd && rk != 0xFFFFFFFFu;
@@ -3014,7 +3039,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
             drain_stores();
             if (lane == 0) __hip_atomic_store((gu32 *)&ctl->done, pend, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-    } else if (wv == 3) {
+    } else if (NORM && wv == 3) {
         // ---- C: candidate rows, C keys, the next pod's best clean entry; next-window prefetch -----
         uint64_t eX = 0, eY = 0, eZ = 0, c1 = 0;
         // NORM: the statics of pod i's entries (this lane's) against pods i+1 and i+2, published by
@@ -3237,6 +3262,164 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
             bmark(-1);
         }
         if (rdiag && lane == 0) { rdiag[4] = nfallback; rdiag[5] = cdef_; rdiag[6] = cmiss_; }
+    } else if (!NORM && wv == 3) {
+        // ---- C (RING, Fit + Balanced (+ext)): every lane's candidate key and the next pod's best
+        // clean entry.  The entries come from ringE (wave 4) and the candidates' rows from ringR /
+        // ringX (wave 5), so a step issues no global load: C's row no longer waits behind older
+        // sc1 entry loads (vector loads complete in issue order).  A/B read a new slot's row from
+        // ringR as well, so C stages nothing.
+        uint64_t c1 = 0;
+        uint32_t nfallback = 0;
+        auto dirty_bit = [&](uint64_t e) -> bool {
+            const uint32_t nidx = e ? key_node(e) : 0u;
+            return (dirty[nidx >> 5] >> (nidx & 31)) & 1u;
+        };
+        for (uint32_t w = 0; w < nwin; ++w) {
+            const uint32_t s0 = w * K, kend = min(K, P - s0);
+            const PodT<F> *wp = wpods2[w & 1];
+            if (*late) {
+                // the first window, or the lists of this one were not all published when wave 4
+                // looked (three pods before the previous window's end): the entries of pods 0-2 and
+                // the rows of pod 0's entries here, before B1 (wave 4 then continues from pod 3)
+                ++nfallback;
+                const uint64_t *lists = lists0 + (size_t)(w & 1) * lwords;
+                if (lane == 0) (void)res_wait_ge(&ctl->rdy[w & 1][0], (w >> 1) * K + kend, c.werr, res_bound(c, w));
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below)
+                uint64_t e[3];
+#pragma unroll
+                for (uint32_t j = 0; j < 3; ++j)
+                    e[j] = j < kend ? load_coh_u64(lists + (size_t)j * 64 + lane) : 0ull;
+#pragma unroll
+                for (uint32_t j = 0; j < 3; ++j) ringE[(s0 + j) % kResRing][lane] = e[j];
+                const uint32_t n0 = e[0] ? key_node(e[0]) : 0u;
+                ringR[s0 % kResRing][lane] = load_row<F>(t, n0);
+                if (F & kFeatExt) {
+                    const RowX x = load_rowx<F>(t, n0);
+                    ringX[s0 % kResRing][lane] = make_int4(x.ae0, x.re0, x.ae1, x.re1);
+                }
+            }
+            // pod 0's candidates against the dirty set at the window start (the inherited slots)
+            const uint64_t e0 = ringE[s0 % kResRing][lane];
+            c1 = (e0 != 0 && !dirty_bit(e0)) ? e0 : 0ull;
+            C1[1][lane] = c1;
+            if (w > 0) bmark(0);
+            __syncthreads();  // B1
+            PodT<F> pcur = wp[0];  // pod i's record (pod i+1's is read each step)
+            for (uint32_t i = 0; i < kend; ++i) {
+                QS_RSTAMP_BEGIN()
+                const uint32_t g = s0 + i;
+                const int par = i & 1;
+                // the step's LDS reads: pod i+1's entry (then its dirty word: the set through pod
+                // i-1, wave D marks a new slot in the step that creates it), pod i's candidate row
+                // (c1's), pod i+1's record.  C never reads the published winner: a candidate taken
+                // by pod i-1's winner is masked by D, which then never names that lane as a source.
+                const uint64_t en = ringE[(g + 1) % kResRing][lane];
+                const RowT<F> r1 = ringR[g % kResRing][lane];
+                RowX x1{};
+                if (F & kFeatExt) {
+                    const int4 e = ringX[g % kResRing][lane];
+                    x1.ae0 = e.x; x1.re0 = e.y; x1.ae1 = e.z; x1.re1 = e.w;
+                }
+                const PodT<F> pn1 = wp[i + 1];
+                const uint32_t en_node = en ? key_node(en) : 0u;
+                const uint32_t dword = dirty[en_node >> 5];
+                QS_RSTAMP_MARK(0)
+                // keyC: candidate c1's row + pod i, scored for pod i+1 (needs no pub)
+                RowT<F> cr = r1;
+                RowX crx = x1;
+                reserve(cr, crx, pcur, +1);
+                const bool f = feasible<F>(cr, crx, pn1, px);
+                const uint32_t tot = node_total<F>(cr, crx, pn1, px, cv, 0, 0.0, 0, 0.0, nullptr);
+                QS_EXP_CAND_KEY(f, tot, cr, pn1)
+                QS_RSTAMP_MARK(1)
+                if (i + 1 < kend) {
+                    keyC[par][lane] = (c1 != 0 && f) ? pack_key(tot + 1, key_node(c1)) : 0ull;
+                    const bool dirt = ((dword >> (en_node & 31)) & 1u) != 0;
+                    c1 = (en != 0 && !dirt) ? en : 0ull;  // pod i+1 against the dirty set through pod i-1
+                    C1[par][lane] = c1;
+                }
+                QS_RSTAMP_MARK(2)
+                pcur = pn1;
+                QS_RSTAMP_END()
+                __syncthreads();
+            }
+            __syncthreads();  // B2
+            __syncthreads();  // B3 (D cleared the dropped slots' dirty bits before B2)
+            bmark(-1);
+        }
+        if (rdiag && lane == 0) { rdiag[4] = nfallback; rdiag[5] = 0; rdiag[6] = 0; }
+    } else if (!NORM && wv == 4) {
+        // ---- wave 4 (RING): list entries three pods ahead.  Step i (stream pod g) writes E(g+2),
+        // whose sc1 load it issued one step earlier (the wait sits at the loop's top, where the
+        // compiler waits for every load in flight anyway), and issues E(g+3).  The next window's
+        // entries need all its lists published: rdy is read at step kend-4 and decided at kend-3
+        // (late = 0: prefetched; else C's fallback at the next window's start).  A wave of its own,
+        // so its loads never sit in front of another wave's.
+        uint64_t ein = 0;   // E(g+2), in flight at the start of step i
+        bool skip = true;   // step 0: E(s0+2) came from C's fallback
+        for (uint32_t w = 0; w < nwin; ++w) {
+            const uint32_t s0 = w * K, kend = min(K, P - s0);
+            const bool hasnext = w + 1 < nwin;
+            const uint32_t knext = hasnext ? min(K, P - s0 - K) : 0u;
+            const uint64_t *lists = lists0 + (size_t)(w & 1) * lwords;
+            const uint64_t *listsn = lists0 + (size_t)((w + 1) & 1) * lwords;
+            const uint32_t tnext = ((w + 1) >> 1) * K + knext;
+            const bool pfw = hasnext && kend >= 6;
+            const uint32_t ic = pfw ? kend - 3 : kend - 1;  // the step that decides the next window's path
+            bool lt = hasnext;
+            uint32_t rdyv = 0;
+            __syncthreads();  // B1
+            for (uint32_t i = 0; i < kend; ++i) {
+                const uint32_t g = s0 + i;
+                if (!(skip && i == 0)) ringE[(g + 2) % kResRing][lane] = ein;
+                if (i == ic) {
+                    if (pfw) lt = !((uint32_t)__builtin_amdgcn_readfirstlane(rdyv) >= tnext);
+                    if (lane == 0) *late = lt ? 1u : 0u;
+                }
+                // E(g+3): this window's pod i+3, or the next window's pod i+3-kend once its lists are in
+                uint64_t v = 0;
+                if (i + 3 < kend) {
+                    v = load_coh_u64(lists + (size_t)(i + 3) * 64 + lane);
+                } else if (i >= ic && !lt && hasnext) {
+                    const uint32_t j = i + 3 - kend;
+                    v = load_coh_u64(listsn + (size_t)min(j, knext - 1) * 64 + lane);
+                    v = j < knext ? v : 0ull;
+                }
+                ein = v;
+                if (pfw && i + 4 == kend) rdyv = load_coh_u32(&ctl->rdy[(w + 1) & 1][0]);
+                __syncthreads();
+            }
+            skip = lt;
+            __syncthreads();  // B2
+            __syncthreads();  // B3
+        }
+    } else if (!NORM && wv == 5) {
+        // ---- wave 5 (RING): the rows of pod g+1's entries (plain loads, issued and waited within
+        // step i) into ringR / ringX for C's step i+1 and A/B's step i+2; the next window's pod 0
+        // only when wave 4 prefetched its entries (late == 0)
+        for (uint32_t w = 0; w < nwin; ++w) {
+            const uint32_t s0 = w * K, kend = min(K, P - s0);
+            const bool hasnext = w + 1 < nwin;
+            const bool pfw = hasnext && kend >= 6;
+            __syncthreads();  // B1
+            for (uint32_t i = 0; i < kend; ++i) {
+                const uint32_t g = s0 + i;
+                const bool go = i + 1 < kend || (pfw ? *late == 0u : !hasnext);
+                if (go) {
+                    const uint64_t e = ringE[(g + 1) % kResRing][lane];
+                    const uint32_t nd = e ? key_node(e) : 0u;
+                    const RowT<F> r = load_row<F>(t, nd);
+                    ringR[(g + 1) % kResRing][lane] = r;
+                    if (F & kFeatExt) {
+                        const RowX x = load_rowx<F>(t, nd);
+                        ringX[(g + 1) % kResRing][lane] = make_int4(x.ae0, x.re0, x.ae1, x.re1);
+                    }
+                }
+                __syncthreads();
+            }
+            __syncthreads();  // B2
+            __syncthreads();  // B3
+        }
     } else if constexpr (NORM) {
         // ---- waves 4-7: slot statics, the rescans' extra hands, the next window's pod records ------
         // Per step (work(i), before the step's barrier; a STOP's rescan of pod i-1 already done):
@@ -3408,8 +3591,8 @@ __global__ __launch_bounds__(kResBS) void k_la_stream_res(DevTable t, const PodT
             __hip_atomic_store(reinterpret_cast<uint64_t *>(rsh.peers[r] + rsh.hello) + rsh.rank, rsh.seq,
                                __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    if ((F & kFeatNorm) == 0 && threadIdx.x >= 256) {
-        // not a pipeline wave: the same barrier count (1 + per window kend + 3)
+    if ((F & kFeatNorm) == 0 && threadIdx.x >= 384) {
+        // waves 6-7 (waves 4-5 fill the entry / row rings): the same barrier count (1 + per window kend + 3)
         __syncthreads();
         for (uint32_t w = 0; w < nwin; ++w)
             for (uint32_t j = 0, nb = min(K, P - w * K) + 3; j < nb; ++j) __syncthreads();

@@ -6,6 +6,9 @@
  *   least_requested_w(a, reqd, RN(1/a)) == ((a - reqd) * 100) / a   (f64 quotient + one fma-exact
  *                                                                      integer correction)
  *   fraction_w(a, r, RN(1/a)) == min(RN(r/a), 1)                     (the same Markstein quotient)
+ *   div_count(x, c) == RN(x / c), c in {3, 4}: BalancedAllocation's mean and variance over three or
+ *   four resources (x >= 0 normal or zero; c = 4 an exact scaling, c = 3 Markstein's correction
+ *   fma(fma(-q0, 3, x), RN(1/3), q0) of q0 = RN(x RN(1/3)))
  * Usage: exact_arith <mode> ; prints "ok <count>" or the first counter-example.  Test infra. */
 #include <math.h>
 #include <stdint.h>
@@ -82,6 +85,14 @@ static int check_wide(int64_t a, int64_t r) {
     if (fraction_w(A, R, y) != w) { printf("FRACW a=%lld r=%lld\n", (long long)a, (long long)r); return 1; }
     return 0;
 }
+static double div_count(double x, uint32_t c) {
+    const double y3 = 0x1.5555555555555p-2; /* RN(1/3) */
+    const double q0 = x * y3;
+    const double r = fma(-q0, 3.0, x);
+    const double q3 = fma(r, y3, q0);
+    return c == 4u ? x * 0.25 : q3;
+}
+static uint64_t rbits(void);
 int main(int argc, char **argv) {
     int mode = argc > 1 ? atoi(argv[1]) : 0;
     if (mode == 0) { /* exhaustive over every allocatable value of spec/synth.md (cpu m, memory MiB) */
@@ -127,6 +138,30 @@ int main(int argc, char **argv) {
             if (r < 0) r = 0;
             if (check_wide(a, r)) return 1;
         }
+    } else if (mode == 5) { /* div_count: random doubles over every binade of [2^-60, 4), the sums and
+                               squared deviations of fractions of small integers, neighbours of
+                               multiples of 1/3, and all-ones significands */
+        for (long k = 0; k < 40000000; k++) {
+            double x;
+            switch (k % 5) {
+                case 0: { int e = -60 + (int)(rnd() % 62); x = ldexp(1.0 + (double)(rbits() >> 12) * 0x1p-52, e); break; }
+                case 1: { double a = (double)(1 + rnd() % 1000), b = (double)(1 + rnd() % 1000);
+                          x = (double)(rnd() % 1001) / a + (double)(rnd() % 1001) / b + (double)(rnd() % 1001) / 997.0; break; }
+                case 2: { double m = (double)(rnd() % 4000) / 1000.0; x = nextafter(m / 3.0 * 3.0, (k & 8) ? 4.0 : 0.0); break; }
+                case 3: { int e = -40 + (int)(rnd() % 42); x = ldexp(2.0 - 0x1p-52, e); break; }
+                default: { double f0 = (double)(rnd() % 100001) / 100000.0, f1 = (double)(rnd() % 100001) / 100000.0;
+                           double f2 = (double)(rnd() % 100001) / 100000.0; double mu = (f0 + f1 + f2) / 3.0;
+                           x = (f0 - mu) * (f0 - mu) + (f1 - mu) * (f1 - mu) + (f2 - mu) * (f2 - mu); break; }
+            }
+            if (!(x < 4.0)) x = fmod(x, 4.0);
+            for (uint32_t c = 3; c <= 4; c++) {
+                checks++;
+                volatile double want = x / (double)c;
+                if (div_count(x, c) != want) { printf("DIVC x=%a c=%u got %a want %a\n", x, c, div_count(x, c), want); return 1; }
+            }
+        }
+        checks += 2;
+        if (div_count(0.0, 3) != 0.0 || div_count(0.0, 4) != 0.0) { printf("DIVC zero\n"); return 1; }
     } else { /* small divisors (weight sums, normalize maxima): n/d <= 100 exhaustive */
         for (uint32_t d = 1; d <= 131070; d += (d < 2048 ? 1 : 97)) {
             double y = 1.0 / (double)d;
@@ -139,3 +174,4 @@ int main(int argc, char **argv) {
     printf("ok %lld\n", checks);
     return 0;
 }
+static uint64_t rbits(void) { return ((uint64_t)rnd() << 32) ^ (uint64_t)rnd(); }

@@ -8,8 +8,9 @@ over the whole compacted range [1, 2^24); and the scan kernel's reciprocal RN(1/
 two f64 Newton steps) exhaustively over [1, 2^24) for every estimate within 2 f32 ulps.  Mode 4: the
 wide layout's LeastAllocated (f64 quotient + one fma-exact integer correction) and Markstein
 BalancedAllocation quotient on 12M pairs over every binade up to 2^46 bytes (all-ones significands,
-requests near the allocatable and near multiples of a / 100).  The GPU parity tests then confirm the
-device agrees.
+requests near the allocatable and near multiples of a / 100).  Mode 5: BalancedAllocation's division
+by the resource count (3 or 4) on 80M cases (scaling by 1/4; Markstein's correction with RN(1/3)).
+The GPU parity tests then confirm the device agrees.
 """
 import os
 import subprocess
@@ -27,7 +28,7 @@ def exe(tmp_path_factory):
     return out
 
 
-@pytest.mark.parametrize("mode", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3, 4, 5])
 def test_division_formulas_exact(exe, mode):
     r = subprocess.run([exe, str(mode)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout

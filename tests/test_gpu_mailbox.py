@@ -15,13 +15,16 @@ pytestmark = pytest.mark.gpu
 CFG4 = dict(enable_taint=1, enable_affinity=1)
 
 
-def _rank(rank, world, qin, qout, cfg, config, n, p, resident="1", delay=0.0, wide=False, skew=False):
+def _rank(rank, world, qin, qout, cfg, config, n, p, resident="1", delay=0.0, wide=False, skew=False,
+          host_mbox=False):
     import sys
     import os
     import time
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [root, os.path.join(root, "custom-k8s-scheduler_amd")]
     os.environ["QS_RESIDENT"] = resident
+    if host_mbox:  # the mailboxes in POSIX shared host memory (qs_dist_mailbox_export, QS_MBOX_HOST)
+        os.environ["QS_MBOX_HOST"] = "1"
     if skew and rank == 1:  # this rank's selectors of windows 40-43 run 3 ms late (mid-stream drift)
         os.environ["QS_INJECT_FAULT"] = "resident_skew"
     import qsched
@@ -60,13 +63,14 @@ def make_cluster(qsched, config, n, p, wide=False):
     return nodes, pods
 
 
-def run_world(world, cfg, config, n, p, resident="1", delay=0.0, wide=False, skew=False):
+def run_world(world, cfg, config, n, p, resident="1", delay=0.0, wide=False, skew=False, host_mbox=False):
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     qout = ctx.Queue()
     qins = [ctx.Queue() for _ in range(world)]
-    procs = [ctx.Process(target=_rank, args=(r, world, qins[r], qout, cfg, config, n, p, resident, delay, wide, skew))
+    procs = [ctx.Process(target=_rank, args=(r, world, qins[r], qout, cfg, config, n, p, resident, delay, wide, skew,
+                                             host_mbox))
              for r in range(world)]
     for pr in procs:
         pr.start()
@@ -123,6 +127,32 @@ def test_mailbox_world2_two_processes(oracle, cfg, config, n, p, resident, delay
         pl, keys, final, eng, res_flag = res[rank]
         assert eng == "lookahead"
         assert res_flag == (1 if resident == "1" else 0), rank
+        bad = np.nonzero(pl != o_pl)[0]
+        assert bad.size == 0, f"rank {rank}: {bad.size} placements differ, first at pod {bad[0]}"
+        assert np.array_equal(keys, o_keys), rank
+        for k in on:
+            assert np.array_equal(final[k], on[k]), (rank, k)
+
+
+@pytest.mark.parametrize("cfg,config,n,p,resident",
+                         [({}, 2, 2000, 4000, "1"), ({}, 2, 2000, 3000, "0"), (CFG4, 4, 1500, 3000, "1")],
+                         ids=["config2-resident", "config2-per-window", "config4-resident"])
+def test_mailbox_world2_host_memory(oracle, cfg, config, n, p, resident):
+    """the same world-2 exchange with every rank's mailbox in coherent host memory
+    (POSIX shared memory registered with HIP, QS_MBOX_HOST=1): the lists, partial maxima, flags and
+    hello words cross the host link, so the system-scope payload -> fence -> flag ordering is
+    exercised without the two ranks sharing the GPU's L2 for them (the one-GPU stand-in for two
+    devices).  Both ranks must return the oracle's placements, keys and final table."""
+    from qsched import pods_from_struct
+    import qsched
+
+    res = run_world(2, cfg, config, n, p, resident, host_mbox=True)
+    nodes, pods = make_cluster(qsched, config, n, p)
+    on = {k: v.copy() for k, v in nodes.items()}
+    o_pl, o_keys, _ = oracle.schedule(on, pods_from_struct(pods), cfg, nthreads=16)
+    for rank in range(2):
+        pl, keys, final, eng, res_flag = res[rank]
+        assert eng == "lookahead" and res_flag == (1 if resident == "1" else 0), rank
         bad = np.nonzero(pl != o_pl)[0]
         assert bad.size == 0, f"rank {rank}: {bad.size} placements differ, first at pod {bad[0]}"
         assert np.array_equal(keys, o_keys), rank

@@ -7,6 +7,8 @@
 //   fw_latency [nodes] [pods] [outputs: 1 all arrays, 0 best only, 2 packed words read in place]
 //   ->  one JSON line.  Mode 2 is qs_score_pod_packed plus one pass over the n words (the per-node
 //   Filter / Score lookups a plugin makes: here a count of the feasible nodes).
+#include <sys/resource.h>
+
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -57,7 +59,11 @@ int main(int argc, char **argv) {
     if (qs_nodes_load(ctx, &in, n) != QS_OK) return 4;
     std::vector<uint8_t> feas(n);
     std::vector<int32_t> scores(4 * (size_t)n), total(n), placement(p);
-    std::vector<double> lat(p);
+    std::vector<double> lat(p), lat_score(p);
+    // per call: involuntary / voluntary context switches and minor page faults of this thread
+    // (getrusage RUSAGE_THREAD around the call), to tell an OS preemption or a first-touch fault
+    // from a device-side stall in the slowest calls (one 3.58 ms call in 5,000)
+    std::vector<long> ivcsw(p), vcsw(p), minflt(p);
     using clk = std::chrono::steady_clock;
     // warm-up (module load, first-touch of the pinned output pages): score-only calls, which leave
     // the table unchanged; a plugin process pays this once, not per pod
@@ -68,6 +74,8 @@ int main(int argc, char **argv) {
             return 5;
     }
     for (uint32_t j = 0; j < p; ++j) {
+        rusage ru0, ru1;
+        getrusage(RUSAGE_THREAD, &ru0);
         const auto t0 = clk::now();
         int32_t best = -2;
         if (score(&pods[j], &best, outputs ? feas.data() : nullptr, outputs ? scores.data() : nullptr,
@@ -75,11 +83,16 @@ int main(int argc, char **argv) {
             std::fprintf(stderr, "qs_score_pod: %s\n", qs_last_error(ctx));
             return 5;
         }
+        lat_score[j] = std::chrono::duration<double, std::micro>(clk::now() - t0).count();
         if (best >= 0 && qs_reserve(ctx, (uint32_t)best, &pods[j]) != QS_OK) {
             std::fprintf(stderr, "qs_reserve: %s\n", qs_last_error(ctx));
             return 6;
         }
         lat[j] = std::chrono::duration<double, std::micro>(clk::now() - t0).count();
+        getrusage(RUSAGE_THREAD, &ru1);
+        ivcsw[j] = ru1.ru_nivcsw - ru0.ru_nivcsw;
+        vcsw[j] = ru1.ru_nvcsw - ru0.ru_nvcsw;
+        minflt[j] = ru1.ru_minflt - ru0.ru_minflt;
         placement[j] = best;
     }
     qs_close(ctx);
@@ -110,10 +123,25 @@ int main(int argc, char **argv) {
     auto pct = [&](double q) { return s[std::min(s.size() - 1, (size_t)(q * (double)(s.size() - 1) + 0.5))]; };
     double sum = 0;
     for (double v : lat) sum += v;
+    // the five slowest calls, with their split and the OS events inside them
+    std::vector<uint32_t> idx(p);
+    for (uint32_t j = 0; j < p; ++j) idx[j] = j;
+    std::sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) { return lat[a] > lat[b]; });
+    long preempted = 0, switched = 0;
+    for (uint32_t j = 0; j < p; ++j) { preempted += ivcsw[j] > 0; switched += vcsw[j] > 0; }
+    char slow[1024];
+    int off = 0;
+    for (uint32_t k = 0; k < std::min<uint32_t>(5, p); ++k) {
+        const uint32_t j = idx[k];
+        off += std::snprintf(slow + off, sizeof slow - off,
+                             "%s{\"call\": %u, \"us\": %.2f, \"score_us\": %.2f, \"ivcsw\": %ld, \"vcsw\": %ld, \"minflt\": %ld}",
+                             k ? ", " : "", j, lat[j], lat_score[j], ivcsw[j], vcsw[j], minflt[j]);
+    }
     std::printf("{\"nodes\": %u, \"pods\": %u, \"outputs\": %s, \"p50_us\": %.2f, \"p99_us\": %.2f, \"mean_us\": %.2f, "
-                "\"max_us\": %.2f, \"pods_per_s\": %.1f, \"placements_match\": %s}\n",
+                "\"max_us\": %.2f, \"pods_per_s\": %.1f, \"placements_match\": %s, \"calls_preempted\": %ld, "
+                "\"calls_with_voluntary_switch\": %ld, \"slowest\": [%s]}\n",
                 n, p, mode == 1 ? "\"feasible+scores+totals\"" : mode == 2 ? "\"packed words read in place\"" : "\"best only\"",
                 pct(0.5), pct(0.99), sum / p, s.back(),
-                p / (sum * 1e-6), match ? "true" : "false");
+                p / (sum * 1e-6), match ? "true" : "false", preempted, switched, slow);
     return match ? 0 : 1;
 }
