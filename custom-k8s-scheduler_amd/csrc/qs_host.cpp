@@ -1229,6 +1229,10 @@ static const uint32_t *score_pod_launch(qs_ctx *c, const qs_pod *pod, uint32_t w
     const uint32_t pidx = c->pend < n ? c->pend : 0xFFFFFFFFu;
     const HostRow prow = pidx < n ? compact_row(c->m, pidx, c->shift, c->wide) : HostRow{};
     const uint64_t seq = ++c->score_seq;
+    // QS_SCORE_DIAG=1: calls slower than 500 us report their launch / wait split on stderr (the
+    // framework path's tail)
+    static const bool sdiag = getenv("QS_SCORE_DIAG") && getenv("QS_SCORE_DIAG")[0] == '1';
+    const auto tl = std::chrono::steady_clock::now();
     HIPCHK(launch_score_pod1(c->dt, dp, &dx, dc, static_cast<uint8_t *>(c->pin), c->score_gs.as<uint64_t>(), seq,
                              pidx, prow, c->stream));
     c->pend = 0xFFFFFFFFu;
@@ -1241,6 +1245,13 @@ static const uint32_t *score_pod_launch(qs_ctx *c, const qs_pod *pod, uint32_t w
             if (*done != seq) fail(QS_EDEVICE, "qs_score_pod: the scoring kernel did not complete");
             break;
         }
+    }
+    if (sdiag) {
+        const auto te = std::chrono::steady_clock::now();
+        const double lu = std::chrono::duration<double, std::micro>(t0 - tl).count();
+        const double wu = std::chrono::duration<double, std::micro>(te - t0).count();
+        if (lu + wu > 500.0) std::fprintf(stderr, "QS_SCORE_DIAG call %llu: launch %.1f us, wait %.1f us\n",
+                                          (unsigned long long)seq, lu, wu);
     }
     std::atomic_thread_fence(std::memory_order_acquire);
     const uint8_t *h = static_cast<const uint8_t *>(c->pin);

@@ -1,0 +1,16 @@
+#!/bin/bash
+# Round-6 evidence after tools/gpu_full.sh: framework-path latency (tools/fw_latency, with the slow
+# calls' launch / wait split, QS_SCORE_DIAG=1), rocprofv3 kernel stats and PMC passes
+# (profile_fetch.sh).
+cd "${GRAFT_REPO_ROOT:-.}"
+mkdir -p gpurun_out
+TAG=${1:-r06}
+export TMPDIR=/tmp
+( for a in "5000 5000 1" "5000 5000 0" "5000 5000 2" "5000 5000 2" "50000 3000 2" "50000 3000 1"; do
+    QS_SCORE_DIAG=1 timeout -k 10 120 custom-k8s-scheduler_amd/fw_latency $a 2>> gpurun_out/fw_diag_$TAG.txt || exit 7
+  done ) > gpurun_out/fw_latency_$TAG.json || exit 7
+cut -c1-260 gpurun_out/fw_latency_$TAG.json
+cat gpurun_out/fw_diag_$TAG.txt | head -20
+bash tools/profile_fetch.sh $TAG || exit 8
+ls gpurun_out/profiles_new | head -40
+echo ROUNDDONE

@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 rm -rf $OUT; mkdir -p $OUT profiles
 ARGS="--steps 2 --warmup 1 --no-cpu"  # config 3 included: its k_la_stream_res row
-PMC_ARGS="--steps 1 --warmup 1 --no-cpu --no-config3 --no-extra"  # the scan leg too: k_scan_soa traffic
+PMC_ARGS="--steps 1 --warmup 1 --no-cpu --no-extra"  # the scan leg too; configs 3, 4, 4-gpu-scoring and 5
 # heartbeat for the GPU pool's silence watchdog (counter passes print nothing for minutes)
 ( while sleep 45; do date >> $OUT/heartbeat; done ) &
 HB=$!
