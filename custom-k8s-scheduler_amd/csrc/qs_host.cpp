@@ -1184,7 +1184,21 @@ static void unpack_scores(const uint32_t *pk, uint32_t n, const uint32_t w[4], u
 // the previous Reserve's row folded in, outputs written by the kernel into pinned host memory,
 // completion seen by polling its done word (no copy command, no stream sync).  Returns the packed
 // per-node words (valid until the next call on the context); *wts = {wfit, wbal, wtt, wna}.
+// QS_SCORE_DIAG=1: a qs_score_pod call slower than 500 us reports its host prep / launch / done-word
+// wait / unpack split on stderr (the framework path's tail)
+static const bool g_sdiag = getenv("QS_SCORE_DIAG") && getenv("QS_SCORE_DIAG")[0] == '1';
+struct ScoreSplit { std::chrono::steady_clock::time_point ts, tl, t0, te; };
+static thread_local ScoreSplit g_split;
+static void score_diag_report(uint64_t seq, std::chrono::steady_clock::time_point tu) {
+    auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+    const ScoreSplit &s = g_split;
+    if (us(s.ts, tu) > 500.0)
+        std::fprintf(stderr, "QS_SCORE_DIAG call %llu: prep %.1f us, launch %.1f us, wait %.1f us, unpack %.1f us\n",
+                     (unsigned long long)seq, us(s.ts, s.tl), us(s.tl, s.t0), us(s.t0, s.te), us(s.te, tu));
+}
+
 static const uint32_t *score_pod_launch(qs_ctx *c, const qs_pod *pod, uint32_t wts[4], int32_t *best) {
+    if (g_sdiag) g_split.ts = std::chrono::steady_clock::now();
     if (!pod) fail(QS_EINVAL, "null pod");
     HIPCHK(hipSetDevice(c->device));
     check_pod(*pod, 0);
@@ -1229,9 +1243,6 @@ static const uint32_t *score_pod_launch(qs_ctx *c, const qs_pod *pod, uint32_t w
     const uint32_t pidx = c->pend < n ? c->pend : 0xFFFFFFFFu;
     const HostRow prow = pidx < n ? compact_row(c->m, pidx, c->shift, c->wide) : HostRow{};
     const uint64_t seq = ++c->score_seq;
-    // QS_SCORE_DIAG=1: calls slower than 500 us report their launch / wait split on stderr (the
-    // framework path's tail)
-    static const bool sdiag = getenv("QS_SCORE_DIAG") && getenv("QS_SCORE_DIAG")[0] == '1';
     const auto tl = std::chrono::steady_clock::now();
     HIPCHK(launch_score_pod1(c->dt, dp, &dx, dc, static_cast<uint8_t *>(c->pin), c->score_gs.as<uint64_t>(), seq,
                              pidx, prow, c->stream));
@@ -1246,12 +1257,10 @@ static const uint32_t *score_pod_launch(qs_ctx *c, const qs_pod *pod, uint32_t w
             break;
         }
     }
-    if (sdiag) {
-        const auto te = std::chrono::steady_clock::now();
-        const double lu = std::chrono::duration<double, std::micro>(t0 - tl).count();
-        const double wu = std::chrono::duration<double, std::micro>(te - t0).count();
-        if (lu + wu > 500.0) std::fprintf(stderr, "QS_SCORE_DIAG call %llu: launch %.1f us, wait %.1f us\n",
-                                          (unsigned long long)seq, lu, wu);
+    if (g_sdiag) {
+        g_split.tl = tl;
+        g_split.t0 = t0;
+        g_split.te = std::chrono::steady_clock::now();
     }
     std::atomic_thread_fence(std::memory_order_acquire);
     const uint8_t *h = static_cast<const uint8_t *>(c->pin);
@@ -1267,6 +1276,7 @@ qs_status qs_score_pod(qs_ctx *c, const qs_pod *pod, uint8_t *feas, int32_t *sco
         uint32_t w[4];
         const uint32_t *pk = score_pod_launch(c, pod, w, best);
         if (pk) unpack_scores(pk, c->m.n, w, feas, score, total);
+        if (g_sdiag && pk) score_diag_report(c->score_seq, std::chrono::steady_clock::now());
     }, /*keep_pending=*/true);
 }
 
@@ -1275,6 +1285,7 @@ qs_status qs_score_pod_packed(qs_ctx *c, const qs_pod *pod, const uint32_t **pac
         uint32_t w[4];
         const uint32_t *pk = score_pod_launch(c, pod, w, best);
         if (packed) *packed = pk;
+        if (g_sdiag && pk) score_diag_report(c->score_seq, std::chrono::steady_clock::now());
     }, /*keep_pending=*/true);
 }
 

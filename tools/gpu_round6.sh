@@ -11,6 +11,14 @@ export TMPDIR=/tmp
   done ) > gpurun_out/fw_latency_$TAG.json || exit 7
 cut -c1-260 gpurun_out/fw_latency_$TAG.json
 cat gpurun_out/fw_diag_$TAG.txt | head -20
+# the diagnostic build's busy cycles and step marks
+if [ -f custom-k8s-scheduler_amd/libqsched_diag.so ]; then
+  for l in config2 config4; do
+    QSCHED_LIB=$PWD/custom-k8s-scheduler_amd/libqsched_diag.so QS_RES_DIAG=1 timeout -k 10 200 python -u bench.py --leg $l --no-cpu > gpurun_out/diag_$l.json 2> gpurun_out/diag_$l.err || exit 9
+    grep -a "busy cycles\|step marks" gpurun_out/diag_$l.err | sort | uniq > gpurun_out/diag_${TAG}_$l.txt
+    cat gpurun_out/diag_${TAG}_$l.txt
+  done
+fi
 bash tools/profile_fetch.sh $TAG || exit 8
 ls gpurun_out/profiles_new | head -40
 echo ROUNDDONE

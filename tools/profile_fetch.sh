@@ -14,5 +14,6 @@ for c in 4 5; do
     tail -3 gpurun_out/prof_$TAG/cfg$c.log > gpurun_out/profiles_new/cfg$c.tail 2>/dev/null
 done
 tail -3 gpurun_out/prof_$TAG/trace.log > gpurun_out/profiles_new/trace.tail 2>/dev/null
+cat gpurun_out/prof_$TAG/*.err > gpurun_out/profiles_new/pmc_errors.txt 2>/dev/null
 rm -rf gpurun_out/prof_$TAG
 exit $rc
