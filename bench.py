@@ -824,9 +824,17 @@ def main():
         # one rank per GPU; this parent never touches the GPU (no exec after GPU init)
         import subprocess
         return subprocess.run(plan["argv"]).returncode
+    # stdout carries the JSON line alone: native libraries' banners (RCCL prints its version lines
+    # on stdout at communicator init) and any other print go to stderr
+    real_out = sys.stdout
+    if real_out is sys.__stdout__:  # the process's fd 1: kept for the JSON line, fd 1 -> stderr
+        sys.stdout.flush()
+        real_out = os.fdopen(os.dup(1), "w")
+        os.dup2(2, 1)
+    emit = lambda obj: print(json.dumps(obj), file=real_out, flush=True)
     cx = Ctx()
     if a.leg:
-        print(json.dumps(run_leg(cx, a, a.leg)), flush=True)
+        emit(run_leg(cx, a, a.leg))
         return 0
     workload = a.workload if a.workload != "auto" else ("config2" if cx.world == 1 else "config3")
     progress(f"{workload}: timed stream ({a.steps} steps, {a.warmup} warmup)")
@@ -956,7 +964,7 @@ def main():
                     "skipped": "this process may use 16 CPUs (affinity / cgroup quota / OMP_NUM_THREADS): "
                                "the nproc arm is cpu_baseline_parallel", "host": host_info()}
             out["cpu_baseline_framework"] = cpu_baseline_framework()
-        print(json.dumps(out), flush=True)
+        emit(out)
     if cx.dist is not None:
         cx.dist.destroy_process_group()
     return 0
