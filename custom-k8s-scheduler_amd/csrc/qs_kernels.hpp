@@ -2645,7 +2645,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
     uint32_t(*stS)[64] = (uint32_t(*)[64])base; base += 2 * 64 * 4;
     uint32_t(*nflag2)[kResNormK] = (uint32_t(*)[kResNormK])base; base += 2 * kResNormK * 4;
     // NORM: the taint / label masks of the current slots by slot lane (waves A / B carry only a
-    // slot's extended resources: the masks are written by wave 6 when a slot is created, by wave A
+    // slot's extended resources: the masks are written by wave 4 when a slot is created, by wave A
     // at a window boundary for the inherited ones, and read by rescans and the boundary)
     DMask *smask = (DMask *)base;
     // RING (Fit + Balanced (+ext); the NORM arrays above are not allocated then, so the rings start
@@ -3423,9 +3423,10 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
     } else if constexpr (NORM) {
         // ---- waves 4-7: slot statics, the rescans' extra hands, the next window's pod records ------
         // Per step (work(i), before the step's barrier; a STOP's rescan of pod i-1 already done):
-        //  wave 6: a slot created by pod i-1's winner: its static against this window's pods from
+        //  wave 4: a slot created by pod i-1's winner: its static against this window's pods from
         //          i+2 on (Tcur; waves A/B take pod i+1's from stS) and against the next window's
-        //          pods (Tnext);
+        //          pods (Tnext) — on wave D's SIMD, the least busy pipeline wave's (round 6: from
+        //          wave 6, which shares wave B's: config 4 147.0 -> 145.1 ms);
         //  wave 7: one share of the inherited slots' statics against the next window's pods (Tnext);
         //  step 0: the next window's pod extension records and flags into LDS.
         // Between B2 and B3, Tnext is rank-compacted into Tcur for the next window's inherited slots.
@@ -3445,12 +3446,12 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
             if (h1) q1 = src[id1];
             uint32_t nfl = 0;
             if (pw == 0 && (uint32_t)lane < knext) nfl = pods[s0 + K + lane].flags;
-            // Waves 6 and 7 keep one pod's extension record and flags per lane in registers for the
-            // window (read from LDS once, at step 1): wave 6 lanes 0-31 this window's pod `lane`,
+            // Waves 4 and 7 keep one pod's extension record and flags per lane in registers for the
+            // window (read from LDS once, at step 1): wave 4 lanes 0-31 this window's pod `lane`,
             // lanes 32-63 and every wave-7 lane the next window's pod `lane & 31`.  Reading a record
             // per lane and step from LDS held the pipeline waves' reads up by ~850 cycles a step.
             const uint32_t qq = (uint32_t)lane & 31u;
-            const bool mycur = wv == 6 && lane < 32;
+            const bool mycur = wv == 4 && lane < 32;
             DPodX myx{};
             uint32_t myf = 0;
             auto load_mine = [&]() {
@@ -3530,9 +3531,9 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                     if (h0) dst[id0] = q0;
                     if (h1) dst[id1] = q1;
                     if (pw == 0 && (uint32_t)lane < knext) nflag2[nb][lane] = nfl;
-                } else if (wv >= 6) {
+                } else if (wv == 4 || wv == 7) {
                     if (i == 1) load_mine();
-                    if (wv == 6) new_slot(i - 1, true);
+                    if (wv == 4) new_slot(i - 1, true);
                     else inherited(i - 1);
                 }
                 __syncthreads();
@@ -3542,8 +3543,8 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                     __syncthreads();  // R5
                 }
             }
-            if (wv >= 6 && kend == 1) load_mine();
-            if (wv == 6) new_slot(kend - 1, false);
+            if ((wv == 4 || wv == 7) && kend == 1) load_mine();
+            if (wv == 4) new_slot(kend - 1, false);
             if (wv == 7)
                 for (uint32_t j = kend - 1; 2 * j < ndi; ++j) inherited(j);  // (short windows: the rest)
             __syncthreads();  // B2 (D's slot ranks)
