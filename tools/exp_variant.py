@@ -33,11 +33,13 @@ def main():
         open(f, "w").write(text[f])
     flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-ffp-contract=off",
              "-Wno-unused-function", "-mllvm", "-amdgpu-atomic-optimizer-strategy=None",
-             f"-I{os.path.join(ROOT, 'include')}"]
+             f"-I{os.path.join(ROOT, 'include')}"] + os.environ.get("EXP_DEFS", "").split()
     obj = os.path.join(dst, "qs_kernels.o")
     subprocess.run(["/opt/rocm/bin/hipcc"] + flags + ["-c", os.path.join(dst, "qs_kernels.hip"), "-o", obj], check=True)
-    others = [os.path.join(PKG, "build", f) for f in ("qs_kernels_wide.o", "qs_kernels_res.o", "qs_kernels_res_wide.o",
-                                                      "qs_host.o", "qs_helpers.o", "qs_dist.o")]
+    # EXP_DEFS="-DQS_RES_DIAG_BLOCK" EXP_OBJS=build_diag: a diagnostic variant (tools/diag_build.sh objects)
+    objs = os.environ.get("EXP_OBJS", "build")
+    others = [os.path.join(PKG, objs, f) for f in ("qs_kernels_wide.o", "qs_kernels_res.o", "qs_kernels_res_wide.o",
+                                                   "qs_host.o", "qs_helpers.o", "qs_dist.o")]
     out = os.path.join(PKG, f"libqsched_{name}.so")
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out, obj] + others +
                    ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"], check=True)
