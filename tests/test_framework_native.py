@@ -33,7 +33,7 @@ def test_framework_host_logic_sanitized():
     """The same host checks built with -fsanitize=address,undefined (SURVEY §5 host sanitizers):
     quantity parsing, interning, pod requests, QoSSort and FitError text run clean."""
     root = os.path.join(os.path.dirname(HERE), "custom-k8s-scheduler_amd")
-    b = subprocess.run(["make", "-C", root, "asan"], capture_output=True, text=True, timeout=600)
+    b = subprocess.run(["make", "-C", root, "asan"], capture_output=True, text=True, timeout=1500)  # (a cold ASan build of the host library takes minutes)
     assert b.returncode == 0, b.stdout[-2000:] + b.stderr[-2000:]
     exe = os.path.join(root, "build", "test_framework_asan")
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1",
