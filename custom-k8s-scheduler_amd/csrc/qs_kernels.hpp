@@ -2457,8 +2457,9 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
 // compacted in place through LDS (rows stay on chip), dropped slots' dirty bits are cleared, wave D
 // loads window w+1's pod records at the start of window w, and wave C polls window w+1's lists five
 // pods before the end of window w and prefetches the entries of its first three pods and the
-// candidate rows of its first pod.  Wave A stores the rows won in window w write-through and, two
-// pods into window w+1 (long drained by then), signals done = w + 1.
+// candidate rows of its first pod.  Wave A stores the rows won in window w write-through and, at
+// window w+1's first pod (drained there; round 6: from the third pod, so the next selections start
+// two pod steps earlier: configs 2 / 3 / 4 -2 % / -5 % / -1 %), signals done = w + 1.
 // Per window and wave: one prologue barrier, one barrier per pod, two boundary barriers.
 //
 // Normalizing profiles (NORM: TaintToleration / NodeAffinity, config 4): list keys
@@ -2957,7 +2958,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                 keyA[1][lane] = slot_key(S, SX, wp[0], podn(0), NORM ? Tcur[lane] : 0u);
             if (w > 0) bmark(0);
             __syncthreads();  // B1
-            const uint32_t isig = min(2u, kend - 1);
+            const uint32_t isig = 0;  // the step that signals done for the previous window
             PodT<F> pprev = wp[0], pcur = wp[0];  // pods i-1 and i (pod i+1's record is read each step)
             PodN pnx = podn(1);                   // NORM: pod i+1's record at step i
             for (uint32_t i = 0; i < kend; ++i) {
@@ -2978,7 +2979,7 @@ __device__ __forceinline__ void la_resolve4_stream(uint32_t *lds, const DevTable
                 if (i > 0) apply(pv, pp, pprev, s0 + i - 1);
                 QS_RSTAMP_MARK(1)
                 if (wv == 1 && pend && i == isig) {
-                    // the previous window's rows went out write-through a window boundary ago
+                    // the previous window's rows went out write-through at the boundary (B2-B3)
                     drain_stores();
                     if (lane == 0) __hip_atomic_store((gu32 *)&ctl->done, pend, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     pend = 0;
