@@ -38,7 +38,7 @@ def test_framework_host_logic_sanitized():
     exe = os.path.join(root, "build", "test_framework_asan")
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1",
                UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
-    r = subprocess.run([exe, "--cpu"], capture_output=True, text=True, timeout=300, env=env)
+    r = subprocess.run([exe, "--cpu"], capture_output=True, text=True, timeout=900, env=env)  # (≈ 4.5 min under ASan)
     print(r.stdout[-3000:])
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "0 failures" in r.stdout
