@@ -3648,8 +3648,8 @@ static hipError_t la_stream_res_f(const DevTable &t, const void *pods, const DPo
         if constexpr ((F & kFeatNorm) == 0) { if (geo.k32) QS_RESK(EE, 2, true); else QS_RESK(EE, 2, false); } }
     if (false) {
     }
-    QS_RESE(3, 1) QS_RESE(5, 1) QS_RESE(8, 1) QS_RESE(16, 1)
-    QS_RESE2(5) QS_RESE2(8) QS_RESE2(16)
+    QS_RESE(3, 1) QS_RESE(5, 1) QS_RESE(7, 1) QS_RESE(8, 1) QS_RESE(16, 1)
+    QS_RESE2(5) QS_RESE2(7) QS_RESE2(8) QS_RESE2(16)
     else return hipErrorInvalidValue;
 #undef QS_RESE
 #undef QS_RESE2
@@ -3666,13 +3666,13 @@ static int la_stream_res_per_cu(const LaGeom &geo, uint32_t n) {
     const void *fn = nullptr;
 #define QS_RESP(EE, KK) \
     if (geo.E == EE && geo.e2 == 1 && (geo.k32 != 0) == KK) fn = (const void *)k_la_stream_res<F, EE, 1, KK>;
-    QS_RESP(3, true) QS_RESP(3, false) QS_RESP(5, true) QS_RESP(5, false)
+    QS_RESP(3, true) QS_RESP(3, false) QS_RESP(5, true) QS_RESP(5, false) QS_RESP(7, true) QS_RESP(7, false)
     QS_RESP(8, true) QS_RESP(8, false) QS_RESP(16, true) QS_RESP(16, false)
 #undef QS_RESP
     if constexpr ((F & kFeatNorm) == 0) {
 #define QS_RESP2(EE, KK) \
         if (geo.E == EE && geo.e2 == 2 && (geo.k32 != 0) == KK) fn = (const void *)k_la_stream_res<F, EE, 2, KK>;
-        QS_RESP2(5, true) QS_RESP2(5, false) QS_RESP2(8, true) QS_RESP2(8, false) QS_RESP2(16, true) QS_RESP2(16, false)
+        QS_RESP2(5, true) QS_RESP2(5, false) QS_RESP2(7, true) QS_RESP2(7, false) QS_RESP2(8, true) QS_RESP2(8, false) QS_RESP2(16, true) QS_RESP2(16, false)
 #undef QS_RESP2
     }
     int per = 0;
