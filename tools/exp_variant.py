@@ -23,7 +23,7 @@ def main():
         shutil.rmtree(dst)
     shutil.copytree(src, dst)
     # each substitution applies to the first of these headers that holds its `old` text
-    files = [os.path.join(dst, f) for f in ("qs_kernels.hpp", "qs_device.hpp")]
+    files = [os.path.join(dst, f) for f in ("qs_kernels.hpp", "qs_device.hpp", "qs_kernels.hip")]
     text = {f: open(f).read() for f in files}
     for old, new in zip(subs[0::2], subs[1::2]):
         f = next((f for f in files if old in text[f]), None)
