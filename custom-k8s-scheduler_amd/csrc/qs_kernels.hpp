@@ -2160,6 +2160,21 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
     for (uint32_t w = 0; w < nwin; ++w) {
         const uint32_t s0 = w * K, kw = min(K, P - s0), b = w & 1;
         if (sid >= kw * G) continue;  // no task of this window (uniform per block)
+        // large chunks (E = 7, 8; Fit + Balanced: config 3's 50,000 nodes, selector-bound): this workgroup's first
+        // task's pod record is read before the wait for the table (pod records never change during
+        // a stream), so its latency hides behind the wait (config 3 652-657 -> 647 ms; with the small
+        // chunks of config 2, whose selectors wait on the resolver anyway, the same code cost 2 %)
+        static_assert(sizeof(PodT<F>) % 16 == 0, "pod record in 16-byte words");
+        constexpr int PW = (int)(sizeof(PodT<F>) / 16);
+        constexpr bool kPodPre = (F & kFeatNorm) == 0 && E >= 7 && E <= 8;  // (registers: not at 16)
+        u32x4 pq[PW];
+        if constexpr (kPodPre) {
+            const u32x4 *src = reinterpret_cast<const u32x4 *>(pods + s0 + min(sid / G, kw - 1));
+#pragma unroll
+            for (int q = 0; q < PW; ++q) pq[q] = src[q];
+#pragma unroll
+            for (int q = 0; q < PW; ++q) asm volatile("" : "+v"(pq[q]));
+        }
         if (w >= 2) {  // the table after window w-2, and this parity's buffers free again
             if (tid == 0) okflag = res_wait_ge(&ctl->done, w - 1, c.werr) ? 1u : 0u;
             if (rdiag && tid == 0) {  // (the resolver posts each window's start time)
@@ -2182,7 +2197,9 @@ __device__ __forceinline__ void res_selector(const DevTable &t, const PodT<F> *_
             }
             const uint32_t k = task / G, g = task % G;
             if (rdiag && c.sel_diag) ts0 = __builtin_amdgcn_s_memrealtime();
-            const PodT<F> p = pods[s0 + k];
+            PodT<F> p;
+            if (kPodPre && task == sid) __builtin_memcpy(&p, pq, sizeof p);
+            else p = pods[s0 + k];
             const uint32_t start = lo + g * chunk, end = min(hi, start + chunk);
             const uint32_t base = start + (uint32_t)w8 * E * kWave + lane;
             uint32_t tv[E];
